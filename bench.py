@@ -1,0 +1,135 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Llama-3-8B ZeRO-3 bf16 training tokens/sec on N MI355X GPUs of one node.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it is
+started under ``torch.distributed.run`` (one rank per GPU, RCCL over xGMI). W untimed
+warmup optimizer steps, then exactly K timed steps bracketed by a barrier +
+``torch.cuda.synchronize()``; the elapsed time is the MAX over ranks; rank 0 prints
+one JSON line. ``value`` is whole-job tokens/sec (all N GPUs); per-GPU work is fixed
+(weak scaling). Data is synthetic (uniform random token ids), weights random-init of
+the real Llama-3-8B architecture; every step runs the full forward, backward,
+reduce-scatter, clipping and AdamW update.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+METRIC = "tokens/sec (node) Llama-3-8B ZeRO-3"
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--seq", type=int, default=8192)
+    ap.add_argument("--mbs", type=int, default=1, help="micro-batch size per GPU")
+    ap.add_argument("--ga", type=int, default=8, help="gradient accumulation steps (reference default 8)")
+    ap.add_argument("--zero", type=int, default=3)
+    ap.add_argument("--ckpt", action="store_true", help="activation checkpointing (recompute)")
+    ap.add_argument("--profile-steps", type=int, default=0)
+    args = ap.parse_args()
+
+    from distributed_llm_training_gpu_manager_amd.models import get_config
+    from distributed_llm_training_gpu_manager_amd.parallel.comm import Comm, init_distributed
+    from distributed_llm_training_gpu_manager_amd.parallel.zero import EngineConfig, ZeroEngine
+    from distributed_llm_training_gpu_manager_amd import _native
+
+    env = init_distributed("cuda" if torch.cuda.is_available() else "cpu")
+    if env.world != args.gpus and env.rank == 0:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={env.world}", file=sys.stderr)
+    if env.device.type == "cuda":
+        _native.hip_ops()  # fail loudly if the HIP kernels are not built
+    comm = Comm()
+    mcfg = get_config(args.model)
+    ecfg = EngineConfig(zero_stage=args.zero, micro_batch_size=args.mbs, seq_len=args.seq, grad_accum=args.ga,
+                        lr=3e-5, warmup_steps=100, total_steps=10000, grad_clip=1.0,
+                        activation_checkpointing=args.ckpt)
+    t0 = time.time()
+    eng = ZeroEngine(mcfg, ecfg, env.device, comm)
+    if env.device.type == "cuda":
+        torch.cuda.synchronize()
+    init_s = time.time() - t0
+
+    gen = torch.Generator(device=env.device)
+    gen.manual_seed(1000 + env.rank)
+    batches = []
+    for _ in range(args.ga):
+        toks = torch.randint(0, mcfg.vocab_size, (args.mbs, args.seq + 1), device=env.device, generator=gen)
+        batches.append((toks[:, :-1].contiguous(), toks[:, 1:].contiguous()))
+
+    def sync():
+        if env.device.type == "cuda":
+            torch.cuda.synchronize()
+        comm.barrier()
+
+    for _ in range(args.warmup):
+        m = eng.train_step(batches)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        m = eng.train_step(batches)
+    sync()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=env.device)
+    comm.all_reduce_max(t)
+    elapsed = float(t.item())
+
+    tokens_per_step_gpu = args.mbs * args.seq * args.ga
+    total_tokens = tokens_per_step_gpu * env.world * args.steps
+    tps = total_tokens / elapsed
+    flops_tok = mcfg.flops_per_token(args.seq, recompute=args.ckpt)
+    tflops_gpu = tps / env.world * flops_tok / 1e12
+    loss = float(m["loss"])
+    if env.rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(tps, 2),
+            "unit": "tokens/s",
+            "n_gpus": env.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1000, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (uniform random token ids; random-init weights)",
+            "config": {
+                "model": mcfg.name,
+                "global_batch": args.mbs * args.ga * env.world,
+                "micro_batch_per_gpu": args.mbs,
+                "grad_accum": args.ga,
+                "seq_len": args.seq,
+                "parallelism": f"zero{args.zero}-dp{env.world}",
+                "activation_checkpointing": args.ckpt,
+            },
+            "extra": {
+                "tokens_per_sec_per_gpu": round(tps / env.world, 2),
+                "model_tflops_per_gpu": round(tflops_gpu, 1),
+                "mfu_vs_2.5PF_dense_bf16": round(tflops_gpu / 2500.0, 4),
+                "final_loss": round(loss, 4),
+                "init_s": round(init_s, 1),
+                "params": eng.num_params(),
+                "mem": {k: round(v, 1) for k, v in eng.memory_report().items()},
+            },
+        }
+        print(json.dumps(out), flush=True)
+    if torch.distributed.is_initialized():
+        torch.distributed.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

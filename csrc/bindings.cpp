@@ -1,0 +1,72 @@
+// Operator registry for the MI355X-native kernels: torch.ops.dlgm.*
+//
+// Registered with TORCH_LIBRARY so the ops are dispatcher-visible (usable
+// from Python, capturable in HIP graphs, and loaded by torch.ops.load_library
+// from the in-tree shared object -- never a pip-installed extension).
+// Only the CUDA (= HIP on ROCm) dispatch key is implemented: CPU tensors take the
+// plain PyTorch reference path in the Python wrappers, GPU tensors must hit
+// these kernels.
+#include <torch/library.h>
+#include <torch/all.h>
+
+// rmsnorm.hip
+std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_rmsnorm_fwd(const at::Tensor& x,
+                                                                const c10::optional<at::Tensor>& residual,
+                                                                const at::Tensor& w, double eps);
+at::Tensor dlgm_rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at::Tensor& w, const at::Tensor& rstd,
+                            const c10::optional<at::Tensor>& dres, at::Tensor dw, bool accumulate_dw);
+// rope.hip
+void dlgm_rope_(at::Tensor qkv, const at::Tensor& cos_t, const at::Tensor& sin_t,
+                const c10::optional<at::Tensor>& pos_ids, int64_t n_rope_heads, int64_t head_dim, int64_t seq_len,
+                bool inverse);
+// swiglu.hip
+at::Tensor dlgm_swiglu_fwd(const at::Tensor& gu);
+at::Tensor dlgm_swiglu_bwd(const at::Tensor& dy, const at::Tensor& gu);
+// cross_entropy.hip
+std::tuple<at::Tensor, at::Tensor> dlgm_cross_entropy_(at::Tensor logits, const at::Tensor& labels,
+                                                       int64_t ignore_index, double grad_scale, bool compute_grad);
+// optim.hip
+void dlgm_grad_stats(at::TensorList grads, at::Tensor out, bool accumulate);
+void dlgm_adamw_step_(at::Tensor p, at::Tensor m, at::Tensor v, const at::Tensor& g,
+                      const c10::optional<at::Tensor>& p16, const c10::optional<at::Tensor>& stats, double lr,
+                      double beta1, double beta2, double eps, double weight_decay, double bc1, double bc2,
+                      double grad_scale, double max_norm);
+void dlgm_accumulate_(at::Tensor dst, const at::Tensor& src, double alpha, double beta);
+void dlgm_cast_f32_bf16_(at::Tensor dst, const at::Tensor& src);
+// flash_attn.hip
+std::tuple<at::Tensor, at::Tensor> dlgm_flash_attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                                       double softmax_scale, bool causal);
+std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Tensor& dout, const at::Tensor& q,
+                                                                   const at::Tensor& k, const at::Tensor& v,
+                                                                   const at::Tensor& out, const at::Tensor& lse,
+                                                                   double softmax_scale, bool causal);
+
+TORCH_LIBRARY(dlgm, m) {
+  m.def("rmsnorm_fwd(Tensor x, Tensor? residual, Tensor w, float eps) -> (Tensor, Tensor, Tensor)");
+  m.def("rmsnorm_bwd(Tensor dy, Tensor h, Tensor w, Tensor rstd, Tensor? dres, Tensor(a!) dw, bool accumulate_dw) -> Tensor");
+  m.def("rope_(Tensor(a!) qkv, Tensor cos, Tensor sin, Tensor? pos_ids, int n_rope_heads, int head_dim, int seq_len, bool inverse) -> ()");
+  m.def("swiglu_fwd(Tensor gu) -> Tensor");
+  m.def("swiglu_bwd(Tensor dy, Tensor gu) -> Tensor");
+  m.def("cross_entropy_(Tensor(a!) logits, Tensor labels, int ignore_index, float grad_scale, bool compute_grad) -> (Tensor, Tensor)");
+  m.def("grad_stats(Tensor[] grads, Tensor(a!) out, bool accumulate) -> ()");
+  m.def("adamw_step_(Tensor(a!) p, Tensor(b!) m, Tensor(c!) v, Tensor g, Tensor(d!)? p16, Tensor? stats, float lr, float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2, float grad_scale, float max_norm) -> ()");
+  m.def("accumulate_(Tensor(a!) dst, Tensor src, float alpha, float beta) -> ()");
+  m.def("cast_f32_bf16_(Tensor(a!) dst, Tensor src) -> ()");
+  m.def("flash_attn_fwd(Tensor q, Tensor k, Tensor v, float softmax_scale, bool causal) -> (Tensor, Tensor)");
+  m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, float softmax_scale, bool causal) -> (Tensor, Tensor, Tensor)");
+}
+
+TORCH_LIBRARY_IMPL(dlgm, CUDA, m) {
+  m.impl("rmsnorm_fwd", &dlgm_rmsnorm_fwd);
+  m.impl("rmsnorm_bwd", &dlgm_rmsnorm_bwd);
+  m.impl("rope_", &dlgm_rope_);
+  m.impl("swiglu_fwd", &dlgm_swiglu_fwd);
+  m.impl("swiglu_bwd", &dlgm_swiglu_bwd);
+  m.impl("cross_entropy_", &dlgm_cross_entropy_);
+  m.impl("grad_stats", &dlgm_grad_stats);
+  m.impl("adamw_step_", &dlgm_adamw_step_);
+  m.impl("accumulate_", &dlgm_accumulate_);
+  m.impl("cast_f32_bf16_", &dlgm_cast_f32_bf16_);
+  m.impl("flash_attn_fwd", &dlgm_flash_attn_fwd);
+  m.impl("flash_attn_bwd", &dlgm_flash_attn_bwd);
+}

@@ -1,0 +1,291 @@
+// Flat-buffer optimizer kernels for the ZeRO engine (gfx950).
+//
+// The ZeRO engine keeps every rank's optimizer partition (fp32 master, exp_avg,
+// exp_avg_sq, fp32 grad) as ONE contiguous buffer each, so the whole update is
+// a single launch instead of DeepSpeed's multi_tensor_apply chunk lists
+// (§2.6 K1, K2, K8):
+//   * grad_stats   : sum(g^2) and count(!isfinite(g)) in one pass (two tiny
+//                    deterministic launches: per-block partials, then a final sum).
+//                    Feeds gradient clipping, the fp16 loss scaler and the NaN trap.
+//   * adamw_step   : decoupled-weight-decay Adam; reads the clip coefficient and
+//                    the overflow flag from the device stats buffer, so a step has
+//                    NO host synchronisation; writes the bf16 compute copy of the
+//                    parameter in the same pass (the all-gather source under ZeRO-3).
+//   * accumulate   : dst(fp32) = beta*dst + alpha*src(bf16|fp32) -- gradient
+//                    accumulation of a bf16 micro-batch grad into the fp32 shard.
+//   * cast_f32_bf16: master -> compute copy (after load / init).
+// All are HBM-streaming: float4 / bf16x8 per lane, grid capped at 16 blocks/CU.
+#include <torch/all.h>
+#include <c10/hip/HIPStream.h>
+#include "dlgm_common.h"
+
+using namespace dlgm;
+
+namespace {
+
+constexpr int kThreads = 256;
+
+int64_t stream_grid(int64_t n_vec) {
+  int64_t b = (n_vec + kThreads - 1) / kThreads;
+  return std::max<int64_t>(1, std::min<int64_t>(b, 256 * 8));
+}
+
+template <typename T>
+__device__ __forceinline__ void load4(const T* p, float (&o)[4]);
+template <>
+__device__ __forceinline__ void load4<float>(const float* p, float (&o)[4]) {
+  f32x4 v = *reinterpret_cast<const f32x4*>(p);
+  o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; o[3] = v[3];
+}
+template <>
+__device__ __forceinline__ void load4<bf16>(const bf16* p, float (&o)[4]) {
+  bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
+  o[0] = (float)v[0]; o[1] = (float)v[1]; o[2] = (float)v[2]; o[3] = (float)v[3];
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void grad_stats_partial_kernel(const T* __restrict__ g, int64_t n,
+                                                                      float2* __restrict__ part) {
+  __shared__ float red[kThreads / 64];
+  float ss = 0.f, bad = 0.f;
+  const int64_t nv = n >> 2;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kThreads) {
+    float v[4];
+    load4<T>(g + i * 4, v);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool fin = __builtin_isfinite(v[j]);
+      bad += fin ? 0.f : 1.f;
+      ss += fin ? v[j] * v[j] : 0.f;
+    }
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = nv * 4 + threadIdx.x; i < n; i += kThreads) {
+      const float v = (float)g[i];
+      const bool fin = __builtin_isfinite(v);
+      bad += fin ? 0.f : 1.f;
+      ss += fin ? v * v : 0.f;
+    }
+  ss = block_sum<kThreads / 64>(ss, red);
+  bad = block_sum<kThreads / 64>(bad, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = make_float2(ss, bad);
+}
+
+__global__ __launch_bounds__(kThreads) void grad_stats_final_kernel(const float2* __restrict__ part, int n,
+                                                                    float* __restrict__ out, bool accumulate) {
+  __shared__ float red[kThreads / 64];
+  float ss = 0.f, bad = 0.f;
+  for (int i = threadIdx.x; i < n; i += kThreads) {
+    ss += part[i].x;
+    bad += part[i].y;
+  }
+  ss = block_sum<kThreads / 64>(ss, red);
+  bad = block_sum<kThreads / 64>(bad, red);
+  if (threadIdx.x == 0) {
+    if (accumulate) {
+      out[0] += ss;
+      out[1] += bad;
+    } else {
+      out[0] = ss;
+      out[1] = bad;
+    }
+  }
+}
+
+struct AdamHyper {
+  float lr, b1, b2, eps, wd, bc1, bc2, grad_scale, max_norm;
+};
+
+__device__ __forceinline__ float clip_coef(const float* stats, const AdamHyper& h, bool& skip) {
+  if (!stats) {
+    skip = false;
+    return h.grad_scale;
+  }
+  skip = stats[1] > 0.f;
+  float coef = h.grad_scale;
+  if (h.max_norm > 0.f) {
+    const float norm = sqrtf(stats[0]) * h.grad_scale;
+    coef *= fminf(1.f, h.max_norm / (norm + 1e-6f));
+  }
+  return coef;
+}
+
+template <typename GT>
+__global__ __launch_bounds__(kThreads) void adamw_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                         float* __restrict__ v, const GT* __restrict__ g,
+                                                         bf16* __restrict__ p16, const float* __restrict__ stats,
+                                                         int64_t n, AdamHyper h) {
+  bool skip;
+  const float gc = clip_coef(stats, h, skip);
+  if (skip) return;  // overflow / NaN: the whole step is dropped (fp16 loss-scaler semantics)
+  const float decay = 1.f - h.lr * h.wd;
+  const float step_size = h.lr / h.bc1;
+  const float inv_sqrt_bc2 = rsqrtf(h.bc2);
+  const int64_t nv = n >> 2;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kThreads) {
+    f32x4 pp = *reinterpret_cast<f32x4*>(p + i * 4);
+    f32x4 mm = *reinterpret_cast<f32x4*>(m + i * 4);
+    f32x4 vv = *reinterpret_cast<f32x4*>(v + i * 4);
+    float gg[4];
+    load4<GT>(g + i * 4, gg);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gj = gg[j] * gc;
+      mm[j] = h.b1 * mm[j] + (1.f - h.b1) * gj;
+      vv[j] = h.b2 * vv[j] + (1.f - h.b2) * gj * gj;
+      const float denom = sqrtf(vv[j]) * inv_sqrt_bc2 + h.eps;
+      pp[j] = pp[j] * decay - step_size * mm[j] / denom;
+    }
+    *reinterpret_cast<f32x4*>(p + i * 4) = pp;
+    *reinterpret_cast<f32x4*>(m + i * 4) = mm;
+    *reinterpret_cast<f32x4*>(v + i * 4) = vv;
+    if (p16) *reinterpret_cast<bf16x4*>(p16 + i * 4) = __builtin_convertvector(pp, bf16x4);
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = nv * 4 + threadIdx.x; i < n; i += kThreads) {
+      const float gj = (float)g[i] * gc;
+      m[i] = h.b1 * m[i] + (1.f - h.b1) * gj;
+      v[i] = h.b2 * v[i] + (1.f - h.b2) * gj * gj;
+      p[i] = p[i] * decay - step_size * m[i] / (sqrtf(v[i]) * inv_sqrt_bc2 + h.eps);
+      if (p16) p16[i] = (bf16)p[i];
+    }
+}
+
+template <typename ST>
+__global__ __launch_bounds__(kThreads) void accumulate_kernel(float* __restrict__ dst, const ST* __restrict__ src,
+                                                              int64_t n, float alpha, float beta) {
+  const int64_t nv = n >> 2;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kThreads) {
+    float s[4];
+    load4<ST>(src + i * 4, s);
+    f32x4 d = beta == 0.f ? (f32x4)(0.f) : *reinterpret_cast<f32x4*>(dst + i * 4) * beta;
+    d += (f32x4){s[0], s[1], s[2], s[3]} * alpha;
+    *reinterpret_cast<f32x4*>(dst + i * 4) = d;
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = nv * 4 + threadIdx.x; i < n; i += kThreads)
+      dst[i] = (beta == 0.f ? 0.f : dst[i] * beta) + alpha * (float)src[i];
+}
+
+__global__ __launch_bounds__(kThreads) void cast_kernel(const float* __restrict__ src, bf16* __restrict__ dst,
+                                                        int64_t n) {
+  const int64_t nv = n >> 2;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kThreads)
+    *reinterpret_cast<bf16x4*>(dst + i * 4) = __builtin_convertvector(*reinterpret_cast<const f32x4*>(src + i * 4), bf16x4);
+  if (blockIdx.x == 0)
+    for (int64_t i = nv * 4 + threadIdx.x; i < n; i += kThreads) dst[i] = (bf16)src[i];
+}
+
+void check_flat(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), name, " must be a contiguous GPU tensor");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+
+}  // namespace
+
+// stats[0] = sum g^2 over all finite elements, stats[1] = count of non-finite elements.
+void dlgm_grad_stats(at::TensorList grads, at::Tensor out, bool accumulate) {
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.numel() >= 2, "grad_stats: bad out");
+  auto stream = c10::hip::getCurrentHIPStream();
+  std::vector<int64_t> grids;
+  int64_t total = 0;
+  for (const auto& g : grads) {
+    check_flat(g, "grad");
+    const int64_t gr = std::min<int64_t>(stream_grid(g.numel() / 4), 512);
+    grids.push_back(gr);
+    total += gr;
+  }
+  if (total == 0) {
+    if (!accumulate) out.zero_();
+    return;
+  }
+  auto part = at::empty({total * 2}, out.options());
+  auto pp = reinterpret_cast<float2*>(part.data_ptr<float>());
+  int64_t off = 0;
+  for (size_t i = 0; i < grads.size(); ++i) {
+    const auto& g = grads[i];
+    if (g.scalar_type() == at::kFloat)
+      grad_stats_partial_kernel<float><<<grids[i], kThreads, 0, stream>>>(g.data_ptr<float>(), g.numel(), pp + off);
+    else {
+      TORCH_CHECK(g.scalar_type() == at::kBFloat16, "grad_stats: grads must be fp32 or bf16");
+      grad_stats_partial_kernel<bf16><<<grids[i], kThreads, 0, stream>>>(
+          reinterpret_cast<const bf16*>(g.data_ptr()), g.numel(), pp + off);
+    }
+    off += grids[i];
+  }
+  grad_stats_final_kernel<<<1, kThreads, 0, stream>>>(pp, (int)total, out.data_ptr<float>(), accumulate);
+  DLGM_CHECK_HIP(hipGetLastError());
+}
+
+void dlgm_adamw_step_(at::Tensor p, at::Tensor m, at::Tensor v, const at::Tensor& g,
+                      const c10::optional<at::Tensor>& p16, const c10::optional<at::Tensor>& stats, double lr,
+                      double beta1, double beta2, double eps, double weight_decay, double bc1, double bc2,
+                      double grad_scale, double max_norm) {
+  check_flat(p, "param");
+  check_flat(m, "exp_avg");
+  check_flat(v, "exp_avg_sq");
+  check_flat(g, "grad");
+  const int64_t n = p.numel();
+  TORCH_CHECK(p.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat,
+              "adamw: master/state must be fp32");
+  TORCH_CHECK(m.numel() == n && v.numel() == n && g.numel() == n, "adamw: size mismatch");
+  bf16* p16p = nullptr;
+  if (p16.has_value() && p16->defined()) {
+    check_flat(*p16, "param_bf16");
+    TORCH_CHECK(p16->scalar_type() == at::kBFloat16 && p16->numel() == n, "adamw: bad bf16 copy");
+    p16p = reinterpret_cast<bf16*>(p16->data_ptr());
+  }
+  const float* sp = nullptr;
+  if (stats.has_value() && stats->defined()) {
+    TORCH_CHECK(stats->scalar_type() == at::kFloat && stats->numel() >= 2 && stats->is_cuda(), "adamw: bad stats");
+    sp = stats->data_ptr<float>();
+  }
+  if (n == 0) return;
+  AdamHyper h{(float)lr, (float)beta1, (float)beta2, (float)eps, (float)weight_decay, (float)bc1, (float)bc2,
+              (float)grad_scale, (float)max_norm};
+  auto stream = c10::hip::getCurrentHIPStream();
+  const int64_t grid = stream_grid(n / 4);
+  if (g.scalar_type() == at::kFloat)
+    adamw_kernel<float><<<grid, kThreads, 0, stream>>>(p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                                                       g.data_ptr<float>(), p16p, sp, n, h);
+  else {
+    TORCH_CHECK(g.scalar_type() == at::kBFloat16, "adamw: grad must be fp32 or bf16");
+    adamw_kernel<bf16><<<grid, kThreads, 0, stream>>>(p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                                                      reinterpret_cast<const bf16*>(g.data_ptr()), p16p, sp, n, h);
+  }
+  DLGM_CHECK_HIP(hipGetLastError());
+}
+
+void dlgm_accumulate_(at::Tensor dst, const at::Tensor& src, double alpha, double beta) {
+  check_flat(dst, "dst");
+  check_flat(src, "src");
+  TORCH_CHECK(dst.scalar_type() == at::kFloat, "accumulate: dst must be fp32");
+  TORCH_CHECK(dst.numel() == src.numel(), "accumulate: size mismatch");
+  const int64_t n = dst.numel();
+  if (n == 0) return;
+  auto stream = c10::hip::getCurrentHIPStream();
+  const int64_t grid = stream_grid(n / 4);
+  if (src.scalar_type() == at::kFloat)
+    accumulate_kernel<float><<<grid, kThreads, 0, stream>>>(dst.data_ptr<float>(), src.data_ptr<float>(), n,
+                                                            (float)alpha, (float)beta);
+  else {
+    TORCH_CHECK(src.scalar_type() == at::kBFloat16, "accumulate: src must be fp32 or bf16");
+    accumulate_kernel<bf16><<<grid, kThreads, 0, stream>>>(dst.data_ptr<float>(),
+                                                           reinterpret_cast<const bf16*>(src.data_ptr()), n,
+                                                           (float)alpha, (float)beta);
+  }
+  DLGM_CHECK_HIP(hipGetLastError());
+}
+
+void dlgm_cast_f32_bf16_(at::Tensor dst, const at::Tensor& src) {
+  check_flat(dst, "dst");
+  check_flat(src, "src");
+  TORCH_CHECK(src.scalar_type() == at::kFloat && dst.scalar_type() == at::kBFloat16 && src.numel() == dst.numel(),
+              "cast: expects fp32 -> bf16 of equal size");
+  const int64_t n = src.numel();
+  if (n == 0) return;
+  auto stream = c10::hip::getCurrentHIPStream();
+  cast_kernel<<<stream_grid(n / 4), kThreads, 0, stream>>>(src.data_ptr<float>(),
+                                                           reinterpret_cast<bf16*>(dst.data_ptr()), n);
+  DLGM_CHECK_HIP(hipGetLastError());
+}

@@ -1,0 +1,275 @@
+// RMSNorm forward / backward (optionally fused with the residual add) for gfx950.
+//
+// Llama-style RMSNorm  y = x * rsqrt(mean(x^2) + eps) * w  sits twice in every
+// transformer block.  Both directions are HBM-bound, so the
+// kernels are built around 16-byte-per-lane accesses:
+//   * one row per wave64: lane l owns 8-element chunks l, l+64, l+128, ... of the
+//     row and keeps them in registers (no LDS round trip for the row data);
+//   * the residual add of the block (h = x + r) is fused into the forward norm,
+//     and the residual-gradient add (dx += dres) into the backward norm, so the
+//     residual stream is read once per direction;
+//   * dw (a column reduction over T rows) is reduced wave -> block in registers
+//     and LDS, written as one fp32 partial row per block, and summed by a tiny
+//     column-reduce kernel (deterministic, no float atomics).
+#include <torch/all.h>
+#include <c10/hip/HIPStream.h>
+#include "dlgm_common.h"
+
+using namespace dlgm;
+
+namespace {
+
+constexpr int kThreads = 256;  // 4 waves -> 4 rows in flight per block
+constexpr int kWaves = kThreads / 64;
+
+template <int MAXC, bool RESID>
+__global__ __launch_bounds__(kThreads) void rmsnorm_fwd_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ r, const bf16* __restrict__ w,
+    bf16* __restrict__ y, bf16* __restrict__ h, float* __restrict__ rstd_out, int T, int D,
+    float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (row >= T) return;
+  const int nch = D >> 3;
+  const size_t base = (size_t)row * D;
+  f32x8 v[MAXC];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+      v[c] = load8f(x + base + ch * 8);
+      if constexpr (RESID) {
+        v[c] += load8f(r + base + ch * 8);
+        store8f(h + base + ch * 8, v[c]);
+        // the normalised value must be computed from the rounded residual
+        // stream so forward and backward see the same h.
+        v[c] = __builtin_convertvector(__builtin_convertvector(v[c], bf16x8), f32x8);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[c][j] * v[c][j];
+    }
+  }
+  ss = wave_sum(ss);
+  const float rs = rsqrtf(ss / (float)D + eps);
+  if (lane == 0) rstd_out[row] = rs;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+      f32x8 wv = load8f(w + ch * 8);
+      store8f(y + base + ch * 8, v[c] * rs * wv);
+    }
+  }
+}
+
+// Backward. Grid-strided over rows: wave `gw` handles rows gw, gw+NW, ...
+// dx = rstd * (dy*w - xhat * mean(dy*w*xhat)) (+ dres);   dw_partial[block] = sum dy*xhat
+template <int MAXC, bool DRES>
+__global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(
+    const bf16* __restrict__ dy, const bf16* __restrict__ hin, const bf16* __restrict__ w,
+    const float* __restrict__ rstd, const bf16* __restrict__ dres, bf16* __restrict__ dx,
+    float* __restrict__ dw_part, int T, int D) {
+  __shared__ __attribute__((aligned(16))) f32x8 red[kWaves][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nch = D >> 3;
+  const int nw = gridDim.x * kWaves;
+  f32x8 acc[MAXC];
+  f32x8 wv[MAXC];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    acc[c] = (f32x8)(0.f);
+    const int ch = lane + c * 64;
+    wv[c] = ch < nch ? load8f(w + ch * 8) : (f32x8)(0.f);
+  }
+  for (int row = blockIdx.x * kWaves + wid; row < T; row += nw) {
+    const size_t base = (size_t)row * D;
+    const float rs = rstd[row];
+    f32x8 g[MAXC], xh[MAXC];
+    float dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int ch = lane + c * 64;
+      if (ch < nch) {
+        g[c] = load8f(dy + base + ch * 8);
+        xh[c] = load8f(hin + base + ch * 8) * rs;
+        acc[c] += g[c] * xh[c];
+        g[c] *= wv[c];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dot += g[c][j] * xh[c][j];
+      }
+    }
+    dot = wave_sum(dot) / (float)D;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int ch = lane + c * 64;
+      if (ch < nch) {
+        f32x8 o = (g[c] - xh[c] * dot) * rs;
+        if constexpr (DRES) o += load8f(dres + base + ch * 8);
+        store8f(dx + base + ch * 8, o);
+      }
+    }
+  }
+  // block-level reduction of the dw accumulators, one 512-column chunk at a time
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    if (c * 64 >= nch) break;  // uniform across the block
+    red[wid][lane] = acc[c];
+    __syncthreads();
+    if (wid == (c & (kWaves - 1))) {
+      f32x8 s = red[0][lane];
+#pragma unroll
+      for (int k = 1; k < kWaves; ++k) s += red[k][lane];
+      const int ch = lane + c * 64;
+      if (ch < nch) {
+        float* dst = dw_part + (size_t)blockIdx.x * D + ch * 8;
+        *reinterpret_cast<f32x4*>(dst) = (f32x4){s[0], s[1], s[2], s[3]};
+        *reinterpret_cast<f32x4*>(dst + 4) = (f32x4){s[4], s[5], s[6], s[7]};
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// dw[d] = (accumulate ? dw[d] : 0) + sum_b part[b][d]; each block owns 64 columns,
+// its 4 waves split the partial rows, LDS combines them.
+template <typename OutT>
+__global__ __launch_bounds__(kThreads) void column_reduce_kernel(const float* __restrict__ part,
+                                                                 OutT* __restrict__ out, int R,
+                                                                 int D, bool accumulate) {
+  __shared__ float red[kWaves][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (col < D)
+    for (int r = wid; r < R; r += kWaves) s += part[(size_t)r * D + col];
+  red[wid][lane] = s;
+  __syncthreads();
+  if (wid == 0 && col < D) {
+    float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    if (accumulate) t += (float)out[col];
+    out[col] = (OutT)t;
+  }
+}
+
+int max_chunks_for(int64_t D) {
+  const int64_t per_lane = (D / 8 + 63) / 64;
+  if (per_lane <= 2) return 2;
+  if (per_lane <= 4) return 4;
+  if (per_lane <= 8) return 8;
+  if (per_lane <= 16) return 16;
+  return -1;
+}
+
+void check_rows(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bf16");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+}  // namespace
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_rmsnorm_fwd(const at::Tensor& x,
+                                                                const c10::optional<at::Tensor>& residual,
+                                                                const at::Tensor& w, double eps) {
+  check_rows(x, "x");
+  check_rows(w, "w");
+  const int64_t D = x.size(-1);
+  const int64_t T = x.numel() / D;
+  TORCH_CHECK(D % 8 == 0, "rmsnorm: hidden size must be a multiple of 8");
+  TORCH_CHECK(w.numel() == D, "rmsnorm: weight size mismatch");
+  const int MAXC = max_chunks_for(D);
+  TORCH_CHECK(MAXC > 0, "rmsnorm: hidden size too large (max 8192)");
+  auto y = at::empty_like(x);
+  auto rstd = at::empty({T}, x.options().dtype(at::kFloat));
+  at::Tensor h;
+  const bool resid = residual.has_value() && residual->defined();
+  if (resid) {
+    check_rows(*residual, "residual");
+    TORCH_CHECK(residual->numel() == x.numel(), "rmsnorm: residual shape mismatch");
+    h = at::empty_like(x);
+  }
+  if (T == 0) return {y, resid ? h : x, rstd};
+  auto stream = c10::hip::getCurrentHIPStream();
+  const dim3 grid((T + kWaves - 1) / kWaves);
+  auto xp = reinterpret_cast<const bf16*>(x.data_ptr());
+  auto rp = resid ? reinterpret_cast<const bf16*>(residual->data_ptr()) : nullptr;
+  auto wp = reinterpret_cast<const bf16*>(w.data_ptr());
+  auto yp = reinterpret_cast<bf16*>(y.data_ptr());
+  auto hp = resid ? reinterpret_cast<bf16*>(h.data_ptr()) : nullptr;
+#define LAUNCH_FWD(C)                                                                        \
+  if (resid)                                                                                 \
+    rmsnorm_fwd_kernel<C, true><<<grid, kThreads, 0, stream>>>(xp, rp, wp, yp, hp,           \
+                                                               rstd.data_ptr<float>(), T, D, \
+                                                               (float)eps);                  \
+  else                                                                                       \
+    rmsnorm_fwd_kernel<C, false><<<grid, kThreads, 0, stream>>>(xp, rp, wp, yp, hp,          \
+                                                                rstd.data_ptr<float>(), T, D, \
+                                                                (float)eps);
+  switch (MAXC) {
+    case 2: LAUNCH_FWD(2); break;
+    case 4: LAUNCH_FWD(4); break;
+    case 8: LAUNCH_FWD(8); break;
+    default: LAUNCH_FWD(16); break;
+  }
+#undef LAUNCH_FWD
+  DLGM_CHECK_HIP(hipGetLastError());
+  return {y, resid ? h : x, rstd};
+}
+
+// Returns dx. dw (bf16 or fp32, D elements, may be a view into a flat grad buffer)
+// receives sum_t dy*xhat (added to its old value when accumulate_dw).
+at::Tensor dlgm_rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at::Tensor& w,
+                            const at::Tensor& rstd, const c10::optional<at::Tensor>& dres,
+                            at::Tensor dw, bool accumulate_dw) {
+  check_rows(dy, "dy");
+  check_rows(h, "h");
+  check_rows(w, "w");
+  const int64_t D = dy.size(-1);
+  const int64_t T = dy.numel() / D;
+  TORCH_CHECK(h.numel() == dy.numel(), "rmsnorm_bwd: shape mismatch");
+  TORCH_CHECK(rstd.numel() == T && rstd.scalar_type() == at::kFloat, "rmsnorm_bwd: bad rstd");
+  TORCH_CHECK(dw.numel() == D && dw.is_contiguous(), "rmsnorm_bwd: bad dw");
+  const int MAXC = max_chunks_for(D);
+  TORCH_CHECK(MAXC > 0 && D % 8 == 0, "rmsnorm_bwd: unsupported hidden size");
+  const bool has_dres = dres.has_value() && dres->defined();
+  if (has_dres) check_rows(*dres, "dres");
+  auto dx = at::empty_like(dy);
+  auto stream = c10::hip::getCurrentHIPStream();
+  // ~4 rows per wave at T=8192 keeps the partial buffer at 512 x D fp32
+  int64_t nblk = std::min<int64_t>((T + kWaves - 1) / kWaves, 512);
+  if (nblk < 1) nblk = 1;
+  auto part = at::empty({nblk, D}, dy.options().dtype(at::kFloat));
+  auto dyp = reinterpret_cast<const bf16*>(dy.data_ptr());
+  auto hp = reinterpret_cast<const bf16*>(h.data_ptr());
+  auto wp = reinterpret_cast<const bf16*>(w.data_ptr());
+  auto drp = has_dres ? reinterpret_cast<const bf16*>(dres->data_ptr()) : nullptr;
+  auto dxp = reinterpret_cast<bf16*>(dx.data_ptr());
+#define LAUNCH_BWD(C)                                                                          \
+  if (has_dres)                                                                                \
+    rmsnorm_bwd_kernel<C, true><<<nblk, kThreads, 0, stream>>>(dyp, hp, wp, rstd.data_ptr<float>(), \
+                                                               drp, dxp, part.data_ptr<float>(), T, D); \
+  else                                                                                         \
+    rmsnorm_bwd_kernel<C, false><<<nblk, kThreads, 0, stream>>>(dyp, hp, wp, rstd.data_ptr<float>(), \
+                                                                drp, dxp, part.data_ptr<float>(), T, D);
+  switch (MAXC) {
+    case 2: LAUNCH_BWD(2); break;
+    case 4: LAUNCH_BWD(4); break;
+    case 8: LAUNCH_BWD(8); break;
+    default: LAUNCH_BWD(16); break;
+  }
+#undef LAUNCH_BWD
+  DLGM_CHECK_HIP(hipGetLastError());
+  const dim3 rgrid((D + 63) / 64);
+  if (dw.scalar_type() == at::kFloat)
+    column_reduce_kernel<float><<<rgrid, kThreads, 0, stream>>>(part.data_ptr<float>(),
+                                                                dw.data_ptr<float>(), nblk, D,
+                                                                accumulate_dw);
+  else {
+    TORCH_CHECK(dw.scalar_type() == at::kBFloat16, "rmsnorm_bwd: dw must be fp32 or bf16");
+    column_reduce_kernel<bf16><<<rgrid, kThreads, 0, stream>>>(
+        part.data_ptr<float>(), reinterpret_cast<bf16*>(dw.data_ptr()), nblk, D, accumulate_dw);
+  }
+  DLGM_CHECK_HIP(hipGetLastError());
+  return dx;
+}

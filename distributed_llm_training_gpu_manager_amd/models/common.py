@@ -1,0 +1,120 @@
+"""Unit abstraction shared by every model family.
+
+A model is a sequence of *units* (embedding, N transformer blocks, head). Each
+unit declares its parameters (:class:`ParamSpec`) and implements an explicit
+``forward`` / ``backward`` pair over plain tensors:
+
+* the ZeRO engine owns all parameter storage as flat buffers (one flat segment
+  per unit) and hands the unit *views* of the gathered/persistent bf16 buffer;
+* ``backward`` writes parameter gradients directly into views of a flat bf16
+  gradient buffer (GEMMs use ``out=`` so no extra copies), which the engine then
+  reduce-scatters / accumulates -- this is the MI355X replacement for DeepSpeed's
+  module hooks + contiguous gradient buffer;
+* nothing in the hot path uses torch.autograd: activation lifetime and memory are
+  explicit, which is what lets the 288 GB HBM plan drop activation recompute.
+
+:class:`AutogradUnit` adapts a plain PyTorch forward for families whose
+backward is not hand-written (it recomputes the forward under autograd in
+backward, i.e. activation checkpointing at unit granularity).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+Params = Dict[str, torch.Tensor]
+
+
+@dataclass
+class ParamSpec:
+    name: str
+    shape: Tuple[int, ...]
+    init: str = "normal"  # normal | ones | zeros | normal_scaled
+    std: float = 0.02
+    weight_decay: bool = True
+
+    @property
+    def numel(self) -> int:
+        return int(math.prod(self.shape))
+
+
+@dataclass
+class StepContext:
+    """Per-micro-batch state shared by all units of one forward/backward."""
+    batch: int
+    seq_len: int
+    input_ids: torch.Tensor  # [B, S] int64
+    labels: torch.Tensor  # [B, S] int64
+    grad_scale: float  # d(loss_total)/d(loss_row)
+    rope: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
+    ep_group: Any = None
+    aux: Dict[str, Any] = field(default_factory=dict)
+
+    @property
+    def tokens(self) -> int:
+        return self.batch * self.seq_len
+
+
+class Unit:
+    """Base class: subclasses define ``specs`` and forward/backward."""
+
+    name: str = "unit"
+
+    def param_specs(self) -> List[ParamSpec]:
+        raise NotImplementedError
+
+    def forward(self, p: Params, x: Any, ctx: StepContext) -> Tuple[Any, Any]:
+        """Return (output, saved). Output of the last unit is the loss sum (device scalar)."""
+        raise NotImplementedError
+
+    def backward(self, p: Params, g: Params, saved: Any, dy: Any, ctx: StepContext) -> Any:
+        """Write parameter grads into ``g`` (views; overwrite, not accumulate) and return d input."""
+        raise NotImplementedError
+
+    # Units whose parameters are needed again at a second position (tied weights)
+    def flops(self, ctx: StepContext) -> float:
+        return 0.0
+
+
+def init_param(spec: ParamSpec, out: torch.Tensor, gen: torch.Generator) -> None:
+    """Deterministic init into a float32 tensor `out` (flat view of the unit)."""
+    if spec.init == "ones":
+        out.fill_(1.0)
+    elif spec.init == "zeros":
+        out.zero_()
+    else:
+        out.normal_(0.0, spec.std, generator=gen)
+
+
+class AutogradUnit(Unit):
+    """Unit whose backward is derived by autograd (recomputes its forward in backward)."""
+
+    def fwd(self, p: Params, x: Any, ctx: StepContext) -> Any:
+        raise NotImplementedError
+
+    def forward(self, p: Params, x: Any, ctx: StepContext):
+        with torch.no_grad():
+            y = self.fwd(p, x, ctx)
+        return y, x
+
+    def backward(self, p: Params, g: Params, saved: Any, dy: Any, ctx: StepContext):
+        x = saved
+        leaves = {k: v.detach().requires_grad_(True) for k, v in p.items()}
+        xin = x.detach().requires_grad_(x.is_floating_point()) if isinstance(x, torch.Tensor) else x
+        with torch.enable_grad():
+            y = self.fwd(leaves, xin, ctx)
+            if dy is None:  # loss unit
+                y.backward()
+            else:
+                y.backward(dy)
+        for k, leaf in leaves.items():
+            if leaf.grad is None:
+                g[k].zero_()
+            else:
+                g[k].copy_(leaf.grad)
+        if isinstance(xin, torch.Tensor) and xin.requires_grad:
+            return xin.grad
+        return None

@@ -1,0 +1,134 @@
+"""GPT-2 family (BASELINE config 1: GPT-2-small ZeRO-1 plumbing run, CPU/gloo).
+
+Blocks are :class:`AutogradUnit` s (LayerNorm / GELU are not on the MI355X
+headline path); attention still goes through :mod:`ops.attention`, i.e. the HIP
+flash kernel on the GPU (head_dim 64 instance) and the fp32 reference on CPU.
+
+Tied input/output embeddings: the embedding table is ONE parameter group that
+appears twice in the stage schedule (first as the token/position embedding,
+last as the LM head). The engine gathers it at both positions and the two
+backward visits accumulate into the same flat gradient segment.
+"""
+from __future__ import annotations
+
+from typing import List
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from .common import AutogradUnit, ParamSpec, Params, StepContext, Unit
+from .config import ModelConfig
+
+
+class GPT2Ends:
+    """Parameter holder for the tied embedding group (wte, wpe, ln_f)."""
+
+    def __init__(self, cfg: ModelConfig):
+        self.cfg = cfg
+
+    def param_specs(self) -> List[ParamSpec]:
+        c = self.cfg
+        specs = [ParamSpec("wte", (c.vocab_size, c.d_model), std=c.init_std, weight_decay=False),
+                 ParamSpec("wpe", (c.max_seq_len, c.d_model), std=0.01, weight_decay=False),
+                 ParamSpec("ln_f_w", (c.d_model,), init="ones", weight_decay=False),
+                 ParamSpec("ln_f_b", (c.d_model,), init="zeros", weight_decay=False)]
+        if not c.tie_embeddings:
+            specs.append(ParamSpec("lm_head", (c.vocab_size, c.d_model), std=c.init_std))
+        return specs
+
+
+class GPT2Embed(Unit):
+    name = "embed"
+
+    def __init__(self, cfg: ModelConfig):
+        self.cfg = cfg
+
+    def forward(self, p: Params, x, ctx: StepContext):
+        ids = ctx.input_ids.reshape(-1)
+        pos = torch.arange(ctx.seq_len, device=ids.device).repeat(ctx.batch)
+        return F.embedding(ids, p["wte"]) + F.embedding(pos, p["wpe"]), (ids, pos)
+
+    def backward(self, p: Params, g: Params, saved, dy, ctx: StepContext):
+        ids, pos = saved
+        # second backward visit of the tied group: the head already wrote d(wte) and d(ln_f)
+        g["wpe"].zero_()
+        g["wpe"].index_put_((pos,), dy, accumulate=True)
+        if not self.cfg.tie_embeddings:
+            g["wte"].zero_()
+        g["wte"].index_put_((ids,), dy.to(g["wte"].dtype), accumulate=True)
+        return None
+
+
+class GPT2Block(AutogradUnit):
+    def __init__(self, cfg: ModelConfig, layer: int):
+        self.cfg = cfg
+        self.name = f"layer{layer}"
+
+    def param_specs(self) -> List[ParamSpec]:
+        c = self.cfg
+        D, Fd = c.d_model, c.ffn_dim
+        proj_std = c.init_std / (2 * c.n_layers) ** 0.5
+        return [
+            ParamSpec("ln1_w", (D,), init="ones", weight_decay=False), ParamSpec("ln1_b", (D,), init="zeros", weight_decay=False),
+            ParamSpec("attn_w", (3 * D, D), std=c.init_std), ParamSpec("attn_b", (3 * D,), init="zeros", weight_decay=False),
+            ParamSpec("proj_w", (D, D), std=proj_std), ParamSpec("proj_b", (D,), init="zeros", weight_decay=False),
+            ParamSpec("ln2_w", (D,), init="ones", weight_decay=False), ParamSpec("ln2_b", (D,), init="zeros", weight_decay=False),
+            ParamSpec("fc_w", (Fd, D), std=c.init_std), ParamSpec("fc_b", (Fd,), init="zeros", weight_decay=False),
+            ParamSpec("out_w", (D, Fd), std=proj_std), ParamSpec("out_b", (D,), init="zeros", weight_decay=False),
+        ]
+
+    def fwd(self, p: Params, x: torch.Tensor, ctx: StepContext) -> torch.Tensor:
+        c = self.cfg
+        B, S, H, hd = ctx.batch, ctx.seq_len, c.n_heads, c.head_dim
+        h = F.layer_norm(x, (c.d_model,), p["ln1_w"], p["ln1_b"], c.norm_eps)
+        qkv = F.linear(h, p["attn_w"], p["attn_b"]).view(B, S, 3, H, hd)
+        a = ops.flash_attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal=True)
+        x = x + F.linear(a.reshape(B * S, c.d_model), p["proj_w"], p["proj_b"])
+        h = F.layer_norm(x, (c.d_model,), p["ln2_w"], p["ln2_b"], c.norm_eps)
+        h = F.gelu(F.linear(h, p["fc_w"], p["fc_b"]), approximate="tanh")
+        return x + F.linear(h, p["out_w"], p["out_b"])
+
+    def flops(self, ctx: StepContext) -> float:
+        c = self.cfg
+        T, S = ctx.tokens, ctx.seq_len
+        return 3.0 * (2 * T * c.d_model * (4 * c.d_model + 2 * c.ffn_dim) + 2 * T * S * c.d_model)
+
+
+class GPT2Head(AutogradUnit):
+    name = "head"
+
+    def __init__(self, cfg: ModelConfig):
+        self.cfg = cfg
+
+    def fwd(self, p: Params, x: torch.Tensor, ctx: StepContext) -> torch.Tensor:
+        c = self.cfg
+        h = F.layer_norm(x, (c.d_model,), p["ln_f_w"], p["ln_f_b"], c.norm_eps)
+        w = p["wte"] if c.tie_embeddings else p["lm_head"]
+        logits = F.linear(h, w).float()
+        return F.cross_entropy(logits, ctx.labels.reshape(-1), reduction="sum") * ctx.grad_scale
+
+    def forward(self, p: Params, x, ctx: StepContext):
+        with torch.no_grad():
+            y = self.fwd(p, x, ctx)
+        return y / ctx.grad_scale, x
+
+    def backward(self, p: Params, g: Params, saved, dy, ctx: StepContext):
+        # first backward visit of the tied group: overwrite wte/ln_f grads (embed adds later)
+        return super().backward(p, g, saved, None, ctx)
+
+    def flops(self, ctx: StepContext) -> float:
+        return 3.0 * 2 * ctx.tokens * self.cfg.d_model * self.cfg.vocab_size
+
+
+def build(cfg: ModelConfig):
+    """Return (param_groups, stages): stage = (unit, group index)."""
+    ends = GPT2Ends(cfg)
+    groups = [("ends", ends.param_specs())]
+    stages = [(GPT2Embed(cfg), 0)]
+    for i in range(cfg.n_layers):
+        blk = GPT2Block(cfg, i)
+        groups.append((blk.name, blk.param_specs()))
+        stages.append((blk, len(groups) - 1))
+    stages.append((GPT2Head(cfg), 0))
+    return groups, stages

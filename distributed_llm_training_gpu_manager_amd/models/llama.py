@@ -1,0 +1,195 @@
+"""Llama-3 family (8B / 70B) as explicit-backward units.
+
+Block dataflow per micro-batch (T = B*S tokens, all bf16, fp32 accumulation
+inside the kernels):
+
+    x        = xa + xb                (fused into the first RMSNorm; the previous
+                                       block hands over its residual as a pair)
+    hn1      = rmsnorm(x) * w_attn    [K3]
+    qkv      = hn1 @ Wqkv^T           hipBLASLt, one GEMM for q, k and v
+    rope_(qkv)                        [K4] in place on the q/k columns
+    attn,lse = flash_attn(q, k, v)    [K6] strided views of qkv, causal GQA
+    o        = attn @ Wo^T
+    hn2, h   = rmsnorm(x + o) * w_mlp [K3, residual add fused]
+    gu       = hn2 @ Wgu^T            one GEMM for gate and up ([2F, D])
+    a        = silu(g) * u            [K5]
+    d        = a @ Wdown^T
+    return (h, d)                     the next unit fuses h + d into its norm
+
+Backward is the exact reverse with GEMMs writing dW straight into the flat
+gradient buffer (``torch.mm(..., out=view)``). With 288 GB of HBM per MI355X,
+all activations of Llama-3-8B at seq 8192 (~1.1 GB/layer) stay resident, so the
+default is NO recompute (SURVEY.md §7.2 memory plan).
+"""
+from __future__ import annotations
+
+from typing import Any, List, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from .common import ParamSpec, Params, StepContext, Unit
+from .config import ModelConfig
+
+
+def _as_pair(x: Any) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    if isinstance(x, tuple):
+        return x
+    return x, None
+
+
+class LlamaEmbedding(Unit):
+    name = "embed"
+
+    def __init__(self, cfg: ModelConfig):
+        self.cfg = cfg
+
+    def param_specs(self) -> List[ParamSpec]:
+        return [ParamSpec("tok_embeddings", (self.cfg.vocab_size, self.cfg.d_model), std=self.cfg.init_std,
+                          weight_decay=False)]
+
+    def forward(self, p: Params, x, ctx: StepContext):
+        ids = ctx.input_ids.reshape(-1)
+        return (F.embedding(ids, p["tok_embeddings"]), None), ids
+
+    def backward(self, p: Params, g: Params, saved, dy, ctx: StepContext):
+        ids = saved
+        gt = g["tok_embeddings"]
+        gt.zero_()
+        gt.index_put_((ids,), dy.reshape(-1, gt.shape[1]), accumulate=True)
+        return None
+
+
+class LlamaBlock(Unit):
+    def __init__(self, cfg: ModelConfig, layer: int):
+        self.cfg = cfg
+        self.layer = layer
+        self.name = f"layer{layer}"
+
+    def param_specs(self) -> List[ParamSpec]:
+        c = self.cfg
+        out_std = c.init_std / (2 * c.n_layers) ** 0.5
+        return [
+            ParamSpec("attn_norm", (c.d_model,), init="ones", weight_decay=False),
+            ParamSpec("wqkv", (c.qkv_dim, c.d_model), std=c.init_std),
+            ParamSpec("wo", (c.d_model, c.n_heads * c.head_dim), std=out_std),
+            ParamSpec("mlp_norm", (c.d_model,), init="ones", weight_decay=False),
+            ParamSpec("w_gate_up", (2 * c.ffn_dim, c.d_model), std=c.init_std),
+            ParamSpec("w_down", (c.d_model, c.ffn_dim), std=out_std),
+        ]
+
+    # -- attention sub-block helpers (shared with Mixtral) --------------------------
+    def attn_forward(self, p: Params, x_pair, ctx: StepContext):
+        c = self.cfg
+        B, S = ctx.batch, ctx.seq_len
+        T = B * S
+        xa, xb = _as_pair(x_pair)
+        hn1, x, rstd1 = ops.rmsnorm_fwd(xa, p["attn_norm"], c.norm_eps, residual=xb)
+        qkv = torch.mm(hn1, p["wqkv"].t())
+        cos, sin = ctx.rope
+        ops.rope_(qkv, cos, sin, c.n_heads + c.n_kv_heads, c.head_dim, S)
+        q, k, v = self._split(qkv, B, S)
+        attn, lse = ops.flash_attn_fwd(q, k, v, causal=True)
+        attn2d = attn.view(T, c.n_heads * c.head_dim)
+        o = torch.mm(attn2d, p["wo"].t())
+        return (x, rstd1, hn1, qkv, attn, lse), o
+
+    def _split(self, qkv: torch.Tensor, B: int, S: int):
+        c = self.cfg
+        hd, H, Hk = c.head_dim, c.n_heads, c.n_kv_heads
+        C = qkv.shape[1]
+        base = qkv.view(B, S, C)
+        q = base[:, :, : H * hd].view(B, S, H, hd)
+        k = base[:, :, H * hd:(H + Hk) * hd].view(B, S, Hk, hd)
+        v = base[:, :, (H + Hk) * hd:].view(B, S, Hk, hd)
+        return q, k, v
+
+    def attn_backward(self, p: Params, g: Params, saved_attn, dh: torch.Tensor, ctx: StepContext):
+        """dh: grad wrt h = x + o. Returns dx (including the residual path)."""
+        c = self.cfg
+        B, S = ctx.batch, ctx.seq_len
+        T = B * S
+        x, rstd1, hn1, qkv, attn, lse = saved_attn
+        attn2d = attn.view(T, c.n_heads * c.head_dim)
+        torch.mm(dh.t(), attn2d, out=g["wo"])
+        dattn = torch.mm(dh, p["wo"]).view_as(attn)
+        q, k, v = self._split(qkv, B, S)
+        dq, dk, dv = ops.flash_attn_bwd(dattn, q, k, v, attn, lse, causal=True)
+        dqkv = torch.cat([dq.view(T, -1), dk.view(T, -1), dv.view(T, -1)], dim=1)
+        cos, sin = ctx.rope
+        ops.rope_(dqkv, cos, sin, c.n_heads + c.n_kv_heads, c.head_dim, S, inverse=True)
+        torch.mm(dqkv.t(), hn1, out=g["wqkv"])
+        dhn1 = torch.mm(dqkv, p["wqkv"])
+        return ops.rmsnorm_bwd(dhn1, x, p["attn_norm"], rstd1, g["attn_norm"], dres=dh)
+
+    # -- unit API --------------------------------------------------------------------
+    def forward(self, p: Params, x_pair, ctx: StepContext):
+        c = self.cfg
+        saved_attn, o = self.attn_forward(p, x_pair, ctx)
+        x = saved_attn[0]
+        hn2, h, rstd2 = ops.rmsnorm_fwd(x, p["mlp_norm"], c.norm_eps, residual=o)
+        gu = torch.mm(hn2, p["w_gate_up"].t())
+        a = ops.swiglu_fwd(gu)
+        d = torch.mm(a, p["w_down"].t())
+        return (h, d), (saved_attn, h, rstd2, hn2, gu, a)
+
+    def backward(self, p: Params, g: Params, saved, dy: torch.Tensor, ctx: StepContext):
+        c = self.cfg
+        saved_attn, h, rstd2, hn2, gu, a = saved
+        torch.mm(dy.t(), a, out=g["w_down"])
+        da = torch.mm(dy, p["w_down"])
+        dgu = ops.swiglu_bwd(da, gu)
+        del da
+        torch.mm(dgu.t(), hn2, out=g["w_gate_up"])
+        dhn2 = torch.mm(dgu, p["w_gate_up"])
+        del dgu
+        dh = ops.rmsnorm_bwd(dhn2, h, p["mlp_norm"], rstd2, g["mlp_norm"], dres=dy)
+        return self.attn_backward(p, g, saved_attn, dh, ctx)
+
+    def flops(self, ctx: StepContext) -> float:
+        c = self.cfg
+        T, S = ctx.tokens, ctx.seq_len
+        gemm = 2 * T * c.d_model * (c.qkv_dim + c.n_heads * c.head_dim + 3 * c.ffn_dim)
+        attn = 2 * T * S * c.n_heads * c.head_dim  # causal: half of 4*T*S*D
+        return 3.0 * (gemm + attn)
+
+
+class LlamaHead(Unit):
+    """Final RMSNorm + LM head + fused cross-entropy (loss and dlogits in one kernel)."""
+
+    name = "head"
+
+    def __init__(self, cfg: ModelConfig):
+        self.cfg = cfg
+
+    def param_specs(self) -> List[ParamSpec]:
+        c = self.cfg
+        return [ParamSpec("norm", (c.d_model,), init="ones", weight_decay=False),
+                ParamSpec("lm_head", (c.vocab_size, c.d_model), std=c.init_std)]
+
+    def forward(self, p: Params, x_pair, ctx: StepContext):
+        c = self.cfg
+        xa, xb = _as_pair(x_pair)
+        hn, x, rstd = ops.rmsnorm_fwd(xa, p["norm"], c.norm_eps, residual=xb)
+        logits = torch.mm(hn, p["lm_head"].t())
+        labels = ctx.labels.reshape(-1)
+        loss_rows, _ = ops.cross_entropy_fwd_bwd_(logits, labels, ctx.grad_scale)
+        # logits now hold d(loss)/d(logits); keep them for backward
+        return loss_rows.sum(), (x, rstd, hn, logits)
+
+    def backward(self, p: Params, g: Params, saved, dy, ctx: StepContext):
+        x, rstd, hn, dlogits = saved
+        torch.mm(dlogits.t(), hn, out=g["lm_head"])
+        dhn = torch.mm(dlogits, p["lm_head"])
+        return ops.rmsnorm_bwd(dhn, x, p["norm"], rstd, g["norm"])
+
+    def flops(self, ctx: StepContext) -> float:
+        return 3.0 * 2 * ctx.tokens * self.cfg.d_model * self.cfg.vocab_size
+
+
+def build(cfg: ModelConfig):
+    """Return (param_groups, stages); every Llama unit owns exactly one parameter group."""
+    units: List[Unit] = [LlamaEmbedding(cfg)] + [LlamaBlock(cfg, i) for i in range(cfg.n_layers)] + [LlamaHead(cfg)]
+    groups = [(u.name, u.param_specs()) for u in units]
+    return groups, [(u, i) for i, u in enumerate(units)]

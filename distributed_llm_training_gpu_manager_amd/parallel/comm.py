@@ -1,0 +1,174 @@
+"""Collective layer: RCCL over xGMI on MI355X (torch.distributed "nccl" == RCCL on ROCm), gloo on CPU.
+
+One process per GPU. Every collective the ZeRO / EP engines issue goes through
+:class:`Comm`, which
+
+* issues RCCL collectives asynchronously (``async_op=True``): RCCL runs them on
+  its own HIP stream ordered after the work already queued on the caller's
+  stream, so gathers/reduce-scatters overlap with the compute that follows;
+  ``Handle.wait()`` only makes the *consumer* stream wait (no host sync);
+* degrades to W == 1 without any copy (the "gathered" buffer IS the shard);
+* emulates ``all_gather_into_tensor`` / ``reduce_scatter_tensor`` / ``AVG`` on
+  gloo (CPU tests, BASELINE config 1) with plain all_gather / all_reduce.
+
+Replaces the NCCL usage DeepSpeed performs for the reference's ZeRO config
+(SURVEY.md §2.7 C1-C8); bucket policy lives in the engine (one transformer
+block per bucket on MI355X -- §5.8).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Callable, List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+class Handle:
+    """Completion handle; ``wait()`` orders the current stream after the collective."""
+
+    def __init__(self, work=None, post: Optional[Callable[[], None]] = None):
+        self._work = work
+        self._post = post
+        self._done = False
+
+    def wait(self) -> None:
+        if self._done:
+            return
+        if self._work is not None:
+            self._work.wait()
+        if self._post is not None:
+            self._post()
+        self._done = True
+
+
+DONE = Handle()
+
+
+@dataclass
+class DistEnv:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+    device: torch.device = torch.device("cpu")
+
+
+def init_distributed(device_type: str = "auto", timeout_s: int = 1800) -> DistEnv:
+    """Initialise the default process group from torchrun-style env vars (idempotent)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if device_type == "auto":
+        device_type = "cuda" if torch.cuda.is_available() else "cpu"
+    if device_type == "cuda":
+        torch.cuda.set_device(local_rank)
+        device = torch.device("cuda", local_rank)
+    else:
+        device = torch.device("cpu")
+    backend = "nccl" if device_type == "cuda" else "gloo"
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kw["device_id"] = device
+        dist.init_process_group(**kw)
+    if dist.is_initialized():
+        backend = dist.get_backend()
+        rank, world = dist.get_rank(), dist.get_world_size()
+    return DistEnv(rank, world, local_rank, backend if world > 1 else "none", device)
+
+
+class Comm:
+    def __init__(self, group=None):
+        self.group = group
+        if dist.is_initialized():
+            self.world = dist.get_world_size(group)
+            self.rank = dist.get_rank(group)
+            self.backend = dist.get_backend(group)
+        else:
+            self.world, self.rank, self.backend = 1, 0, "none"
+        self.is_gloo = self.backend == "gloo"
+
+    # -- gathers ---------------------------------------------------------------------------
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = True) -> Handle:
+        """out = concat over ranks of inp (out.numel() == world * inp.numel())."""
+        if self.world == 1:
+            if out.data_ptr() != inp.data_ptr():
+                out.copy_(inp)
+            return DONE
+        if not self.is_gloo:
+            return Handle(dist.all_gather_into_tensor(out, inp, group=self.group, async_op=async_op))
+        parts = list(out.chunk(self.world))
+        work = dist.all_gather(parts, inp, group=self.group, async_op=async_op)
+        return Handle(work)
+
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, avg: bool = True,
+                       async_op: bool = True) -> Handle:
+        """out = (sum or mean over ranks of inp)[rank's chunk]."""
+        if self.world == 1:
+            if out.data_ptr() != inp.data_ptr():
+                out.copy_(inp)
+            return DONE
+        if not self.is_gloo:
+            op = dist.ReduceOp.AVG if avg else dist.ReduceOp.SUM
+            return Handle(dist.reduce_scatter_tensor(out, inp, op=op, group=self.group, async_op=async_op))
+        buf = inp.clone()
+        work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
+
+        def post():
+            chunk = buf.chunk(self.world)[self.rank]
+            out.copy_(chunk / self.world if avg else chunk)
+        return Handle(work, post)
+
+    def all_reduce(self, t: torch.Tensor, avg: bool = False, async_op: bool = True) -> Handle:
+        if self.world == 1:
+            return DONE
+        if avg and not self.is_gloo:
+            return Handle(dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.group, async_op=async_op))
+        work = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
+        return Handle(work, (lambda: t.div_(self.world)) if avg else None)
+
+    def all_reduce_max(self, t: torch.Tensor) -> None:
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+
+    def all_to_all_single(self, out: torch.Tensor, inp: torch.Tensor, out_splits: Optional[List[int]] = None,
+                          in_splits: Optional[List[int]] = None, async_op: bool = False) -> Handle:
+        if self.world == 1:
+            out.copy_(inp)
+            return DONE
+        if not self.is_gloo:
+            return Handle(dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group,
+                                                 async_op=async_op))
+        # gloo has no all_to_all: emulate with per-peer send/recv pairs (CPU tests only)
+        ins = list(inp.split(in_splits if in_splits else [inp.shape[0] // self.world] * self.world))
+        outs = list(out.split(out_splits if out_splits else [out.shape[0] // self.world] * self.world))
+        ops = []
+        for peer in range(self.world):
+            if peer == self.rank:
+                outs[peer].copy_(ins[peer])
+                continue
+            ops.append(dist.P2POp(dist.isend, ins[peer].contiguous(), peer, group=self.group))
+            ops.append(dist.P2POp(dist.irecv, outs[peer], peer, group=self.group))
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        return DONE
+
+    def broadcast(self, t: torch.Tensor, src: int = 0) -> None:
+        if self.world > 1:
+            dist.broadcast(t, src=src, group=self.group)
+
+    def barrier(self) -> None:
+        if self.world > 1:
+            if self.backend == "nccl":
+                # device barrier via a 1-element all-reduce (no host-side NCCL barrier quirks)
+                t = torch.zeros(1, device=torch.cuda.current_device())
+                dist.all_reduce(t, group=self.group)
+                torch.cuda.synchronize()
+            else:
+                dist.barrier(group=self.group)

@@ -1,0 +1,455 @@
+"""In-house ZeRO-0/1/2/3 engine over flat per-unit parameter segments (RCCL over xGMI).
+
+This replaces the DeepSpeed engine that the reference shells out to
+(``ai_engine/deepspeed_launcher.py:124-238`` emits the config; SURVEY.md §2.5
+N1/N4/N5/N6, §2.7 C1-C5, §2.8). It consumes the same knobs (stage, bucket
+sizes, gradient clipping, AdamW hyper-parameters, WarmupDecayLR) but is laid
+out for MI355X:
+
+Storage (per rank; P = partition world = W for stages 1-3, 1 for stage 0)
+    p16_shard   bf16 [sum_g N_g / P]   compute copy of this rank's partition
+    master, exp_avg, exp_avg_sq, grad_shard  fp32 [same]  -- ONE buffer each, so
+                the optimizer is one fused HIP launch with no host sync
+    p16_full    bf16 [sum_g N_g]       stages 1-2 (persistent gathered params)
+    grad_full   fp32 [sum_g N_g]       stage 1 (local accumulation until the boundary)
+
+Buckets = units: every transformer block is one flat segment (Llama-3-8B:
+218 M params, 436 MB bf16; 70B: 856 M, 1.7 GB). That is the MI355X bucket policy
+of SURVEY.md §5.8: with 288 GB per GPU we move whole blocks in single, large
+RCCL collectives instead of DeepSpeed's 5e8-element buckets.
+
+Schedule (one micro-batch)
+    forward : for each unit  -> wait gather(unit) [stage 3], prefetch gather(next),
+              unit.forward, free gathered params (the head's are kept for backward)
+    backward: for each unit in reverse -> wait gather, prefetch gather(prev),
+              unit.backward writes bf16 grads into a flat scratch segment,
+              async reduce-scatter(avg) of that segment (stage 2/3) whose fp32
+              accumulation is deferred by one unit so RCCL overlaps the next
+              unit's backward
+    step    : grad_stats (sum g^2, #non-finite) -> all_reduce(2 floats) ->
+              fused AdamW reading clip coef / overflow flag on device ->
+              (stage 1/2) all-gather updated bf16 params
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from .. import ops
+from ..models import ModelConfig, StepContext, build_model
+from ..models.common import ParamSpec, init_param
+from .comm import Comm, DONE, Handle
+
+ALIGN = 64  # elements; keeps every param / shard view 128-byte aligned (bf16) for the HIP kernels
+
+
+def _round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+@dataclass
+class EngineConfig:
+    zero_stage: int = 3
+    micro_batch_size: int = 1
+    seq_len: int = 2048
+    grad_accum: int = 1
+    lr: float = 3e-5
+    betas: Tuple[float, float] = (0.9, 0.999)
+    eps: float = 1e-8
+    weight_decay: float = 0.01
+    grad_clip: float = 1.0
+    scheduler: str = "WarmupDecayLR"
+    warmup_steps: int = 100
+    total_steps: int = 10000
+    warmup_min_lr: float = 0.0
+    warmup_type: str = "log"  # DeepSpeed WarmupLR default
+    comm_dtype: torch.dtype = torch.bfloat16
+    activation_checkpointing: bool = False
+    cpu_checkpointing: bool = False
+    prefetch: bool = True
+    seed: int = 1234
+    init_device: str = "auto"  # "cpu" gives bit-identical init on any device (tests); auto: cpu below 1e9 params
+    fp16: bool = False  # dynamic loss scaling path (reference fp16 block)
+    loss_scale: float = 0.0  # 0 = dynamic
+    initial_scale_power: int = 16
+    loss_scale_window: int = 1000
+    hysteresis: int = 2
+    min_loss_scale: float = 1.0
+
+    @property
+    def tokens_per_micro(self) -> int:
+        return self.micro_batch_size * self.seq_len
+
+
+class FlatGroup:
+    """One parameter group (= one unit) as a flat, ALIGN-padded, W-divisible segment."""
+
+    def __init__(self, idx: int, name: str, specs: List[ParamSpec], part_world: int):
+        self.idx, self.name, self.specs = idx, name, specs
+        self.layout: Dict[str, Tuple[int, Tuple[int, ...]]] = {}
+        off = 0
+        for s in specs:
+            self.layout[s.name] = (off, tuple(s.shape))
+            off += _round_up(s.numel, ALIGN)
+        self.numel = _round_up(max(off, 1), ALIGN * part_world)
+        self.shard_numel = self.numel // part_world
+        self.real_numel = sum(s.numel for s in specs)
+        self.shard_off = 0
+        self.full_off = 0
+
+    def views(self, flat: torch.Tensor) -> Dict[str, torch.Tensor]:
+        out = {}
+        for s in self.specs:
+            off, shape = self.layout[s.name]
+            out[s.name] = flat.narrow(0, off, s.numel).view(shape)
+        return out
+
+
+class LossScaler:
+    """fp16 dynamic loss scaler kept on the device (DeepSpeed fp16 block semantics)."""
+
+    def __init__(self, cfg: EngineConfig, device):
+        self.dynamic = cfg.loss_scale == 0
+        self.scale = float(cfg.loss_scale if cfg.loss_scale else 2.0 ** cfg.initial_scale_power)
+        self.window, self.hyst, self.min_scale = cfg.loss_scale_window, cfg.hysteresis, cfg.min_loss_scale
+        self._good = 0
+        self._hyst_left = cfg.hysteresis
+
+    def update(self, overflow: bool) -> None:
+        if not self.dynamic:
+            return
+        if overflow:
+            self._hyst_left -= 1
+            if self._hyst_left <= 0:
+                self.scale = max(self.scale / 2.0, self.min_scale)
+                self._hyst_left = self.hyst
+            self._good = 0
+        else:
+            self._good += 1
+            if self._good % self.window == 0:
+                self.scale *= 2.0
+
+
+def lr_at(cfg: EngineConfig, step: int) -> float:
+    """LR for optimizer step `step` (1-based), DeepSpeed WarmupLR / WarmupDecayLR / WarmupCosineLR."""
+    it = step - 1
+    lo, hi, wu = cfg.warmup_min_lr, cfg.lr, max(1, cfg.warmup_steps)
+    if cfg.scheduler in ("constant", "none", None):
+        return hi
+    if it < wu:
+        if cfg.warmup_type == "log":
+            gamma = math.log(it + 1) / math.log(wu)
+        else:
+            gamma = it / wu
+        return lo + (hi - lo) * gamma
+    if cfg.scheduler == "WarmupLR":
+        return hi
+    total = max(cfg.total_steps, wu + 1)
+    frac = max(0.0, (total - it) / max(1, total - wu))
+    if cfg.scheduler == "WarmupCosineLR":
+        return hi * 0.5 * (1 + math.cos(math.pi * (1 - frac)))
+    return hi * frac  # WarmupDecayLR: linear decay to 0 at total_num_steps
+
+
+class ZeroEngine:
+    def __init__(self, model_cfg: ModelConfig, cfg: EngineConfig, device: torch.device, comm: Optional[Comm] = None,
+                 ep_comm: Optional[Comm] = None):
+        self.mcfg, self.cfg, self.device = model_cfg, cfg, device
+        self.comm = comm or Comm()
+        self.ep_comm = ep_comm
+        self.W, self.rank = self.comm.world, self.comm.rank
+        self.stage = cfg.zero_stage
+        assert self.stage in (0, 1, 2, 3), "ZeRO stage must be 0..3"
+        self.P = 1 if self.stage == 0 else self.W
+        groups, self.stages = build_model(model_cfg)
+        self.groups = [FlatGroup(i, n, s, self.P) for i, (n, s) in enumerate(groups)]
+        soff = foff = 0
+        for g in self.groups:
+            g.shard_off, g.full_off = soff, foff
+            soff += g.shard_numel
+            foff += g.numel
+        self.shard_total, self.full_total = soff, foff
+        # MI355X compute dtype is bf16 (fp16 requests keep the loss-scaler path but compute in bf16)
+        self.dtype = torch.bfloat16
+        self.is_cuda = device.type == "cuda"
+        self._alloc()
+        self._init_params()
+        self.step_count = 0
+        self.scaler = LossScaler(cfg, device) if cfg.fp16 else None
+        self.stats = torch.zeros(2, dtype=torch.float32, device=device)
+        self.loss_acc = torch.zeros((), dtype=torch.float32, device=device)
+        from ..ops.rope import rope_tables
+        if model_cfg.arch in ("llama", "mixtral"):
+            self.rope = rope_tables(model_cfg.head_dim, max(cfg.seq_len, 1), model_cfg.rope_theta, device,
+                                    model_cfg.rope_scaling)
+        else:
+            self.rope = None
+        # group visit bookkeeping (tied weights appear twice)
+        self._bwd_last_visit: Dict[int, int] = {}
+        for si, (_, gi) in enumerate(self.stages):
+            self._bwd_last_visit[gi] = min(si, self._bwd_last_visit.get(gi, si))
+        self._live: Dict[int, Tuple[torch.Tensor, Handle]] = {}
+        self._gbuf_pool: Dict[int, List[torch.Tensor]] = {}
+        self.timers: Dict[str, float] = {}
+        self.hooks: List[Any] = []  # callables(engine, metrics) after each step (NaN trap, monitors)
+
+    # ------------------------------------------------------------------ storage
+    def _alloc(self) -> None:
+        dev, n = self.device, self.shard_total
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.master = torch.zeros(n, **f32)
+        self.exp_avg = torch.zeros(n, **f32)
+        self.exp_avg_sq = torch.zeros(n, **f32)
+        self.grad_shard = torch.zeros(n, **f32)
+        self.p16_shard = torch.zeros(n, dtype=self.dtype, device=dev)
+        self.p16_full = None
+        self.grad_full = None
+        if self.stage == 0:
+            self.p16_full = self.p16_shard  # P == 1: shard == full
+        elif self.stage in (1, 2):
+            self.p16_full = torch.zeros(self.full_total, dtype=self.dtype, device=dev)
+        if self.stage == 1:
+            self.grad_full = torch.zeros(self.full_total, **f32)
+
+    def _init_params(self) -> None:
+        init_dev = self.cfg.init_device
+        if init_dev == "auto":
+            init_dev = "cpu" if sum(g.real_numel for g in self.groups) < 1e9 else self.device.type
+        gen = torch.Generator(device=init_dev)
+        for g in self.groups:
+            full = torch.zeros(g.numel, dtype=torch.float32, device=init_dev)
+            views = g.views(full)
+            gen.manual_seed(self.cfg.seed * 1000003 + g.idx)
+            for s in g.specs:
+                init_param(s, views[s.name], gen)
+            full = full.to(self.device)
+            r0 = (self.rank if self.P > 1 else 0) * g.shard_numel
+            self.master.narrow(0, g.shard_off, g.shard_numel).copy_(full.narrow(0, r0, g.shard_numel))
+            if self.p16_full is not None and self.p16_full is not self.p16_shard:
+                self.p16_full.narrow(0, g.full_off, g.numel).copy_(full)
+            del full
+        ops.cast_f32_bf16_(self.p16_shard, self.master) if self.dtype == torch.bfloat16 else \
+            self.p16_shard.copy_(self.master)
+
+    # ------------------------------------------------------------------ params
+    def _shard16(self, g: FlatGroup) -> torch.Tensor:
+        return self.p16_shard.narrow(0, g.shard_off, g.shard_numel)
+
+    def _issue_gather(self, gi: int) -> None:
+        if gi in self._live:
+            return
+        g = self.groups[gi]
+        if self.stage < 3:
+            flat = self.p16_full.narrow(0, g.full_off, g.numel)
+            self._live[gi] = (flat, DONE)
+        elif self.W == 1:
+            self._live[gi] = (self._shard16(g), DONE)
+        else:
+            buf = torch.empty(g.numel, dtype=self.dtype, device=self.device)
+            self._live[gi] = (buf, self.comm.all_gather(buf, self._shard16(g), async_op=True))
+
+    def fetch(self, gi: int) -> Dict[str, torch.Tensor]:
+        self._issue_gather(gi)
+        flat, h = self._live[gi]
+        h.wait()
+        return self.groups[gi].views(flat)
+
+    def release(self, gi: int) -> None:
+        if self.stage == 3:
+            self._live.pop(gi, None)
+
+    # ------------------------------------------------------------------ grads
+    def _grad_target_full(self, g: FlatGroup) -> Optional[torch.Tensor]:
+        if self.stage == 0:
+            return self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
+        if self.stage == 1:
+            return self.grad_full.narrow(0, g.full_off, g.numel)
+        return None
+
+    def _reduce_group_grad(self, gi: int, gbuf: torch.Tensor, first_micro: bool, last_micro: bool,
+                           pending: List[Tuple[Handle, Any]]) -> None:
+        g = self.groups[gi]
+        beta = 0.0 if first_micro else 1.0
+        if self.stage in (0, 1):
+            tgt = self._grad_target_full(g)
+            ops.accumulate_(tgt, gbuf, 1.0, beta)
+            self._release_gbuf(gbuf)
+            if last_micro:
+                if self.stage == 0:
+                    h = self.comm.all_reduce(tgt, avg=True, async_op=True)
+                    pending.append((h, None))
+                else:
+                    out = self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
+                    h = self.comm.reduce_scatter(out, tgt, avg=True, async_op=True)
+                    pending.append((h, tgt))
+            return
+        shard_tgt = self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
+        if self.W == 1:
+            ops.accumulate_(shard_tgt, gbuf, 1.0, beta)
+            self._release_gbuf(gbuf)
+            return
+        src = gbuf
+        if self.cfg.comm_dtype != gbuf.dtype:
+            src = gbuf.to(self.cfg.comm_dtype)
+            self._release_gbuf(gbuf)
+        out = torch.empty(g.shard_numel, dtype=src.dtype, device=self.device)
+        h = self.comm.reduce_scatter(out, src, avg=True, async_op=True)
+        pending.append((h, (shard_tgt, out, beta, src)))
+
+    def _acquire_gbuf(self, numel: int) -> torch.Tensor:
+        # flat bf16 gradient scratch, pooled per size and zeroed ONCE: units write only their
+        # parameter ranges, so the ALIGN padding stays zero (garbage there would reach the
+        # optimizer and trip the non-finite check)
+        free = self._gbuf_pool.setdefault(numel, [])
+        if free:
+            return free.pop()
+        return torch.zeros(numel, dtype=self.dtype, device=self.device)
+
+    def _release_gbuf(self, buf: torch.Tensor) -> None:
+        self._gbuf_pool.setdefault(buf.numel(), []).append(buf)
+
+    def _drain(self, pending: List[Tuple[Handle, Any]], keep: int) -> None:
+        while len(pending) > keep:
+            h, payload = pending.pop(0)
+            h.wait()
+            if isinstance(payload, tuple):
+                shard_tgt, out, beta, src = payload
+                ops.accumulate_(shard_tgt, out, 1.0, beta)
+                if src is not None and src.dtype == self.dtype:
+                    self._release_gbuf(src)
+
+    # ------------------------------------------------------------------ step
+    def _context(self, ids: torch.Tensor, labels: torch.Tensor) -> StepContext:
+        B, S = ids.shape
+        gs = 1.0 / (B * S * self.cfg.grad_accum)
+        if self.scaler is not None:
+            gs *= self.scaler.scale
+        return StepContext(batch=B, seq_len=S, input_ids=ids, labels=labels, grad_scale=gs, rope=self.rope,
+                           ep_group=self.ep_comm)
+
+    def micro_step(self, ids: torch.Tensor, labels: torch.Tensor, first: bool, last: bool) -> torch.Tensor:
+        ctx = self._context(ids, labels)
+        n = len(self.stages)
+        saved: List[Any] = [None] * n
+        x: Any = None
+        ckpt = self.cfg.activation_checkpointing
+        # ---- forward
+        for si, (unit, gi) in enumerate(self.stages):
+            p = self.fetch(gi)
+            if self.cfg.prefetch and si + 1 < n:
+                self._issue_gather(self.stages[si + 1][1])
+            if ckpt and si < n - 1:
+                y, _ = unit.forward(p, x, ctx)
+                saved[si] = ("ckpt", x)
+            else:
+                y, saved[si] = unit.forward(p, x, ctx)
+            if gi != self.stages[-1][1]:
+                self.release(gi)  # the head's params stay gathered: backward starts with it
+            x = y
+        loss = x
+        # ---- backward
+        dy: Any = None
+        pending: List[Tuple[Handle, Any]] = []
+        gbufs: Dict[int, torch.Tensor] = {}
+        for si in range(n - 1, -1, -1):
+            unit, gi = self.stages[si]
+            p = self.fetch(gi)
+            if self.cfg.prefetch and si > 0:
+                self._issue_gather(self.stages[si - 1][1])
+            g = self.groups[gi]
+            if gi not in gbufs:
+                gbufs[gi] = self._acquire_gbuf(g.numel)
+            gv = g.views(gbufs[gi])
+            sv = saved[si]
+            if isinstance(sv, tuple) and len(sv) == 2 and isinstance(sv[0], str) and sv[0] == "ckpt":
+                _, sv = unit.forward(p, sv[1], ctx)
+            dy = unit.backward(p, gv, sv, dy, ctx)
+            saved[si] = None
+            if self._bwd_last_visit[gi] == si:
+                self._reduce_group_grad(gi, gbufs.pop(gi), first, last, pending)
+                self.release(gi)
+                self._drain(pending, keep=1)
+        self._drain(pending, keep=0)
+        self._live.clear() if self.stage == 3 else None
+        return loss
+
+    def optimizer_step(self) -> Dict[str, Any]:
+        self.step_count += 1
+        cfg = self.cfg
+        ops.grad_stats([self.grad_shard], self.stats)
+        if self.P > 1:
+            self.comm.all_reduce(self.stats, async_op=False).wait()
+        lr = lr_at(cfg, self.step_count)
+        inv_scale = 1.0 / self.scaler.scale if self.scaler else 1.0
+        ops.adamw_step_(self.master, self.exp_avg, self.exp_avg_sq, self.grad_shard,
+                        self.p16_shard if self.dtype == torch.bfloat16 else None, self.stats, lr=lr,
+                        beta1=cfg.betas[0], beta2=cfg.betas[1], eps=cfg.eps, weight_decay=cfg.weight_decay,
+                        step=self.step_count, grad_scale=inv_scale, max_norm=cfg.grad_clip)
+        if self.dtype != torch.bfloat16:
+            self.p16_shard.copy_(self.master)
+        if self.stage in (1, 2):
+            hs = []
+            for g in self.groups:
+                hs.append(self.comm.all_gather(self.p16_full.narrow(0, g.full_off, g.numel), self._shard16(g),
+                                               async_op=True))
+            for h in hs:
+                h.wait()
+        if self.scaler is not None:
+            self.scaler.update(bool(self.stats[1].item() > 0))
+        return {"lr": lr, "stats": self.stats}
+
+    def train_step(self, micro_batches: Sequence[Tuple[torch.Tensor, torch.Tensor]]) -> Dict[str, Any]:
+        """Run len(micro_batches) == grad_accum micro-batches and one optimizer step.
+
+        Returns device tensors (``loss`` mean over the global batch of this rank,
+        ``grad_norm``) -- nothing here synchronises with the host.
+        """
+        assert len(micro_batches) == self.cfg.grad_accum
+        self.loss_acc.zero_()
+        for i, (ids, labels) in enumerate(micro_batches):
+            loss = self.micro_step(ids, labels, first=(i == 0), last=(i == len(micro_batches) - 1))
+            self.loss_acc += loss.float()
+        out = self.optimizer_step()
+        tokens = sum(int(ids.numel()) for ids, _ in micro_batches)
+        metrics = {"loss": self.loss_acc / tokens, "grad_norm": self.stats[0].sqrt()
+                   * (1.0 / self.scaler.scale if self.scaler else 1.0),
+                   "nonfinite": self.stats[1], "lr": out["lr"], "step": self.step_count, "tokens": tokens}
+        for hk in self.hooks:
+            hk(self, metrics)
+        return metrics
+
+    # ------------------------------------------------------------------ helpers
+    def full_params(self) -> Dict[str, torch.Tensor]:
+        """Gather all parameters (fp32 master) -- for tests / consolidated checkpoints."""
+        out = {}
+        for g in self.groups:
+            shard = self.master.narrow(0, g.shard_off, g.shard_numel)
+            if self.P > 1:
+                full = torch.empty(g.numel, dtype=torch.float32, device=self.device)
+                self.comm.all_gather(full, shard, async_op=False).wait()
+            else:
+                full = shard
+            for k, v in g.views(full).items():
+                out[f"{g.name}.{k}"] = v.clone()
+        return out
+
+    def memory_report(self) -> Dict[str, float]:
+        gb = 1024 ** 3
+        rep = {
+            "optimizer_state_GiB": 3 * self.shard_total * 4 / gb,
+            "grad_shard_GiB": self.shard_total * 4 / gb,
+            "param_shard_GiB": self.shard_total * 2 / gb,
+            "param_full_GiB": (self.full_total * 2 / gb) if self.p16_full is not None else 0.0,
+            "grad_full_GiB": (self.full_total * 4 / gb) if self.grad_full is not None else 0.0,
+        }
+        if self.is_cuda:
+            rep["allocated_GiB"] = torch.cuda.memory_allocated(self.device) / gb
+            rep["peak_GiB"] = torch.cuda.max_memory_allocated(self.device) / gb
+        return rep
+
+    def num_params(self) -> int:
+        return sum(g.real_numel for g in self.groups)
