@@ -309,9 +309,11 @@ struct BwdParams {
   const bf16* dout;
   const float* lse;    // [B, Hq, S], natural log of sum exp(scale * s)
   const float* delta;  // [B, Hq, S]
-  float* dq;           // fp32 [B, S, Hq, D] accumulator
-  bf16* dk;            // [B, S, Hkv, D]
-  bf16* dv;            // [B, S, Hkv, D]
+  bf16* dq;            // [B, S, Hq, D]
+  float* dk_part;      // [group, B, S, Hkv, D] fp32 partials (one per q head of the GQA group)
+  float* dv_part;
+  bf16* dk;            // [B, S, Hkv, D] (written directly when group == 1)
+  bf16* dv;
   int64_t q_sb, q_ss, q_sh;
   int64_t k_sb, k_ss, k_sh;
   int64_t v_sb, v_ss, v_sh;
@@ -322,204 +324,171 @@ struct BwdParams {
   bool causal;
 };
 
-constexpr int kBwdThreads = 256;  // 4 waves x 32 keys
-constexpr int kBwdBKV = 128;
-constexpr int kBwdBQ = 32;
+typedef __attribute__((address_space(1))) const void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+// One LDS-DMA piece: 64 lanes x 16 B = 1 KiB landing lane-linearly at `lds` (wave-uniform).
+__device__ __forceinline__ void glds16(const void* src, void* lds) {
+  __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)lds, 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const void* src, void* lds) {
+  __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)lds, 4, 0, 0);
+}
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Stage ROWS x D bf16 rows (row r at base + r*row_stride, r clamped to < nrows_valid) into an
+// LDS image swizzled by SWZ, using LDS-DMA pieces issued by `wave` of `nwaves`. The image is
+// lane-linear per piece; the swizzle is applied to the global SOURCE address (involution).
+template <int D, int ROWS, int SWZ>  // SWZ: 0 = row image, 1 = dual image
+__device__ __forceinline__ void stage_rows(bf16* img, const bf16* base, int64_t row_stride, int row0, int nvalid,
+                                           int wave, int nwaves, int lane) {
+  constexpr int CH = D / 8;
+  constexpr int PR = 64 / CH;               // rows per 1 KiB piece
+  constexpr int NP = ROWS / PR;             // pieces
+  const int rin = lane / CH, phys = lane % CH;
+  for (int pc = wave; pc < NP; pc += nwaves) {
+    const int row = pc * PR + rin;
+    const int logical = SWZ ? swz_dual<D>(row, phys) : swz_row<D>(row, phys);
+    int grow = row0 + row;
+    grow = grow < nvalid ? grow : nvalid - 1;
+    glds16(base + (int64_t)grow * row_stride + logical * 8, img + pc * 512);
+  }
+}
+
+// ---- dK / dV: one workgroup per (b, q head, 128 keys); 4 waves x 32 keys on the MFMA lanes.
+constexpr int kKvThreads = 256;
+constexpr int kKvBKV = 128;
+constexpr int kKvBQ = 32;
 
 template <int D>
-__global__ __launch_bounds__(kBwdThreads, 1) void flash_bwd_kernel(BwdParams p) {
-  constexpr int CH = D / 8;
+__global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams p) {
   constexpr int KK = D / 16;
   constexpr int DT = D / 32;
-  // LDS: K image [128][D] (dual swizzle, tr-read for dQ), Q and dO tiles [32][D] (dual),
-  // dS^T image [128 keys][32 q] (64-B rows), lse/delta for the q tile.
-  __shared__ __attribute__((aligned(16))) bf16 k_lds[kBwdBKV * D];
-  __shared__ __attribute__((aligned(16))) bf16 q_lds[kBwdBQ * D];
-  __shared__ __attribute__((aligned(16))) bf16 do_lds[kBwdBQ * D];
-  __shared__ __attribute__((aligned(16))) bf16 ds_lds[kBwdBKV * kBwdBQ];
-  __shared__ float lse_lds[kBwdBQ];
-  __shared__ float dl_lds[kBwdBQ];
+  constexpr int QT = kKvBQ * D;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * QT + kKvBKV * D];  // [buf][Q | dO], then V rows
+  __shared__ __attribute__((aligned(16))) float rc[2][64];        // [buf][lse 0..31 | delta 32..63]
+  bf16* vimg = smem + 2 * 2 * QT;  // this block's 128 V rows (row image): B operand of dP, re-read per tile
 
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, h = lane >> 5, i16 = lane & 15, g = lane >> 4;
-  const int nkt = (p.S + kBwdBKV - 1) / kBwdBKV;
-  const int work = xcd_remap(blockIdx.x, gridDim.x);
-  const int bk = work / nkt;
-  const int kt = nkt - 1 - (work - bk * nkt);  // under the causal mask the first key blocks see the most queries
-  const int b = bk / p.Hkv, hk = bk % p.Hkv;
+  const int nkt = (p.S + kKvBKV - 1) / kKvBKV;
   const int group = p.Hq / p.Hkv;
-  const int k0 = kt * kBwdBKV;
-  const int kw0 = k0 + 32 * w;  // this wave's 32 keys
+  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = work / nkt;                 // blocks of one (b, hq) share the Q / dO stream -> one XCD
+  const int kt = work - bh * nkt;            // ascending = most queries first under the causal mask
+  const int b = bh / p.Hq, hq = bh % p.Hq;
+  const int hk = hq / group, hh = hq % group;
+  const int k0 = kt * kKvBKV;
+  const int kw0 = k0 + 32 * w;
+  const int key = kw0 + r;
   const bf16* kb = p.k + b * p.k_sb + hk * p.k_sh;
   const bf16* vb = p.v + b * p.v_sb + hk * p.v_sh;
+  const bf16* qb = p.q + b * p.q_sb + hq * p.q_sh;
+  const bf16* dob = p.dout + b * p.do_sb + hq * p.do_sh;
+  const float* lseb = p.lse + ((int64_t)b * p.Hq + hq) * p.S;
+  const float* dlb = p.delta + ((int64_t)b * p.Hq + hq) * p.S;
 
-  // stage K block into LDS (dual image) and this wave's K / V rows into registers
-  for (int c = threadIdx.x; c < kBwdBKV * CH; c += kBwdThreads) {
-    const int row = c / CH, ch = c % CH;
-    const int kv = k0 + row;
-    uint4 val = kv < p.S ? *reinterpret_cast<const uint4*>(kb + (int64_t)kv * p.k_ss + ch * 8) : make_uint4(0, 0, 0, 0);
-    *reinterpret_cast<uint4*>(k_lds + row * D + swz_dual<D>(row, ch) * 8) = val;
-  }
-  bf16x8 kf[KK], vf[KK];  // B operands: K^T / V^T, lane holds row (kw0 + r), d = 16kk + 8h ..
-  {
-    const int kv = kw0 + r;
+  // K^T B-operand fragments of this wave's 32 keys stay in registers for the whole block; the V
+  // rows go to LDS once (registers are the binding constraint at 2 waves / SIMD)
+  bf16x8 kf[KK];
 #pragma unroll
-    for (int kk = 0; kk < KK; ++kk) {
-      kf[kk] = kv < p.S ? *reinterpret_cast<const bf16x8*>(kb + (int64_t)kv * p.k_ss + 16 * kk + 8 * h) : (bf16x8)((bf16)0.f);
-      vf[kk] = kv < p.S ? *reinterpret_cast<const bf16x8*>(vb + (int64_t)kv * p.v_ss + 16 * kk + 8 * h) : (bf16x8)((bf16)0.f);
-    }
+  for (int kk = 0; kk < KK; ++kk) {
+    const bool ok = key < p.S;
+    kf[kk] = ok ? *reinterpret_cast<const bf16x8*>(kb + (int64_t)key * p.k_ss + 16 * kk + 8 * h) : (bf16x8)((bf16)0.f);
   }
-  f32x16 dkt[DT], dvt[DT];  // dK^T, dV^T : [d][key], col = key = kw0 + r
+  stage_rows<D, kKvBKV, 0>(vimg, vb, p.v_ss, k0, p.S, w, 4, lane);
+  f32x16 dkt[DT], dvt[DT];  // dK^T, dV^T : [d][key]
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) {
     dkt[dt] = (f32x16)(0.f);
     dvt[dt] = (f32x16)(0.f);
   }
-  const int nqt = (p.S + kBwdBQ - 1) / kBwdBQ;
-  const int qt_begin = p.causal ? k0 / kBwdBQ : 0;
-  const int key = kw0 + r;
+  const int nqt = (p.S + kKvBQ - 1) / kKvBQ;
+  const int t0 = p.causal ? k0 / kKvBQ : 0;
 
-  for (int hh = 0; hh < group; ++hh) {
-    const int hq = hk * group + hh;
-    const bf16* qb = p.q + b * p.q_sb + hq * p.q_sh;
-    const bf16* dob = p.dout + b * p.do_sb + hq * p.do_sh;
-    const float* lseb = p.lse + ((int64_t)b * p.Hq + hq) * p.S;
-    const float* dlb = p.delta + ((int64_t)b * p.Hq + hq) * p.S;
-    float* dqb = p.dq + ((int64_t)b * p.S * p.Hq + hq) * D;
-    for (int qt = qt_begin; qt < nqt; ++qt) {
-      const int q0 = qt * kBwdBQ;
-      __syncthreads();  // previous tile's LDS reads are done
-      for (int c = threadIdx.x; c < kBwdBQ * CH; c += kBwdThreads) {
-        const int row = c / CH, ch = c % CH;
-        const int q = q0 + row;
-        uint4 qv = make_uint4(0, 0, 0, 0), dv = make_uint4(0, 0, 0, 0);
-        if (q < p.S) {
-          qv = *reinterpret_cast<const uint4*>(qb + (int64_t)q * p.q_ss + ch * 8);
-          dv = *reinterpret_cast<const uint4*>(dob + (int64_t)q * p.do_ss + ch * 8);
-        }
-        *reinterpret_cast<uint4*>(q_lds + row * D + swz_dual<D>(row, ch) * 8) = qv;
-        *reinterpret_cast<uint4*>(do_lds + row * D + swz_dual<D>(row, ch) * 8) = dv;
-      }
-      if (threadIdx.x < kBwdBQ) {
-        const int q = q0 + threadIdx.x;
-        lse_lds[threadIdx.x] = q < p.S ? lseb[q] * kLog2e : INFINITY;  // log2 domain; +inf -> p = 0
-        dl_lds[threadIdx.x] = q < p.S ? dlb[q] : 0.f;
-      }
-      __syncthreads();
-      const bool wave_active = !(p.causal && q0 + kBwdBQ - 1 < kw0);  // some query sees some key
+  auto stage = [&](int buf, int t) {
+    const int q0 = t * kKvBQ;
+    bf16* img = smem + buf * 2 * QT;
+    stage_rows<D, kKvBQ, 1>(img, qb, p.q_ss, q0, p.S, w, 4, lane);
+    stage_rows<D, kKvBQ, 1>(img + QT, dob, p.do_ss, q0, p.S, w, 4, lane);
+    if (w == 0) {
+      int q = q0 + (lane & 31);
+      q = q < p.S ? q : p.S - 1;
+      glds4((lane < 32 ? lseb : dlb) + q, &rc[buf][0]);
+    }
+  };
+
+  if (t0 < nqt) stage(0, t0);
+  vm_drain();
+  __syncthreads();
+  for (int t = t0; t < nqt; ++t) {
+    const int buf = (t - t0) & 1;
+    if (t + 1 < nqt) stage(buf ^ 1, t + 1);
+    const int q0 = t * kKvBQ;
+    const bool active = !(p.causal && q0 + kKvBQ - 1 < kw0);
+    if (active) {
+      const bf16* qi = smem + buf * 2 * QT;
+      const bf16* di = qi + QT;
       f32x16 sacc, dpacc;
-      if (wave_active) {
-        // init accumulators with the row constants: S' = S*scale*log2e - lse2, dP' = dP - delta
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int qr = (i & 3) + 8 * (i >> 2) + 4 * h;
-          sacc[i] = -lse_lds[qr] / p.scale_log2;
-          dpacc[i] = -dl_lds[qr];
-        }
-        // S = Q K^T (key on lane): A = Q rows, B = K^T frags
+      for (int i = 0; i < 16; ++i) {
+        const int qr = (i & 3) + 8 * (i >> 2) + 4 * h;
+        sacc[i] = -rc[buf][qr] / p.scale;  // S' = S - lse/scale  ->  p = exp2(S' * scale * log2e)
+        dpacc[i] = -rc[buf][32 + qr];
+      }
 #pragma unroll
-        for (int kk = 0; kk < KK; ++kk) {
-          bf16x8 a = lds_read_b128(q_lds + r * D + swz_dual<D>(r, 2 * kk + h) * 8);
-          sacc = mfma32(a, kf[kk], sacc);
-        }
-        // dP = dO V^T
+      for (int kk = 0; kk < KK; ++kk) {
+        bf16x8 a = lds_read_b128(qi + r * D + swz_dual<D>(r, 2 * kk + h) * 8);
+        sacc = mfma32(a, kf[kk], sacc);
+      }
+      const int vrow = 32 * w + r;
 #pragma unroll
-        for (int kk = 0; kk < KK; ++kk) {
-          bf16x8 a = lds_read_b128(do_lds + r * D + swz_dual<D>(r, 2 * kk + h) * 8);
-          dpacc = mfma32(a, vf[kk], dpacc);
-        }
-        // P and dS (row = query, col = key)
+      for (int kk = 0; kk < KK; ++kk) {
+        bf16x8 a = lds_read_b128(di + r * D + swz_dual<D>(r, 2 * kk + h) * 8);
+        bf16x8 vv = lds_read_b128(vimg + vrow * D + swz_row<D>(vrow, 2 * kk + h) * 8);
+        dpacc = mfma32(a, vv, dpacc);
+      }
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int q = q0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-          float pv = exp2f(sacc[i] * p.scale_log2);
-          if (key >= p.S || q >= p.S || (p.causal && key > q)) pv = 0.f;
-          sacc[i] = pv;
-          dpacc[i] = pv * dpacc[i] * p.scale;  // dS (includes the softmax scale for dQ / dK)
-        }
-        bf16x8 pfr[2], dsf[2];
+      for (int i = 0; i < 16; ++i) {
+        const int q = q0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        float pv = exp2f(sacc[i] * p.scale_log2);
+        if (key >= p.S || q >= p.S || (p.causal && key > q)) pv = 0.f;
+        sacc[i] = pv;
+        dpacc[i] = pv * dpacc[i] * p.scale;
+      }
+      bf16x8 pfr[2], dsf[2];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        pfr[s2] = (bf16x8){(bf16)sacc[8 * s2 + 0], (bf16)sacc[8 * s2 + 1], (bf16)sacc[8 * s2 + 2],
+                           (bf16)sacc[8 * s2 + 3], (bf16)sacc[8 * s2 + 4], (bf16)sacc[8 * s2 + 5],
+                           (bf16)sacc[8 * s2 + 6], (bf16)sacc[8 * s2 + 7]};
+        dsf[s2] = (bf16x8){(bf16)dpacc[8 * s2 + 0], (bf16)dpacc[8 * s2 + 1], (bf16)dpacc[8 * s2 + 2],
+                           (bf16)dpacc[8 * s2 + 3], (bf16)dpacc[8 * s2 + 4], (bf16)dpacc[8 * s2 + 5],
+                           (bf16)dpacc[8 * s2 + 6], (bf16)dpacc[8 * s2 + 7]};
+      }
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const int col = dt * 32 + 16 * (g & 1) + 4 * (i16 & 3);
+        const int ch = col >> 3, within = col & 7;
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          pfr[s2] = (bf16x8){(bf16)sacc[8 * s2 + 0], (bf16)sacc[8 * s2 + 1], (bf16)sacc[8 * s2 + 2],
-                             (bf16)sacc[8 * s2 + 3], (bf16)sacc[8 * s2 + 4], (bf16)sacc[8 * s2 + 5],
-                             (bf16)sacc[8 * s2 + 6], (bf16)sacc[8 * s2 + 7]};
-          dsf[s2] = (bf16x8){(bf16)dpacc[8 * s2 + 0], (bf16)dpacc[8 * s2 + 1], (bf16)dpacc[8 * s2 + 2],
-                             (bf16)dpacc[8 * s2 + 3], (bf16)dpacc[8 * s2 + 4], (bf16)dpacc[8 * s2 + 5],
-                             (bf16)dpacc[8 * s2 + 6], (bf16)dpacc[8 * s2 + 7]};
-        }
-        // dV^T += dO^T P ; dK^T += Q^T dS   (A operands by transposed reads of the q-tile images)
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          const int col = dt * 32 + 16 * (g & 1) + 4 * (i16 & 3);
-          const int ch = col >> 3, within = col & 7;
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const int r1 = 16 * s2 + 4 * h + (i16 >> 2);
-            const int r2 = r1 + 8;
-            bf16x8 a_do = cat(lds_read_tr(do_lds + r1 * D + swz_dual<D>(r1, ch) * 8 + within),
-                              lds_read_tr(do_lds + r2 * D + swz_dual<D>(r2, ch) * 8 + within));
-            dvt[dt] = mfma32(a_do, pfr[s2], dvt[dt]);
-            bf16x8 a_q = cat(lds_read_tr(q_lds + r1 * D + swz_dual<D>(r1, ch) * 8 + within),
-                             lds_read_tr(q_lds + r2 * D + swz_dual<D>(r2, ch) * 8 + within));
-            dkt[dt] = mfma32(a_q, dsf[s2], dkt[dt]);
-          }
-        }
-        // dS^T image [key 0..127][q 0..31]: 64-B rows, 8-B pieces; swizzle 16-B chunks by key
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int krow = 32 * w + r;
-          const int qc = 8 * g4 + 4 * h;  // 4 consecutive queries
-          const int ch = qc >> 3, within = qc & 7;
-          bf16x4 v = {(bf16)dpacc[4 * g4 + 0], (bf16)dpacc[4 * g4 + 1], (bf16)dpacc[4 * g4 + 2],
-                      (bf16)dpacc[4 * g4 + 3]};
-          *reinterpret_cast<bf16x4*>(ds_lds + krow * kBwdBQ + ((ch ^ ((krow >> 1) & 3)) * 8) + within) = v;
-        }
-      } else {
-        // keys of this wave all lie after the tile's queries: dS = 0
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int krow = 32 * w + r;
-          const int qc = 8 * g4 + 4 * h;
-          const int ch = qc >> 3, within = qc & 7;
-          *reinterpret_cast<bf16x4*>(ds_lds + krow * kBwdBQ + ((ch ^ ((krow >> 1) & 3)) * 8) + within) =
-              (bf16x4)((bf16)0.f);
-        }
-      }
-      __syncthreads();
-      // dQ[q][d] += dS[q][key] K[key][d] over the block's 128 keys; wave w owns d-tile w (D=128)
-      // A = dS (q on rows, natural k order) via transposed reads of the dS^T image,
-      // B = K (key = k, d on lane) via transposed reads of the K image.
-      for (int dt = w; dt < DT; dt += 4) {
-        f32x16 dqacc = (f32x16)(0.f);
-        const int kmax = p.causal ? min(kBwdBKV, q0 + kBwdBQ - k0) : kBwdBKV;  // keys beyond the last query give dS = 0
-#pragma unroll 2
-        for (int ks = 0; ks < kBwdBKV / 16; ++ks) {
-          if (ks * 16 >= kmax) break;
-          // A: lane (r = q, h) elements j = dS[q = r][key = 16ks + 8h + j]; rows of the dS^T image are keys
-          const int qcol = 16 * (g & 1) + 4 * (i16 & 3);  // column block of the dS^T image (queries)
-          const int kr1 = 16 * ks + 8 * h + (i16 >> 2);
-          const int kr2 = kr1 + 4;
-          const int ach = qcol >> 3, aw = qcol & 7;
-          bf16x8 a = cat(lds_read_tr(ds_lds + kr1 * kBwdBQ + ((ach ^ ((kr1 >> 1) & 3)) * 8) + aw),
-                         lds_read_tr(ds_lds + kr2 * kBwdBQ + ((ach ^ ((kr2 >> 1) & 3)) * 8) + aw));
-          // B: lane (r = d, h) elements j = K[key = 16ks + 8h + j][d = 32dt + r]
-          const int dcol = dt * 32 + 16 * (g & 1) + 4 * (i16 & 3);
-          const int bch = dcol >> 3, bw = dcol & 7;
-          bf16x8 bb = cat(lds_read_tr(k_lds + kr1 * D + swz_dual<D>(kr1, bch) * 8 + bw),
-                          lds_read_tr(k_lds + kr2 * D + swz_dual<D>(kr2, bch) * 8 + bw));
-          dqacc = mfma32(a, bb, dqacc);
-        }
-        // rows = queries, col = d: each atomic instruction covers two 128-B row segments
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int q = q0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-          if (q < p.S) atomicAdd(dqb + (int64_t)q * p.Hq * D + dt * 32 + r, dqacc[i]);
+          const int r1 = 16 * s2 + 4 * h + (i16 >> 2);
+          const int r2 = r1 + 8;
+          bf16x8 a_do = cat(lds_read_tr(di + r1 * D + swz_dual<D>(r1, ch) * 8 + within),
+                            lds_read_tr(di + r2 * D + swz_dual<D>(r2, ch) * 8 + within));
+          dvt[dt] = mfma32(a_do, pfr[s2], dvt[dt]);
+          bf16x8 a_q = cat(lds_read_tr(qi + r1 * D + swz_dual<D>(r1, ch) * 8 + within),
+                           lds_read_tr(qi + r2 * D + swz_dual<D>(r2, ch) * 8 + within));
+          dkt[dt] = mfma32(a_q, dsf[s2], dkt[dt]);
         }
       }
     }
+    vm_drain();  // the next tile's LDS-DMA has landed
+    __syncthreads();
   }
-  // write dK, dV (scale already folded into dS)
-  if (key < p.S) {
+  if (key >= p.S) return;
+  if (group == 1) {
     bf16* dkr = p.dk + (((int64_t)b * p.S + key) * p.Hkv + hk) * D;
     bf16* dvr = p.dv + (((int64_t)b * p.S + key) * p.Hkv + hk) * D;
 #pragma unroll
@@ -532,15 +501,164 @@ __global__ __launch_bounds__(kBwdThreads, 1) void flash_bwd_kernel(BwdParams p) 
         *reinterpret_cast<bf16x4*>(dvr + d) = (bf16x4){(bf16)dvt[dt][4 * g4 + 0], (bf16)dvt[dt][4 * g4 + 1],
                                                        (bf16)dvt[dt][4 * g4 + 2], (bf16)dvt[dt][4 * g4 + 3]};
       }
+  } else {
+    const int64_t off = ((((int64_t)hh * p.B + b) * p.S + key) * p.Hkv + hk) * D;
+    float* dkr = p.dk_part + off;
+    float* dvr = p.dv_part + off;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = dt * 32 + 8 * g4 + 4 * h;
+        *reinterpret_cast<f32x4*>(dkr + d) = (f32x4){dkt[dt][4 * g4 + 0], dkt[dt][4 * g4 + 1], dkt[dt][4 * g4 + 2],
+                                                     dkt[dt][4 * g4 + 3]};
+        *reinterpret_cast<f32x4*>(dvr + d) = (f32x4){dvt[dt][4 * g4 + 0], dvt[dt][4 * g4 + 1], dvt[dt][4 * g4 + 2],
+                                                     dvt[dt][4 * g4 + 3]};
+      }
   }
 }
 
-__global__ void f32_to_bf16_rows_kernel(const float* __restrict__ src, bf16* __restrict__ dst, int64_t n) {
+// Sum the per-q-head fp32 partials of the GQA group (fixed order: deterministic) -> bf16.
+__global__ __launch_bounds__(256) void gqa_reduce_kernel(const float* __restrict__ part, bf16* __restrict__ out,
+                                                         int group, int64_t n) {
   const int64_t nv = n >> 3;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
-    f32x4 a = *reinterpret_cast<const f32x4*>(src + i * 8);
-    f32x4 c = *reinterpret_cast<const f32x4*>(src + i * 8 + 4);
-    store8f(dst + i * 8, (f32x8){a[0], a[1], a[2], a[3], c[0], c[1], c[2], c[3]});
+    f32x8 s = (f32x8)(0.f);
+    for (int gq = 0; gq < group; ++gq) {
+      const float* src = part + gq * n + i * 8;
+      f32x4 a = *reinterpret_cast<const f32x4*>(src);
+      f32x4 c = *reinterpret_cast<const f32x4*>(src + 4);
+      s += (f32x8){a[0], a[1], a[2], a[3], c[0], c[1], c[2], c[3]};
+    }
+    store8f(out + i * 8, s);
+  }
+}
+
+// ---- dQ: one workgroup per (b, q head, 128 queries) -- the forward's structure (query on the
+// lane, S^T = K Q^T, dP^T = V dO^T); dQ^T += K^T dS^T takes the dS^T accumulator in place as the
+// B operand, so dQ needs no atomics and no LDS round trip.
+constexpr int kDqThreads = 256;
+constexpr int kDqBQ = 128;
+constexpr int kDqBKV = 64;
+
+template <int D>
+__global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams p) {
+  constexpr int KK = D / 16;
+  constexpr int DT = D / 32;
+  constexpr int TILE = kDqBKV * D;
+  __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];  // [buf][K | V]
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, h = lane >> 5, i16 = lane & 15, g = lane >> 4;
+  const int nqt = (p.S + kDqBQ - 1) / kDqBQ;
+  const int group = p.Hq / p.Hkv;
+  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_kv = group * nqt;
+  const int bk = work / per_kv;
+  const int rem = work - bk * per_kv;
+  const int qt = nqt - 1 - rem / group;
+  const int hq = (bk % p.Hkv) * group + rem % group;
+  const int b = bk / p.Hkv;
+  const int hk = hq / group;
+  const int q0 = qt * kDqBQ;
+  const int q0w = q0 + 32 * w;
+  const int qcol = q0w + r;
+  const bf16* qb = p.q + b * p.q_sb + hq * p.q_sh;
+  const bf16* dob = p.dout + b * p.do_sb + hq * p.do_sh;
+  const bf16* kb = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16* vb = p.v + b * p.v_sb + hk * p.v_sh;
+
+  bf16x8 qf[KK], dof[KK];
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) {
+    const bool ok = qcol < p.S;
+    qf[kk] = ok ? *reinterpret_cast<const bf16x8*>(qb + (int64_t)qcol * p.q_ss + 16 * kk + 8 * h) : (bf16x8)((bf16)0.f);
+    dof[kk] = ok ? *reinterpret_cast<const bf16x8*>(dob + (int64_t)qcol * p.do_ss + 16 * kk + 8 * h) : (bf16x8)((bf16)0.f);
+  }
+  const int64_t rowc = ((int64_t)b * p.Hq + hq) * p.S;
+  const float lse2 = qcol < p.S ? p.lse[rowc + qcol] * kLog2e : INFINITY;
+  const float dl = qcol < p.S ? p.delta[rowc + qcol] : 0.f;
+
+  f32x16 dqt[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) dqt[dt] = (f32x16)(0.f);
+
+  const int kv_end = p.causal ? min(p.S, q0 + kDqBQ) : p.S;
+  const int nt = (kv_end + kDqBKV - 1) / kDqBKV;
+  auto stage = [&](int buf, int t) {
+    bf16* img = smem + buf * 2 * TILE;
+    stage_rows<D, kDqBKV, 1>(img, kb, p.k_ss, t * kDqBKV, p.S, w, 4, lane);
+    stage_rows<D, kDqBKV, 0>(img + TILE, vb, p.v_ss, t * kDqBKV, p.S, w, 4, lane);
+  };
+  stage(0, 0);
+  vm_drain();
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nt) stage(buf ^ 1, t + 1);
+    const int kv0 = t * kDqBKV;
+    if (!(p.causal && kv0 > q0w + 31)) {
+      const bf16* kt = smem + buf * 2 * TILE;
+      const bf16* vt = kt + TILE;
+      f32x16 s[2] = {(f32x16)(0.f), (f32x16)(0.f)};
+      f32x16 dp[2] = {(f32x16)(-dl), (f32x16)(-dl)};
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int row = 32 * u + r;
+          bf16x8 a = lds_read_b128(kt + row * D + swz_dual<D>(row, 2 * kk + h) * 8);
+          s[u] = mfma32(a, qf[kk], s[u]);
+          bf16x8 c = lds_read_b128(vt + row * D + swz_row<D>(row, 2 * kk + h) * 8);
+          dp[u] = mfma32(c, dof[kk], dp[u]);
+        }
+      }
+      bf16x8 dsf[2][2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int kv = kv0 + 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
+          float pv = exp2f(s[u][i] * p.scale_log2 - lse2);
+          if (kv >= p.S || (p.causal && kv > qcol)) pv = 0.f;
+          s[u][i] = pv * dp[u][i] * p.scale;
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+          dsf[u][s2] = (bf16x8){(bf16)s[u][8 * s2 + 0], (bf16)s[u][8 * s2 + 1], (bf16)s[u][8 * s2 + 2],
+                                (bf16)s[u][8 * s2 + 3], (bf16)s[u][8 * s2 + 4], (bf16)s[u][8 * s2 + 5],
+                                (bf16)s[u][8 * s2 + 6], (bf16)s[u][8 * s2 + 7]};
+      }
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const int col = dt * 32 + 16 * (g & 1) + 4 * (i16 & 3);
+        const int ch = col >> 3, within = col & 7;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const int r1 = 32 * u + 16 * s2 + 4 * h + (i16 >> 2);
+            const int r2 = r1 + 8;
+            bf16x8 a = cat(lds_read_tr(kt + r1 * D + swz_dual<D>(r1, ch) * 8 + within),
+                           lds_read_tr(kt + r2 * D + swz_dual<D>(r2, ch) * 8 + within));
+            dqt[dt] = mfma32(a, dsf[u][s2], dqt[dt]);
+          }
+      }
+    }
+    vm_drain();
+    __syncthreads();
+  }
+  if (qcol < p.S) {
+    bf16* orow = p.dq + (((int64_t)b * p.S + qcol) * p.Hq + hq) * D;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = dt * 32 + 8 * g4 + 4 * h;
+        *reinterpret_cast<bf16x4*>(orow + d) = (bf16x4){(bf16)dqt[dt][4 * g4 + 0], (bf16)dqt[dt][4 * g4 + 1],
+                                                        (bf16)dqt[dt][4 * g4 + 2], (bf16)dqt[dt][4 * g4 + 3]};
+      }
   }
 }
 
@@ -595,16 +713,21 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
   check_qkv(dout, "dout");
   const int B = q.size(0), S = q.size(1), Hq = q.size(2), D = q.size(3);
   const int Hkv = k.size(2);
+  const int group = Hq / Hkv;
   TORCH_CHECK(D == 128 || D == 64, "flash_attn_bwd: head dim must be 64 or 128");
   TORCH_CHECK(out.is_contiguous() && out.sizes() == q.sizes(), "flash_attn_bwd: out must be contiguous [B,S,Hq,D]");
   TORCH_CHECK(lse.is_contiguous() && lse.numel() == (int64_t)B * Hq * S, "flash_attn_bwd: bad lse");
   TORCH_CHECK(dout.sizes() == q.sizes(), "flash_attn_bwd: dout shape mismatch");
-  auto dq32 = at::zeros({B, S, Hq, D}, q.options().dtype(at::kFloat));
   auto dk = at::empty({B, S, Hkv, D}, q.options());
   auto dv = at::empty({B, S, Hkv, D}, q.options());
   auto dq = at::empty({B, S, Hq, D}, q.options());
   if (B == 0 || S == 0) return {dq.zero_(), dk.zero_(), dv.zero_()};
   auto delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
+  at::Tensor dk_part, dv_part;
+  if (group > 1) {
+    dk_part = at::empty({group, B, S, Hkv, D}, q.options().dtype(at::kFloat));
+    dv_part = at::empty({group, B, S, Hkv, D}, q.options().dtype(at::kFloat));
+  }
   auto stream = c10::hip::getCurrentHIPStream();
   const int64_t rows = (int64_t)B * S * Hq;
   auto dop = reinterpret_cast<const bf16*>(dout.data_ptr());
@@ -619,20 +742,29 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
   DLGM_CHECK_HIP(hipGetLastError());
   BwdParams p{reinterpret_cast<const bf16*>(q.data_ptr()), reinterpret_cast<const bf16*>(k.data_ptr()),
               reinterpret_cast<const bf16*>(v.data_ptr()), dop, lse.data_ptr<float>(), delta.data_ptr<float>(),
-              dq32.data_ptr<float>(), reinterpret_cast<bf16*>(dk.data_ptr()), reinterpret_cast<bf16*>(dv.data_ptr()),
-              q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2), v.stride(0), v.stride(1),
-              v.stride(2), dout.stride(0), dout.stride(1), dout.stride(2), B, S, Hq, Hkv, (float)softmax_scale,
-              (float)(softmax_scale * kLog2e), causal};
-  const int nkt = (S + kBwdBKV - 1) / kBwdBKV;
-  const int64_t blocks = (int64_t)nkt * B * Hkv;
-  if (D == 128)
-    flash_bwd_kernel<128><<<blocks, kBwdThreads, 0, stream>>>(p);
-  else
-    flash_bwd_kernel<64><<<blocks, kBwdThreads, 0, stream>>>(p);
+              reinterpret_cast<bf16*>(dq.data_ptr()), group > 1 ? dk_part.data_ptr<float>() : nullptr,
+              group > 1 ? dv_part.data_ptr<float>() : nullptr, reinterpret_cast<bf16*>(dk.data_ptr()),
+              reinterpret_cast<bf16*>(dv.data_ptr()), q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1),
+              k.stride(2), v.stride(0), v.stride(1), v.stride(2), dout.stride(0), dout.stride(1), dout.stride(2), B, S,
+              Hq, Hkv, (float)softmax_scale, (float)(softmax_scale * kLog2e), causal};
+  const int64_t kv_blocks = (int64_t)B * Hq * ((S + kKvBKV - 1) / kKvBKV);
+  const int64_t dq_blocks = (int64_t)B * Hq * ((S + kDqBQ - 1) / kDqBQ);
+  if (D == 128) {
+    flash_bwd_dkdv_kernel<128><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+    flash_bwd_dq_kernel<128><<<dq_blocks, kDqThreads, 0, stream>>>(p);
+  } else {
+    flash_bwd_dkdv_kernel<64><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+    flash_bwd_dq_kernel<64><<<dq_blocks, kDqThreads, 0, stream>>>(p);
+  }
   DLGM_CHECK_HIP(hipGetLastError());
-  const int64_t n = dq32.numel();
-  f32_to_bf16_rows_kernel<<<std::min<int64_t>((n / 8 + 255) / 256, 4096), 256, 0, stream>>>(
-      dq32.data_ptr<float>(), reinterpret_cast<bf16*>(dq.data_ptr()), n);
-  DLGM_CHECK_HIP(hipGetLastError());
+  if (group > 1) {
+    const int64_t n = (int64_t)B * S * Hkv * D;
+    const int64_t grid = std::min<int64_t>((n / 8 + 255) / 256, 4096);
+    gqa_reduce_kernel<<<grid, 256, 0, stream>>>(dk_part.data_ptr<float>(), reinterpret_cast<bf16*>(dk.data_ptr()),
+                                                group, n);
+    gqa_reduce_kernel<<<grid, 256, 0, stream>>>(dv_part.data_ptr<float>(), reinterpret_cast<bf16*>(dv.data_ptr()),
+                                                group, n);
+    DLGM_CHECK_HIP(hipGetLastError());
+  }
   return {dq, dk, dv};
 }

@@ -1,0 +1,244 @@
+"""Job registry + per-job supervisor: process ownership, log draining, heartbeat, auto-resume, MTTR.
+
+The reference starts ``deepspeed`` with ``subprocess.Popen(stdout=PIPE, stderr=PIPE)``
+and drops the handle (``ai_engine/deepspeed_launcher.py:354-362``): no registry, no
+exit code, pipes never drained (the child blocks once ~64 KiB of output accumulate)
+and the README's auto-resume claim (``README.md:14``) has no implementation. Here:
+
+* every job runs in its own process group (``start_new_session``) so the whole rank
+  tree can be signalled (spot notice -> SIGUSR1, cancel -> SIGTERM/SIGKILL);
+* stdout/stderr go to ``<run_dir>/job.log`` (no pipes to fill up);
+* the training ranks publish progress to ``<run_dir>/status.json``
+  (``DLGM_STATUS_FILE``): a stale heartbeat is treated like a crash;
+* on a non-zero exit (SIGKILL'd rank, NaN halt = exit code 3, hang) the supervisor
+  relaunches the job with ``--resume=auto`` (the engine rolls back to the newest
+  checkpoint tag whose manifest verifies) up to ``max_restarts`` times, and records
+  MTTR = time of the first completed step after the restart - time the failure was
+  detected.
+"""
+from __future__ import annotations
+
+import json
+import os
+import signal
+import subprocess
+import tempfile
+import threading
+import time
+from dataclasses import asdict, dataclass, field
+from typing import Dict, List, Optional
+
+EXIT_NAN_HALT = 3
+EXIT_PREEMPTED = 4
+
+
+@dataclass
+class JobSpec:
+    job_id: str
+    argv: List[str]
+    env: Dict[str, str] = field(default_factory=dict)
+    auto_resume: bool = True
+    max_restarts: int = 3
+    save_dir: Optional[str] = None
+    run_dir: Optional[str] = None
+    heartbeat_timeout_s: float = 0.0  # 0 = disabled
+    resume_arg: str = "--resume=auto"
+    restart_on_preempt: bool = False
+
+
+class Job:
+    def __init__(self, spec: JobSpec):
+        self.spec = spec
+        self.run_dir = spec.run_dir or os.path.join(tempfile.gettempdir(), "dlgm_jobs", spec.job_id)
+        os.makedirs(self.run_dir, exist_ok=True)
+        self.log_path = os.path.join(self.run_dir, "job.log")
+        self.status_path = os.path.join(self.run_dir, "status.json")
+        self.status = "pending"
+        self.pid: Optional[int] = None
+        self.restarts = 0
+        self.exit_codes: List[int] = []
+        self.events: List[Dict] = []
+        self.mttr_s: List[float] = []
+        self.created = time.time()
+        self.ended: Optional[float] = None
+        self._proc: Optional[subprocess.Popen] = None
+        self._cancel = threading.Event()
+        self._lock = threading.Lock()
+
+    def event(self, kind: str, **kw) -> None:
+        with self._lock:
+            self.events.append({"t": time.time(), "event": kind, **kw})
+
+    def progress(self) -> Optional[Dict]:
+        try:
+            with open(self.status_path) as f:
+                return json.load(f)
+        except (OSError, ValueError):
+            return None
+
+    def to_dict(self) -> Dict:
+        return {
+            "job_id": self.spec.job_id, "status": self.status, "pid": self.pid, "restarts": self.restarts,
+            "exit_codes": list(self.exit_codes), "log_path": self.log_path, "run_dir": self.run_dir,
+            "mttr_s": list(self.mttr_s), "events": list(self.events[-50:]), "progress": self.progress(),
+            "command": self.spec.argv, "created": self.created, "ended": self.ended,
+        }
+
+
+class Supervisor(threading.Thread):
+    def __init__(self, job: Job, poll_s: float = 0.2):
+        super().__init__(daemon=True, name=f"supervisor-{job.spec.job_id}")
+        self.job = job
+        self.poll_s = poll_s
+
+    def _start(self, resume: bool) -> subprocess.Popen:
+        spec = self.job.spec
+        argv = list(spec.argv)
+        if resume and spec.resume_arg not in argv:
+            argv.append(spec.resume_arg)
+        env = {**os.environ, **spec.env, "DLGM_STATUS_FILE": self.job.status_path, "DLGM_JOB_ID": spec.job_id,
+               "DLGM_RESTART": str(self.job.restarts)}
+        if spec.save_dir:
+            env["DLGM_SAVE_DIR"] = spec.save_dir
+        log = open(self.job.log_path, "ab", buffering=0)
+        try:
+            proc = subprocess.Popen(argv, stdout=log, stderr=subprocess.STDOUT, env=env, start_new_session=True)
+        finally:
+            log.close()
+        self.job.pid = proc.pid
+        self.job._proc = proc
+        self.job.status = "running"
+        self.job.event("started", pid=proc.pid, resume=resume)
+        return proc
+
+    def _kill_group(self, proc: subprocess.Popen, grace_s: float = 10.0) -> None:
+        try:
+            os.killpg(proc.pid, signal.SIGTERM)
+        except ProcessLookupError:
+            return
+        t0 = time.time()
+        while proc.poll() is None and time.time() - t0 < grace_s:
+            time.sleep(0.05)
+        if proc.poll() is None:
+            try:
+                os.killpg(proc.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+            proc.wait()
+
+    def run(self) -> None:
+        job, spec = self.job, self.job.spec
+        proc = self._start(resume=False)
+        failure_t: Optional[float] = None
+        step_at_failure = -1
+        while True:
+            rc = proc.poll()
+            prog = job.progress()
+            if failure_t is not None and prog and prog.get("step", -1) > step_at_failure and \
+                    prog.get("restart", 0) == job.restarts and prog.get("time", 0) >= failure_t:
+                job.mttr_s.append(prog["time"] - failure_t)
+                job.event("recovered", mttr_s=job.mttr_s[-1], step=prog.get("step"))
+                failure_t = None
+            if rc is None and spec.heartbeat_timeout_s > 0 and prog and \
+                    time.time() - prog.get("time", time.time()) > spec.heartbeat_timeout_s:
+                job.event("heartbeat_lost", last=prog.get("time"))
+                self._kill_group(proc, grace_s=2.0)
+                rc = proc.poll() if proc.poll() is not None else -9
+            if job._cancel.is_set():
+                self._kill_group(proc)
+                job.status = "cancelled"
+                break
+            if rc is None:
+                time.sleep(self.poll_s)
+                continue
+            job.exit_codes.append(rc)
+            job.event("exited", rc=rc)
+            if rc == 0:
+                job.status = "succeeded"
+                break
+            preempted = rc == EXIT_PREEMPTED
+            if preempted and not spec.restart_on_preempt:
+                job.status = "preempted"
+                break
+            if spec.auto_resume and job.restarts < spec.max_restarts:
+                # make sure no straggler rank of the failed attempt survives
+                try:
+                    os.killpg(proc.pid, signal.SIGKILL)
+                except (ProcessLookupError, PermissionError):
+                    pass
+                failure_t = time.time()
+                step_at_failure = (prog or {}).get("step", -1)
+                job.restarts += 1
+                job.status = "restarting"
+                job.event("restarting", attempt=job.restarts, reason="nan_halt" if rc == EXIT_NAN_HALT else "crash")
+                proc = self._start(resume=True)
+                continue
+            job.status = "failed"
+            break
+        job.ended = time.time()
+
+
+class JobRegistry:
+    """Thread-safe registry of supervised jobs (process-global via :func:`default_registry`)."""
+
+    def __init__(self):
+        self._jobs: Dict[str, Job] = {}
+        self._lock = threading.Lock()
+
+    def submit(self, spec: JobSpec) -> Job:
+        job = Job(spec)
+        sup = Supervisor(job)
+        # start the first attempt synchronously so launch errors (missing binary) surface to the caller
+        proc = sup._start(resume=False)
+        sup._start = (lambda first=[proc], orig=sup._start: (lambda resume: first.pop() if first else orig(resume)))()
+        with self._lock:
+            self._jobs[spec.job_id] = job
+        sup.start()
+        return job
+
+    def get(self, job_id: str) -> Optional[Job]:
+        with self._lock:
+            return self._jobs.get(job_id)
+
+    def list(self) -> List[Job]:
+        with self._lock:
+            return list(self._jobs.values())
+
+    def cancel(self, job_id: str) -> bool:
+        job = self.get(job_id)
+        if job is None:
+            return False
+        job._cancel.set()
+        return True
+
+    def signal(self, job_id: str, sig: int) -> bool:
+        job = self.get(job_id)
+        if job is None or job.pid is None:
+            return False
+        try:
+            os.killpg(job.pid, sig)
+            return True
+        except ProcessLookupError:
+            return False
+
+
+_DEFAULT: Optional[JobRegistry] = None
+
+
+def default_registry() -> JobRegistry:
+    global _DEFAULT
+    if _DEFAULT is None:
+        _DEFAULT = JobRegistry()
+    return _DEFAULT
+
+
+def write_status(step: int, **kw) -> None:
+    """Called by training rank 0 after each completed step (atomic replace)."""
+    path = os.environ.get("DLGM_STATUS_FILE")
+    if not path:
+        return
+    rec = {"step": step, "time": time.time(), "restart": int(os.environ.get("DLGM_RESTART", "0")), **kw}
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump(rec, f)
+    os.replace(tmp, path)
