@@ -1,0 +1,119 @@
+"""Multi-process ZeRO equivalence on CPU/gloo (the "multi-node without a cluster" fake).
+
+W=2 ranks x GA=1 (each rank a different micro-batch) must produce the same
+parameters as W=1 x GA=2 over the same two micro-batches, for every ZeRO stage.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from distributed_llm_training_gpu_manager_amd.models import get_config
+from distributed_llm_training_gpu_manager_amd.parallel.comm import Comm
+from distributed_llm_training_gpu_manager_amd.parallel.zero import EngineConfig, ZeroEngine
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _data(model, steps, n_micro):
+    mc = get_config(model)
+    g = torch.Generator().manual_seed(11)
+    return [[torch.randint(0, mc.vocab_size, (2, 33), generator=g) for _ in range(n_micro)] for _ in range(steps)]
+
+
+def _cfg(stage, ga, comm_dtype=torch.float32):
+    return EngineConfig(zero_stage=stage, micro_batch_size=2, seq_len=32, grad_accum=ga, lr=1e-2,
+                        scheduler="constant", init_device="cpu", grad_clip=1.0, comm_dtype=comm_dtype)
+
+
+def _worker(rank, world, port, model, stage, steps, out_path, comm_dtype=torch.float32):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    eng = ZeroEngine(get_config(model), _cfg(stage, 1, comm_dtype), torch.device("cpu"), Comm())
+    losses = []
+    for mbs in _data(model, steps, world):
+        t = mbs[rank]
+        m = eng.train_step([(t[:, :-1], t[:, 1:])])
+        losses.append(float(m["loss"]))
+    params = eng.full_params()
+    if rank == 0:
+        torch.save({"params": params, "losses": losses}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _single(model, stage, steps):
+    eng = ZeroEngine(get_config(model), _cfg(stage, 2), torch.device("cpu"))
+    losses = []
+    for mbs in _data(model, steps, 2):
+        m = eng.train_step([(t[:, :-1], t[:, 1:]) for t in mbs])
+        losses.append(float(m["loss"]))
+    return eng.full_params(), losses
+
+
+@pytest.mark.parametrize("stage", [0, 1, 2, 3])
+@pytest.mark.parametrize("model", ["llama-tiny"])
+def test_zero_stage_world2_matches_single(tmp_path, stage, model):
+    out = str(tmp_path / "w2.pt")
+    mp.spawn(_worker, args=(2, _free_port(), model, stage, 2, out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    ref_params, ref_losses = _single(model, stage, 2)
+    # the world-2 loss is rank 0's own micro-batch; compare the parameters, which see both
+    for k, v in ref_params.items():
+        err = float((got["params"][k] - v).abs().max() / v.abs().max().clamp_min(1e-6))
+        assert err < 2e-2, (k, err)
+
+
+def test_gpt2_zero1_world2(tmp_path):
+    """BASELINE config 1 shape: GPT-2 family under ZeRO-1 on gloo (tied embeddings)."""
+    out = str(tmp_path / "g.pt")
+    mp.spawn(_worker, args=(2, _free_port(), "gpt2-tiny", 1, 2, out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    ref_params, _ = _single("gpt2-tiny", 1, 2)
+    for k, v in ref_params.items():
+        err = float((got["params"][k] - v).abs().max() / v.abs().max().clamp_min(1e-6))
+        assert err < 2e-2, (k, err)
+
+
+def _grad_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = ZeroEngine(get_config("llama-tiny"), _cfg(3, 1, torch.bfloat16), torch.device("cpu"), Comm())
+    t = _data("llama-tiny", 1, world)[0][rank]
+    eng.micro_step(t[:, :-1], t[:, 1:], first=True, last=True)
+    shards = [torch.empty_like(eng.grad_shard) for _ in range(world)]
+    dist.all_gather(shards, eng.grad_shard)
+    if rank == 0:
+        torch.save({"shards": shards}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_zero3_world2_bf16_comm_gradients(tmp_path):
+    """The GPU default path: bf16 reduce-scatter of each flat gradient segment, fp32 accumulation.
+
+    Compared on the gradients (Adam amplifies the sign of near-cancelling grads, so parameters
+    after a step are not a meaningful bf16-vs-fp32 comparison).
+    """
+    out = str(tmp_path / "b.pt")
+    mp.spawn(_grad_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    shards = torch.load(out, weights_only=True)["shards"]
+    eng = ZeroEngine(get_config("llama-tiny"), _cfg(3, 2), torch.device("cpu"))
+    for i, t in enumerate(_data("llama-tiny", 1, 2)[0]):
+        eng.micro_step(t[:, :-1], t[:, 1:], first=i == 0, last=i == 1)
+    for g in eng.groups:
+        ref = eng.grad_shard.narrow(0, g.shard_off, g.shard_numel)
+        half = g.shard_numel // 2
+        got = torch.cat([shards[r].narrow(0, g.shard_off // 2, half) for r in range(2)])
+        err = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-8))
+        assert err < 2e-2, (g.name, err)
