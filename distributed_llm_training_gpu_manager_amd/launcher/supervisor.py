@@ -86,10 +86,11 @@ class Job:
 
 
 class Supervisor(threading.Thread):
-    def __init__(self, job: Job, poll_s: float = 0.2):
+    def __init__(self, job: Job, poll_s: float = 0.2, first_proc: Optional[subprocess.Popen] = None):
         super().__init__(daemon=True, name=f"supervisor-{job.spec.job_id}")
         self.job = job
         self.poll_s = poll_s
+        self._first = first_proc
 
     def _start(self, resume: bool) -> subprocess.Popen:
         spec = self.job.spec
@@ -128,9 +129,10 @@ class Supervisor(threading.Thread):
 
     def run(self) -> None:
         job, spec = self.job, self.job.spec
-        proc = self._start(resume=False)
+        proc = self._first if self._first is not None else self._start(resume=False)
         failure_t: Optional[float] = None
         step_at_failure = -1
+        attempt_t0 = time.time()
         while True:
             rc = proc.poll()
             prog = job.progress()
@@ -139,8 +141,11 @@ class Supervisor(threading.Thread):
                 job.mttr_s.append(prog["time"] - failure_t)
                 job.event("recovered", mttr_s=job.mttr_s[-1], step=prog.get("step"))
                 failure_t = None
-            if rc is None and spec.heartbeat_timeout_s > 0 and prog and \
-                    time.time() - prog.get("time", time.time()) > spec.heartbeat_timeout_s:
+            # heartbeat: only records of the current attempt count, measured from the attempt start
+            last_beat = max(attempt_t0, prog.get("time", 0)) if prog and prog.get("restart", 0) == job.restarts \
+                else attempt_t0
+            if rc is None and spec.heartbeat_timeout_s > 0 and prog is not None and \
+                    time.time() - last_beat > spec.heartbeat_timeout_s:
                 job.event("heartbeat_lost", last=prog.get("time"))
                 self._kill_group(proc, grace_s=2.0)
                 rc = proc.poll() if proc.poll() is not None else -9
@@ -172,6 +177,7 @@ class Supervisor(threading.Thread):
                 job.status = "restarting"
                 job.event("restarting", attempt=job.restarts, reason="nan_halt" if rc == EXIT_NAN_HALT else "crash")
                 proc = self._start(resume=True)
+                attempt_t0 = time.time()
                 continue
             job.status = "failed"
             break
@@ -187,10 +193,9 @@ class JobRegistry:
 
     def submit(self, spec: JobSpec) -> Job:
         job = Job(spec)
-        sup = Supervisor(job)
         # start the first attempt synchronously so launch errors (missing binary) surface to the caller
-        proc = sup._start(resume=False)
-        sup._start = (lambda first=[proc], orig=sup._start: (lambda resume: first.pop() if first else orig(resume)))()
+        proc = Supervisor(job)._start(resume=False)
+        sup = Supervisor(job, first_proc=proc)
         with self._lock:
             self._jobs[spec.job_id] = job
         sup.start()

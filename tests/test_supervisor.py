@@ -1,0 +1,80 @@
+"""Job supervisor: log draining, exit codes, auto-resume with MTTR, cancel, heartbeat loss."""
+import json
+import os
+import sys
+import textwrap
+import time
+
+from distributed_llm_training_gpu_manager_amd.launcher.supervisor import JobRegistry, JobSpec
+
+
+def _script(tmp_path, body: str) -> str:
+    p = tmp_path / "job.py"
+    p.write_text(textwrap.dedent(body))
+    return str(p)
+
+
+FAKE_TRAIN = """
+import json, os, sys, time
+resume = "--resume=auto" in sys.argv
+state = os.path.join(os.path.dirname(os.environ["DLGM_STATUS_FILE"]), "ckpt_step")
+start = int(open(state).read()) if resume and os.path.exists(state) else 0
+for step in range(start + 1, 7):
+    time.sleep(0.05)
+    open(state, "w").write(str(step))
+    from distributed_llm_training_gpu_manager_amd.launcher.supervisor import write_status
+    write_status(step, loss=1.0 / step)
+    print("step", step, flush=True)
+    if step == 3 and not resume:
+        os.kill(os.getpid(), 9)   # mid-run SIGKILL
+sys.exit(0)
+"""
+
+
+def _wait(job, states, timeout=30):
+    t0 = time.time()
+    while job.status not in states and time.time() - t0 < timeout:
+        time.sleep(0.05)
+    return job.status
+
+
+def test_sigkill_auto_resume_measures_mttr(tmp_path):
+    reg = JobRegistry()
+    env = {"PYTHONPATH": os.path.dirname(os.path.dirname(os.path.abspath(__file__)))}
+    job = reg.submit(JobSpec(job_id="j1", argv=[sys.executable, _script(tmp_path, FAKE_TRAIN)], env=env,
+                             run_dir=str(tmp_path / "run")))
+    assert _wait(job, ("succeeded", "failed")) == "succeeded", open(job.log_path).read()
+    assert job.restarts == 1 and job.exit_codes[0] == -9 and job.exit_codes[-1] == 0
+    assert len(job.mttr_s) == 1 and 0 < job.mttr_s[0] < 20
+    log = open(job.log_path).read()
+    assert "step 3" in log and "step 6" in log  # drained to file, resumed after step 3
+    assert any(e["event"] == "recovered" for e in job.to_dict()["events"])
+
+
+def test_failure_without_resume_and_cancel(tmp_path):
+    reg = JobRegistry()
+    job = reg.submit(JobSpec(job_id="j2", argv=[sys.executable, "-c", "import sys; sys.exit(5)"], auto_resume=False,
+                             run_dir=str(tmp_path / "r2")))
+    assert _wait(job, ("failed",)) == "failed" and job.exit_codes == [5]
+    job3 = reg.submit(JobSpec(job_id="j3", argv=[sys.executable, "-c", "import time; time.sleep(60)"],
+                              run_dir=str(tmp_path / "r3")))
+    time.sleep(0.3)
+    assert reg.cancel("j3")
+    assert _wait(job3, ("cancelled",)) == "cancelled"
+
+
+def test_heartbeat_loss_triggers_restart(tmp_path):
+    reg = JobRegistry()
+    body = """
+    import os, sys, time
+    from distributed_llm_training_gpu_manager_amd.launcher.supervisor import write_status
+    write_status(1)
+    if "--resume=auto" not in sys.argv:
+        time.sleep(60)   # hang
+    write_status(2)
+    """
+    env = {"PYTHONPATH": os.path.dirname(os.path.dirname(os.path.abspath(__file__)))}
+    job = reg.submit(JobSpec(job_id="j4", argv=[sys.executable, _script(tmp_path, body)], env=env,
+                             heartbeat_timeout_s=1.0, run_dir=str(tmp_path / "r4")))
+    assert _wait(job, ("succeeded", "failed")) == "succeeded"
+    assert job.restarts == 1 and any(e["event"] == "heartbeat_lost" for e in job.events)
