@@ -1,0 +1,66 @@
+"""Consume a DeepSpeed-schema JSON (as emitted by :func:`launcher.config.generate_config`) into EngineConfig.
+
+Every key the reference's generator writes (``ai_engine/deepspeed_launcher.py:124-238``)
+is either honoured or explicitly reported as not applicable on MI355X.
+"""
+from __future__ import annotations
+
+import json
+from typing import Any, Dict, List, Tuple, Union
+
+import torch
+
+from ..parallel.zero import EngineConfig
+
+
+def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, **overrides) -> Tuple[EngineConfig, List[str]]:
+    if isinstance(ds, str):
+        with open(ds) as f:
+            ds = json.load(f)
+    notes: List[str] = []
+    zo = ds.get("zero_optimization", {})
+    opt = ds.get("optimizer", {}).get("params", {})
+    sch = ds.get("scheduler", {})
+    sp = sch.get("params", {})
+    fp16 = ds.get("fp16", {}).get("enabled", False)
+    bf16 = ds.get("bf16", {}).get("enabled", False)
+    if fp16 and not bf16:
+        notes.append("fp16 requested: MI355X engine computes in bf16 and keeps the dynamic loss scaler")
+    comm = ds.get("communication_data_type", "bf16")
+    comm_dtype = {"fp32": torch.float32, "float32": torch.float32}.get(comm, torch.bfloat16)
+    if comm in ("fp16", "float16"):
+        notes.append("communication_data_type fp16 mapped to bf16 (A20)")
+    off_o = zo.get("offload_optimizer", {}).get("device", "none")
+    off_p = zo.get("offload_param", {}).get("device", "none")
+    if off_p != "none":
+        notes.append(f"offload_param={off_p}: not needed on MI355X (288 GB HBM); parameters stay in HBM")
+    act = ds.get("activation_checkpointing")
+    cfg = EngineConfig(
+        zero_stage=int(zo.get("stage", 0)),
+        micro_batch_size=int(ds.get("train_micro_batch_size_per_gpu", 1)),
+        seq_len=seq_len,
+        grad_accum=int(ds.get("gradient_accumulation_steps", 1)),
+        lr=float(opt.get("lr", sp.get("warmup_max_lr", 3e-5))),
+        betas=tuple(opt.get("betas", (0.9, 0.999))),
+        eps=float(opt.get("eps", 1e-8)),
+        weight_decay=float(opt.get("weight_decay", 0.01)),
+        grad_clip=float(ds.get("gradient_clipping", 0.0)),
+        scheduler=sch.get("type", "constant"),
+        warmup_steps=int(sp.get("warmup_num_steps", 0)),
+        total_steps=int(sp.get("total_num_steps", 10 ** 9)),
+        warmup_min_lr=float(sp.get("warmup_min_lr", 0.0)),
+        warmup_type=sp.get("warmup_type", "log"),
+        comm_dtype=comm_dtype,
+        activation_checkpointing=bool(act),
+        cpu_checkpointing=bool(act and act.get("cpu_checkpointing", False)),
+        fp16=bool(fp16 and not bf16),
+        loss_scale=float(ds.get("fp16", {}).get("loss_scale", 0.0)),
+        initial_scale_power=int(ds.get("fp16", {}).get("initial_scale_power", 16)),
+        loss_scale_window=int(ds.get("fp16", {}).get("loss_scale_window", 1000)),
+        hysteresis=int(ds.get("fp16", {}).get("hysteresis", 2)),
+        min_loss_scale=float(ds.get("fp16", {}).get("min_loss_scale", 1.0)),
+        offload_optimizer=off_o,
+    )
+    for k, v in overrides.items():
+        setattr(cfg, k, v)
+    return cfg, notes

@@ -1,0 +1,228 @@
+"""Training loop: the script the launcher runs on every rank (``python -m distributed_llm_training_gpu_manager_amd.train``).
+
+Contract kept from DeepSpeed scripts: it takes ``--deepspeed_config=<json>`` (the
+file written by the launcher) and reads ``RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*`` from
+the environment (``torch.distributed.run``). Everything the reference delegates to a
+user script is here: synthetic data, the ZeRO engine, in-process
+loss monitoring, the NaN trap, async checkpoints, auto-resume and spot preemption.
+
+Exit codes (read by the supervisor): 0 done, 3 NaN/Inf halt, 4 preempted (emergency
+checkpoint written). Rank 0 publishes per-step progress to ``DLGM_STATUS_FILE``.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import signal
+import sys
+import threading
+import time
+import urllib.request
+from typing import Any, Dict, List, Optional, Tuple
+
+import torch
+
+from ..ckpt.checkpoint import AsyncCheckpointer, export_consolidated
+from ..health.loss_monitor import LossSpikeMonitor, MonitorConfig, TrainingMetrics
+from ..health.nan_trap import NanTrap
+from ..launcher.supervisor import EXIT_NAN_HALT, EXIT_PREEMPTED, write_status
+from ..models import get_config
+from ..parallel.comm import Comm, init_distributed
+from ..parallel.zero import EngineConfig, ZeroEngine
+from .dsconfig import engine_config_from_ds
+
+
+class SyntheticData:
+    """Deterministic random token batches: (seed, rank, step, micro) -> the same tokens after a restart."""
+
+    def __init__(self, vocab: int, mbs: int, seq: int, ga: int, seed: int, rank: int, device: torch.device):
+        self.vocab, self.mbs, self.seq, self.ga = vocab, mbs, seq, ga
+        self.seed, self.rank, self.device = seed, rank, device
+        self.gen = torch.Generator(device=device)
+
+    def batches(self, step: int) -> List[Tuple[torch.Tensor, torch.Tensor]]:
+        out = []
+        for mi in range(self.ga):
+            self.gen.manual_seed(((self.seed * 1_000_003 + self.rank) * 1_000_003 + step) * 131 + mi)
+            toks = torch.randint(0, self.vocab, (self.mbs, self.seq + 1), device=self.device, generator=self.gen)
+            out.append((toks[:, :-1].contiguous(), toks[:, 1:].contiguous()))
+        return out
+
+
+class MetricsPusher:
+    """Best-effort, non-blocking POST of TrainingMetrics to the control plane's /monitoring/ingest."""
+
+    def __init__(self, url: Optional[str], job_id: str):
+        self.url, self.job_id = url, job_id
+        self._buf: List[Dict[str, Any]] = []
+        self._lock = threading.Lock()
+
+    def push(self, m: Dict[str, Any]) -> None:
+        if not self.url:
+            return
+        with self._lock:
+            self._buf.append(m)
+            batch, self._buf = self._buf, []
+        threading.Thread(target=self._send, args=(batch,), daemon=True).start()
+
+    def _send(self, batch) -> None:
+        body = json.dumps({"job_id": self.job_id, "metrics": batch}).encode()
+        req = urllib.request.Request(self.url.rstrip("/") + "/api/v1/monitoring/ingest", data=body,
+                                     headers={"content-type": "application/json"}, method="POST")
+        try:
+            urllib.request.urlopen(req, timeout=2).read()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class Trainer:
+    def __init__(self, args: argparse.Namespace):
+        self.args = args
+        self.env = init_distributed(args.device)
+        self.comm = Comm()
+        self.mcfg = get_config(args.model, **({"max_seq_len": max(args.seq_len, 1)} if args.seq_len else {}))
+        if args.deepspeed_config:
+            self.ecfg, self.notes = engine_config_from_ds(args.deepspeed_config, args.seq_len, seed=args.seed)
+        else:
+            self.ecfg, self.notes = EngineConfig(zero_stage=args.zero_stage, micro_batch_size=args.micro_batch,
+                                                 seq_len=args.seq_len, grad_accum=args.grad_accum, lr=args.lr,
+                                                 seed=args.seed), []
+        if args.lr_scale != 1.0:
+            self.ecfg.lr *= args.lr_scale
+        self.engine = ZeroEngine(self.mcfg, self.ecfg, self.env.device, self.comm)
+        self.monitor = LossSpikeMonitor(MonitorConfig())
+        self.trap = NanTrap(self.env.device, self.monitor)
+        save_dir = args.save_dir or os.environ.get("DLGM_SAVE_DIR")
+        self.ckpt = AsyncCheckpointer(self.engine, save_dir, mode=args.ckpt_mode) if save_dir else None
+        self.data = SyntheticData(self.mcfg.vocab_size, self.ecfg.micro_batch_size, args.seq_len,
+                                  self.ecfg.grad_accum, args.seed, self.env.rank, self.env.device)
+        self.pusher = MetricsPusher(args.metrics_url if self.env.rank == 0 else None,
+                                    os.environ.get("DLGM_JOB_ID", args.job_id))
+        self.preempt = False
+        signal.signal(signal.SIGUSR1, self._on_preempt)
+        signal.signal(signal.SIGTERM, self._on_preempt)
+        self.log: List[Dict[str, Any]] = []
+
+    def _on_preempt(self, signum, frame) -> None:
+        self.preempt = True
+
+    def _say(self, msg: str) -> None:
+        if self.env.rank == 0:
+            print(f"[train] {msg}", flush=True)
+
+    def _sync_flag(self, flag: bool) -> bool:
+        """All ranks agree on a host-side flag (preemption signals may reach ranks at different steps)."""
+        if self.comm.world == 1:
+            return flag
+        t = torch.tensor([1.0 if flag else 0.0], device=self.env.device)
+        self.comm.all_reduce_max(t)
+        return bool(t.item() > 0)
+
+    def run(self) -> int:
+        a = self.args
+        start = 0
+        if self.ckpt is not None and a.resume not in ("none", ""):
+            t0 = time.time()
+            cs = self.ckpt.load("auto" if a.resume in ("auto", "latest") else a.resume)
+            if cs is not None:
+                start = int(cs.get("step", self.engine.step_count))
+                self._say(f"resumed from step {start} in {time.time() - t0:.2f}s "
+                          f"(rollbacks: {getattr(self.ckpt, 'rollbacks', [])})")
+                self.monitor.reset()
+        for n in self.notes:
+            self._say(f"note: {n}")
+        tokens_step = self.ecfg.micro_batch_size * a.seq_len * self.ecfg.grad_accum * self.env.world
+        t_last = time.time()
+        rc = 0
+        for step in range(start + 1, a.steps + 1):
+            if a.inject_nan_step == step:
+                self.engine.fault_inject_nan = True
+            m = self.engine.train_step(self.data.batches(step))
+            self.trap.record(step, self.engine.stats)
+            # deterministic halt decision: every rank reads the (all-reduced) stats of THIS step
+            bad = float(self.engine.stats[1].item())
+            now = time.time()
+            loss = float(m["loss"])
+            rec = {"step": step, "loss": loss, "grad_norm": float(m["grad_norm"]), "lr": m["lr"],
+                   "step_s": now - t_last, "tokens_per_sec": tokens_step / max(now - t_last, 1e-9)}
+            t_last = now
+            self.log.append(rec)
+            if self.env.rank == 0:
+                write_status(step, loss=loss, nonfinite=bad)
+                alerts = self.monitor.ingest(TrainingMetrics(step=step, loss=loss, learning_rate=m["lr"],
+                                                             gradient_norm=rec["grad_norm"],
+                                                             tokens_per_sec=rec["tokens_per_sec"]))
+                self.pusher.push({"step": step, "loss": loss if math.isfinite(loss) else 1e30,
+                                  "learning_rate": m["lr"], "gradient_norm": rec["grad_norm"]
+                                  if math.isfinite(rec["grad_norm"]) else 1e30})
+                if step % a.log_interval == 0 or alerts:
+                    self._say(json.dumps(rec) + ("" if not alerts else f" alerts={[x.alert_type for x in alerts]}"))
+            first_attempt = os.environ.get("DLGM_RESTART", "0") == "0"
+            if a.kill_at_step == step and first_attempt and self.env.rank == 0:
+                if self.ckpt is not None:
+                    self.ckpt.wait()  # the drill kills after the last interval checkpoint is durable
+                os.kill(os.getpid(), signal.SIGKILL)
+            if a.preempt_at_step == step and first_attempt:
+                os.kill(os.getpid(), signal.SIGUSR1)
+            if bad > 0 and a.halt_on_nan:
+                self._say(f"NaN/Inf gradients at step {step} ({int(bad)} elements): update skipped on device; halting")
+                rc = EXIT_NAN_HALT
+                break
+            if self.ckpt is not None and a.save_interval > 0 and step % a.save_interval == 0:
+                self.ckpt.save(step, client_state={"step": step})
+            if self._sync_flag(self.preempt):
+                t0 = time.time()
+                if self.ckpt is not None:
+                    self.ckpt.save(step, client_state={"step": step, "preempted": True}, blocking=True)
+                self._say(f"preemption: emergency checkpoint at step {step} in {time.time() - t0:.2f}s; exiting")
+                rc = EXIT_PREEMPTED
+                break
+        if self.ckpt is not None:
+            self.ckpt.wait()
+            if rc == 0 and a.export:
+                export_consolidated(self.engine, a.export)
+        self.trap.close()
+        if a.log_json and self.env.rank == 0:
+            with open(a.log_json, "w") as f:
+                json.dump({"log": self.log, "ckpt": self.ckpt.history if self.ckpt else [],
+                           "trap": self.trap.records}, f)
+        if torch.distributed.is_initialized():
+            torch.distributed.destroy_process_group()
+        return rc
+
+
+def parse_args(argv=None) -> argparse.Namespace:
+    ap = argparse.ArgumentParser(description="MI355X ZeRO training (DeepSpeed-config compatible)")
+    ap.add_argument("--deepspeed_config", "--deepspeed-config", default=None)
+    ap.add_argument("--model", default="llama-tiny")
+    ap.add_argument("--seq-len", type=int, default=256)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--device", default="auto")
+    ap.add_argument("--zero-stage", type=int, default=3)
+    ap.add_argument("--micro-batch", type=int, default=1)
+    ap.add_argument("--grad-accum", type=int, default=1)
+    ap.add_argument("--lr", type=float, default=3e-4)
+    ap.add_argument("--lr-scale", type=float, default=1.0)
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--save-dir", default=None)
+    ap.add_argument("--save-interval", type=int, default=0)
+    ap.add_argument("--ckpt-mode", default="auto", choices=["auto", "device", "host"])
+    ap.add_argument("--resume", default="none")
+    ap.add_argument("--export", default=None, help="consolidated bf16 safetensors at the end (16-bit gather on save)")
+    ap.add_argument("--inject-nan-step", type=int, default=-1)
+    ap.add_argument("--kill-at-step", type=int, default=-1, help="fault drill: SIGKILL this rank after the step "
+                    "(first attempt only)")
+    ap.add_argument("--preempt-at-step", type=int, default=-1, help="spot drill: deliver SIGUSR1 after the step")
+    ap.add_argument("--halt-on-nan", type=int, default=1)
+    ap.add_argument("--metrics-url", default=None)
+    ap.add_argument("--job-id", default="local")
+    ap.add_argument("--log-interval", type=int, default=1)
+    ap.add_argument("--log-json", default=None)
+    a, unknown = ap.parse_known_args(argv)
+    return a
+
+
+def main(argv=None) -> int:
+    return Trainer(parse_args(argv)).run()

@@ -72,6 +72,7 @@ class EngineConfig:
     cpu_checkpointing: bool = False
     prefetch: bool = True
     seed: int = 1234
+    offload_optimizer: str = "none"  # none | cpu (ZeRO-Offload parity path, C++ AVX2 AdamW on pinned host state)
     init_device: str = "auto"  # "cpu" gives bit-identical init on any device (tests); auto: cpu below 1e9 params
     fp16: bool = False  # dynamic loss scaling path (reference fp16 block)
     loss_scale: float = 0.0  # 0 = dynamic
@@ -194,8 +195,10 @@ class ZeroEngine:
             self._bwd_last_visit[gi] = min(si, self._bwd_last_visit.get(gi, si))
         self._live: Dict[int, Tuple[torch.Tensor, Handle]] = {}
         self._gbuf_pool: Dict[int, List[torch.Tensor]] = {}
+        self.fault_inject_nan = False  # fault injection: poison one gradient element on the next micro-step
         self.timers: Dict[str, float] = {}
         self.hooks: List[Any] = []  # callables(engine, metrics) after each step (NaN trap, monitors)
+        self.pre_step_hooks: List[Any] = []  # callables(engine) before the optimizer touches master/m/v
 
     # ------------------------------------------------------------------ storage
     def _alloc(self) -> None:
@@ -369,6 +372,9 @@ class ZeroEngine:
                 _, sv = unit.forward(p, sv[1], ctx)
             dy = unit.backward(p, gv, sv, dy, ctx)
             saved[si] = None
+            if self.fault_inject_nan:
+                gbufs[gi][0] = float("nan")
+                self.fault_inject_nan = False
             if self._bwd_last_visit[gi] == si:
                 self._reduce_group_grad(gi, gbufs.pop(gi), first, last, pending)
                 self.release(gi)
@@ -377,7 +383,19 @@ class ZeroEngine:
         self._live.clear() if self.stage == 3 else None
         return loss
 
+    def sync_params_from_master(self) -> None:
+        """Recompute the bf16 compute copies from the fp32 master (after restore / external edits)."""
+        ops.cast_f32_bf16_(self.p16_shard, self.master)
+        if self.stage in (1, 2):
+            hs = [self.comm.all_gather(self.p16_full.narrow(0, g.full_off, g.numel), self._shard16(g), async_op=True)
+                  for g in self.groups]
+            for h in hs:
+                h.wait()
+        self._live.clear()
+
     def optimizer_step(self) -> Dict[str, Any]:
+        for hk in self.pre_step_hooks:
+            hk(self)
         self.step_count += 1
         cfg = self.cfg
         ops.grad_stats([self.grad_shard], self.stats)

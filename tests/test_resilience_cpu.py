@@ -1,0 +1,145 @@
+"""Checkpoint / resume / NaN-trap / spot / auto-resume drills on CPU (BASELINE configs 3-5 plumbing)."""
+import json
+import os
+import signal
+import sys
+import threading
+import time
+from http.server import BaseHTTPRequestHandler, HTTPServer
+
+import pytest
+import torch
+
+from distributed_llm_training_gpu_manager_amd.ckpt.checkpoint import AsyncCheckpointer, complete_tags
+from distributed_llm_training_gpu_manager_amd.ckpt.spot import SpotInstanceResiliencyManager
+from distributed_llm_training_gpu_manager_amd.engine.trainer import Trainer, parse_args
+from distributed_llm_training_gpu_manager_amd.launcher.supervisor import (EXIT_NAN_HALT, EXIT_PREEMPTED,
+                                                                         JobRegistry, JobSpec)
+from distributed_llm_training_gpu_manager_amd.models import get_config
+from distributed_llm_training_gpu_manager_amd.parallel.zero import EngineConfig, ZeroEngine
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _train(tmp, *extra):
+    return Trainer(parse_args(["--seq-len", "32", "--save-dir", str(tmp), "--log-interval", "100", *extra]))
+
+
+def _master(tr):
+    return tr.engine.master.clone()
+
+
+def test_resume_is_bit_exact(tmp_path):
+    a = _train(tmp_path / "a", "--steps", "6")
+    assert a.run() == 0
+    ref = _master(a)
+    b = _train(tmp_path / "b", "--steps", "4", "--save-interval", "2")
+    assert b.run() == 0
+    c = _train(tmp_path / "b", "--steps", "6", "--resume", "auto")
+    assert c.run() == 0
+    assert c.engine.step_count == 6 and torch.equal(_master(c), ref)
+
+
+def test_corrupt_latest_rolls_back(tmp_path):
+    b = _train(tmp_path, "--steps", "4", "--save-interval", "2")
+    b.run()
+    assert complete_tags(str(tmp_path)) == ["global_step2", "global_step4"]
+    f = tmp_path / "global_step4" / "zero_pp_rank_0_mp_rank_00_optim_states.master.bin"
+    data = bytearray(f.read_bytes())
+    data[100] ^= 0xFF
+    f.write_bytes(bytes(data))
+    c = _train(tmp_path, "--steps", "4")
+    cs = c.ckpt.load("auto")
+    assert cs["step"] == 2 and c.engine.step_count == 2 and "checksum" in c.ckpt.rollbacks[0]
+
+
+def test_reshard_world_change(tmp_path):
+    """Elastic restore: a W=1 ZeRO-3 checkpoint loaded into a different partition layout."""
+    mc = get_config("llama-tiny")
+    e1 = ZeroEngine(mc, EngineConfig(zero_stage=3, seq_len=32, init_device="cpu"), torch.device("cpu"))
+    e1.master.normal_()
+    ck = AsyncCheckpointer(e1, str(tmp_path))
+    ck.save(3, {"step": 3}, blocking=True)
+    e2 = ZeroEngine(mc, EngineConfig(zero_stage=3, seq_len=32, init_device="cpu", seed=99), torch.device("cpu"))
+    # fake a different layout by loading through the reshard path explicitly
+    ck2 = AsyncCheckpointer(e2, str(tmp_path))
+    meta = torch.load(tmp_path / "global_step3" / "mp_rank_00_model_states.pt", weights_only=True)
+    mans = {0: json.load(open(tmp_path / "global_step3" / "manifest_r0.json"))}
+    ck2._reshard_from(str(tmp_path / "global_step3"), meta, mans, True)
+    assert torch.equal(e1.master, e2.master)
+
+
+def test_nan_injection_halts_with_code_3(tmp_path):
+    t = _train(tmp_path, "--steps", "6", "--inject-nan-step", "3")
+    before = None
+    rc = t.run()
+    assert rc == EXIT_NAN_HALT
+    assert t.log[-1]["step"] == 3  # halted at the poisoned step: latency 0 steps after detection
+    assert any(a.alert_type == "divergence" for a in t.monitor._all_alerts)
+    assert t.trap.halted and t.trap.trip_step == 3
+
+
+class _Meta(BaseHTTPRequestHandler):
+    notice = False
+
+    def do_PUT(self):
+        self.send_response(200)
+        self.end_headers()
+        self.wfile.write(b"token")
+
+    def do_GET(self):
+        if self.path.endswith("instance-action") and _Meta.notice:
+            self.send_response(200)
+            self.end_headers()
+            self.wfile.write(json.dumps({"action": "terminate", "time": "2026-10-15T00:00:00Z"}).encode())
+        else:
+            self.send_response(404)
+            self.end_headers()
+
+    def log_message(self, *a):
+        pass
+
+
+def test_spot_manager_against_fake_metadata_server():
+    srv = HTTPServer(("127.0.0.1", 0), _Meta)
+    th = threading.Thread(target=srv.serve_forever, daemon=True)
+    th.start()
+    base = f"http://127.0.0.1:{srv.server_port}"
+    got = []
+    mgr = SpotInstanceResiliencyManager(check_interval_sec=0.05, provider="aws", on_preemption=got.append,
+                                        urls={"aws_token": base + "/latest/api/token",
+                                              "aws_action": base + "/latest/meta-data/spot/instance-action"})
+    assert mgr.check_once() is None
+    _Meta.notice = True
+    import asyncio
+    n = asyncio.run(mgr.monitor_preemption_notices(None))
+    assert n["provider"] == "aws" and n["action"] == "terminate" and got
+    srv.shutdown()
+    m2 = SpotInstanceResiliencyManager(provider="gcp", urls={"gcp": base + "/nothing"})
+    m2.simulate = True
+    assert m2.check_once()["provider"] == "simulated"
+
+
+def test_spot_preemption_drill_emergency_checkpoint_and_restore(tmp_path):
+    t = _train(tmp_path, "--steps", "10", "--preempt-at-step", "4")
+    assert t.run() == EXIT_PREEMPTED
+    assert complete_tags(str(tmp_path))[-1] == "global_step4"
+    r = _train(tmp_path, "--steps", "6", "--resume", "auto")
+    assert r.run() == 0 and r.log[0]["step"] == 5
+
+
+def test_supervised_sigkill_auto_resume_mttr(tmp_path):
+    """BASELINE config 4 plumbing: mid-run SIGKILL -> supervisor relaunch -> rollback -> MTTR recorded."""
+    reg = JobRegistry()
+    argv = [sys.executable, "-m", "distributed_llm_training_gpu_manager_amd.train", "--steps", "8",
+            "--seq-len", "32", "--save-interval", "2", "--kill-at-step", "5", "--device", "cpu"]
+    job = reg.submit(JobSpec(job_id="drill", argv=argv, env={"PYTHONPATH": ROOT}, save_dir=str(tmp_path / "ck"),
+                             run_dir=str(tmp_path / "run")))
+    t0 = time.time()
+    while job.status not in ("succeeded", "failed") and time.time() - t0 < 120:
+        time.sleep(0.1)
+    log = open(job.log_path).read()
+    assert job.status == "succeeded", log
+    assert job.exit_codes[0] == -signal.SIGKILL and job.restarts == 1
+    assert "resumed from step 4" in log
+    assert len(job.mttr_s) == 1 and job.mttr_s[0] > 0

@@ -5,9 +5,9 @@ Two libraries are produced next to the Python package:
 
 * ``_dlgm_hip.so``  -- the HIP kernels (csrc/kernels/*.hip) + TORCH_LIBRARY
   registrations (csrc/bindings.cpp), loaded with ``torch.ops.load_library``;
-* ``_dlgm_host.so`` -- the host runtime (csrc/host/*.cpp): pinned-memory
-  checkpoint ring + writer threads, AVX-512 CPU AdamW, NaN-trap watcher. It links
-  only against the HIP runtime (no torch) and is driven through ``ctypes``.
+* ``_dlgm_host.so`` -- the host runtime (csrc/host/*.cpp): multi-threaded
+  checkpoint writer/reader with CRC32C, AVX2/FMA CPU AdamW (ZeRO-Offload). Plain
+  C++ built with g++ (no HIP, no torch), driven through ``ctypes``.
 
 We drive hipcc directly instead of ``torch.utils.cpp_extension`` so that no
 hipify pass ever touches the sources and the objects are always built for
@@ -87,6 +87,33 @@ def _build_lib(name: str, sources: list[Path], cflags: list[str], ldflags: list[
     return out
 
 
+def _build_host(sources: list[Path], jobs: int, verbose: bool, force: bool) -> Path:
+    """Host runtime: plain C++ (g++, no HIP/torch), -O3 with SSE4.2 CRC32C and AVX2/FMA AdamW."""
+    BUILD.mkdir(parents=True, exist_ok=True)
+    cxx = os.environ.get("CXX", "g++")
+    flags = ["-O3", "-std=c++17", "-fPIC", "-fopenmp", "-mavx2", "-mfma", "-Wall", "-Wno-unused-function"]
+    objs, todo = [], []
+    for src in sources:
+        obj = BUILD / f"{src.stem}.host.o"
+        objs.append(obj)
+        if force or not obj.exists() or obj.stat().st_mtime < src.stat().st_mtime:
+            todo.append((src, obj))
+    for src, obj in todo:
+        cmd = [cxx, *flags, "-c", str(src), "-o", str(obj)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"compile failed: {src}\n{res.stderr}")
+    out = PKG / "_dlgm_host.so"
+    if force or todo or not out.exists():
+        cmd = [cxx, "-shared", "-fopenmp", *map(str, objs), "-o", str(out), "-lpthread"]
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"link failed: _dlgm_host.so\n{res.stderr}")
+    return out
+
+
 def build(jobs: int | None = None, verbose: bool = False, force: bool = False) -> list[Path]:
     jobs = jobs or min(8, os.cpu_count() or 4)
     tlib, tinc, abi = _torch_paths()
@@ -100,9 +127,7 @@ def build(jobs: int | None = None, verbose: bool = False, force: bool = False) -
     outs = [_build_lib("_dlgm_hip.so", kern_src, torch_flags, kern_ld, jobs, verbose, force)]
     host_src = sorted((CSRC / "host").glob("*.cpp"))
     if host_src:
-        host_flags = [*common, "-fopenmp", "-mavx2", "-mfma"]
-        host_ld = ["-fopenmp", "-lpthread", f"-L{tlib}", "-lamdhip64", f"-Wl,-rpath,{tlib}"]
-        outs.append(_build_lib("_dlgm_host.so", host_src, host_flags, host_ld, jobs, verbose, force))
+        outs.append(_build_host(host_src, jobs, verbose, force))
     return outs
 
 
