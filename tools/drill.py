@@ -1,0 +1,112 @@
+#!/usr/bin/env python3
+"""Resilience drills on real hardware -> JSON (BASELINE configs 3-5 metrics).
+
+  nan     : inject a NaN gradient at step K -> steps & ms until the job halts (exit 3)
+  sigkill : supervised run, SIGKILL at step K -> auto-resume -> MTTR (failure detected -> first
+            completed step after the restart), plus checkpoint capture / write / restore times
+  spot    : SIGUSR1 at step K (what the spot manager sends) -> emergency checkpoint -> exit 4 ->
+            restore on a fresh process -> first step
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import re
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from distributed_llm_training_gpu_manager_amd.launcher.supervisor import JobRegistry, JobSpec  # noqa: E402
+
+
+def train_argv(a, extra):
+    return [sys.executable, "-m", "distributed_llm_training_gpu_manager_amd.train", "--model", a.model,
+            "--seq-len", str(a.seq), "--micro-batch", "1", "--grad-accum", str(a.ga), "--zero-stage", "3",
+            "--lr", "3e-5", *extra]
+
+
+def run(argv, timeout):
+    t0 = time.time()
+    p = subprocess.run(argv, capture_output=True, text=True, timeout=timeout, cwd=ROOT,
+                       env={**os.environ, "PYTHONPATH": ROOT})
+    return p.returncode, p.stdout + p.stderr, time.time() - t0
+
+
+def drill_nan(a, work):
+    log = os.path.join(work, "nan.json")
+    rc, out, dt = run(train_argv(a, ["--steps", str(a.k + 3), "--inject-nan-step", str(a.k), "--log-json", log]),
+                      a.timeout)
+    d = json.load(open(log)) if os.path.exists(log) else {}
+    steps = [r["step"] for r in d.get("log", [])]
+    trap = d.get("trap", [])
+    return {"drill": "nan", "exit_code": rc, "inject_step": a.k, "last_step_run": steps[-1] if steps else None,
+            "halt_latency_steps": (steps[-1] - a.k) if steps else None,
+            "halt_latency_ms": None if not d.get("log") else round(1000 * d["log"][-1]["step_s"], 1),
+            "trap_records": trap[-3:], "tail": out[-600:]}
+
+
+def drill_sigkill(a, work):
+    ck = os.path.join(work, "ck")
+    reg = JobRegistry()
+    argv = train_argv(a, ["--steps", str(a.k + 2), "--save-interval", str(a.save_interval), "--kill-at-step",
+                          str(a.k), "--log-json", os.path.join(work, "kill.json")])
+    t0 = time.time()
+    job = reg.submit(JobSpec(job_id="sigkill-drill", argv=argv, env={"PYTHONPATH": ROOT}, save_dir=ck,
+                             run_dir=os.path.join(work, "run")))
+    while job.status not in ("succeeded", "failed") and time.time() - t0 < a.timeout:
+        time.sleep(0.2)
+    log = open(job.log_path).read()
+    resumed = re.findall(r"resumed from step (\d+) in ([0-9.]+)s", log)
+    hist = {}
+    if os.path.exists(os.path.join(work, "kill.json")):
+        hist = json.load(open(os.path.join(work, "kill.json"))).get("ckpt", [])
+    return {"drill": "sigkill", "status": job.status, "exit_codes": job.exit_codes, "restarts": job.restarts,
+            "mttr_s": [round(x, 2) for x in job.mttr_s], "resume_load_s": [float(s) for _, s in resumed],
+            "resumed_from_step": [int(s) for s, _ in resumed], "events": job.events, "ckpt_after_resume": hist,
+            "tail": log[-800:]}
+
+
+def drill_spot(a, work):
+    ck = os.path.join(work, "ck_spot")
+    rc, out, dt = run(train_argv(a, ["--steps", str(a.k + 5), "--save-dir", ck, "--preempt-at-step", str(a.k)]),
+                      a.timeout)
+    em = re.findall(r"emergency checkpoint at step (\d+) in ([0-9.]+)s", out)
+    rc2, out2, dt2 = run(train_argv(a, ["--steps", str(a.k + 1), "--save-dir", ck, "--resume", "auto"]), a.timeout)
+    res = re.findall(r"resumed from step (\d+) in ([0-9.]+)s", out2)
+    return {"drill": "spot", "exit_code_preempted": rc, "emergency_ckpt": em, "restore_exit": rc2,
+            "restore": res, "restore_process_wall_s": round(dt2, 2), "tail": (out[-300:], out2[-300:])}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--drills", default="nan,sigkill,spot")
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--seq", type=int, default=8192)
+    ap.add_argument("--ga", type=int, default=1)
+    ap.add_argument("--k", type=int, default=3)
+    ap.add_argument("--save-interval", type=int, default=2)
+    ap.add_argument("--timeout", type=float, default=900)
+    ap.add_argument("--out", default="gpurun_out/drills.json")
+    ap.add_argument("--work", default=None)
+    a = ap.parse_args()
+    work = a.work or tempfile.mkdtemp(prefix="dlgm_drill_")
+    res = {"model": a.model, "seq": a.seq, "ga": a.ga}
+    for d in a.drills.split(","):
+        t0 = time.time()
+        res[d] = {"nan": drill_nan, "sigkill": drill_sigkill, "spot": drill_spot}[d](a, work)
+        res[d]["wall_s"] = round(time.time() - t0, 1)
+        print(json.dumps({k: v for k, v in res[d].items() if k != "tail"})[:2000], flush=True)
+        os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+    shutil.rmtree(work, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()
