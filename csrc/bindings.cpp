@@ -41,6 +41,11 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
                                                                    const at::Tensor& out, const at::Tensor& lse,
                                                                    double softmax_scale, bool causal);
 
+// moe.hip
+at::Tensor dlgm_moe_combine_fwd(const at::Tensor& y, const at::Tensor& pos, const c10::optional<at::Tensor>& gates);
+std::tuple<at::Tensor, at::Tensor> dlgm_moe_combine_bwd(const at::Tensor& dout, const at::Tensor& y,
+                                                        const at::Tensor& pos, const at::Tensor& gates);
+
 TORCH_LIBRARY(dlgm, m) {
   m.def("rmsnorm_fwd(Tensor x, Tensor? residual, Tensor w, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("rmsnorm_bwd(Tensor dy, Tensor h, Tensor w, Tensor rstd, Tensor? dres, Tensor(a!) dw, bool accumulate_dw) -> Tensor");
@@ -53,6 +58,8 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("accumulate_(Tensor(a!) dst, Tensor src, float alpha, float beta) -> ()");
   m.def("cast_f32_bf16_(Tensor(a!) dst, Tensor src) -> ()");
   m.def("flash_attn_fwd(Tensor q, Tensor k, Tensor v, float softmax_scale, bool causal) -> (Tensor, Tensor)");
+  m.def("moe_combine_fwd(Tensor y, Tensor pos, Tensor? gates) -> Tensor");
+  m.def("moe_combine_bwd(Tensor dout, Tensor y, Tensor pos, Tensor gates) -> (Tensor, Tensor)");
   m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, float softmax_scale, bool causal) -> (Tensor, Tensor, Tensor)");
 }
 
@@ -69,4 +76,6 @@ TORCH_LIBRARY_IMPL(dlgm, CUDA, m) {
   m.impl("cast_f32_bf16_", &dlgm_cast_f32_bf16_);
   m.impl("flash_attn_fwd", &dlgm_flash_attn_fwd);
   m.impl("flash_attn_bwd", &dlgm_flash_attn_bwd);
+  m.impl("moe_combine_fwd", &dlgm_moe_combine_fwd);
+  m.impl("moe_combine_bwd", &dlgm_moe_combine_bwd);
 }

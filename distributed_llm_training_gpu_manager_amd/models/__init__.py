@@ -3,7 +3,7 @@ from .config import ModelConfig, PRESETS, get_config
 from .common import ParamSpec, StepContext, Unit, AutogradUnit
 
 
-def build_model(cfg: ModelConfig):
+def build_model(cfg: ModelConfig, ep_rank: int = 0, ep_size: int = 1):
     """Return ``(param_groups, stages)`` for the engine.
 
     param_groups: list of (name, [ParamSpec]) -- one flat ZeRO segment each.
@@ -15,6 +15,7 @@ def build_model(cfg: ModelConfig):
         from .gpt2 import build
     elif cfg.arch == "mixtral":
         from .mixtral import build
+        return build(cfg, ep_rank, ep_size)
     else:
         raise ValueError(f"unknown arch {cfg.arch}")
     return build(cfg)

@@ -20,6 +20,7 @@ backward, i.e. activation checkpointing at unit granularity).
 from __future__ import annotations
 
 import math
+import zlib
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -35,6 +36,8 @@ class ParamSpec:
     init: str = "normal"  # normal | ones | zeros | normal_scaled
     std: float = 0.02
     weight_decay: bool = True
+    experts: int = 0  # >0: leading dim indexes experts; each expert is seeded by its GLOBAL index
+    expert_offset: int = 0
 
     @property
     def numel(self) -> int:
@@ -79,8 +82,17 @@ class Unit:
         return 0.0
 
 
-def init_param(spec: ParamSpec, out: torch.Tensor, gen: torch.Generator) -> None:
-    """Deterministic init into a float32 tensor `out` (flat view of the unit)."""
+def init_param(spec: ParamSpec, out: torch.Tensor, gen: torch.Generator, seed: int = 0) -> None:
+    """Deterministic init into a float32 tensor `out` (flat view of the unit).
+
+    Expert tensors are initialised expert by expert from a seed of the global expert
+    index, so a model sharded over any expert-parallel size starts from the same weights.
+    """
+    if spec.experts and spec.init not in ("ones", "zeros"):
+        for e in range(spec.experts):
+            gen.manual_seed(seed * 7919 + (spec.expert_offset + e) * 104729 + zlib.crc32(spec.name.encode()) % 1000)
+            out[e].normal_(0.0, spec.std, generator=gen)
+        return
     if spec.init == "ones":
         out.fill_(1.0)
     elif spec.init == "zeros":

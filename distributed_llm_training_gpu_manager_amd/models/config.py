@@ -28,6 +28,7 @@ class ModelConfig:
     n_experts: int = 0
     top_k: int = 2
     init_std: float = 0.02
+    router_aux_coef: float = 0.02
     rope_scaling: Optional[dict] = field(default=None, compare=False)
 
     @property

@@ -1,0 +1,178 @@
+"""Mixtral 8x7B (sparse MoE, top-2 of 8 experts) with expert parallelism -- BASELINE config 5.
+
+Attention is the Llama block's (GQA, RoPE theta 1e6). The FFN is a routed mixture:
+
+    logits = hn2 @ Wr^T                   [T, E]   (fp32 softmax)
+    top-2 per token, gates = softmax over the two selected logits (Mixtral)
+    sort (token, k) slots by expert       one gather into expert order
+    EP all-to-all                          rows to the rank owning the expert (RCCL)
+    per local expert: SwiGLU MLP           dense hipBLASLt GEMMs on contiguous rows
+    EP all-to-all back, combine            out[t] = sum_k gate * y[slot]  (HIP gather kernel)
+
+Backward is hand-written: the combine adjoint gives d(expert outputs) and d(gates),
+the expert MLPs run their backward on the expert ranks, the dispatch adjoint is
+again a gather-sum (no atomics), and the router gets the top-k softmax gradient
+plus the Switch/Mixtral load-balancing auxiliary loss gradient
+(coef * E * sum_e f_e * P_e, averaged over layers).
+
+Parameter groups per layer: ``layer{i}`` (attention, norms, router -- ZeRO-sharded
+over all ranks) and ``layer{i}.experts`` (this EP rank's experts -- sharded over
+the expert-data-parallel group only).
+"""
+from __future__ import annotations
+
+from typing import Any, List, Tuple
+
+import torch
+
+from .. import ops
+from ..ops.moe import moe_combine, moe_combine_bwd
+from ..parallel.ep import ExpertDispatcher
+from .common import ParamSpec, Params, StepContext, Unit
+from .config import ModelConfig
+from .llama import LlamaBlock, LlamaEmbedding, LlamaHead
+
+
+class MixtralBlock(LlamaBlock):
+    def __init__(self, cfg: ModelConfig, layer: int, ep_rank: int = 0, ep_size: int = 1):
+        super().__init__(cfg, layer)
+        self.ep_rank, self.ep_size = ep_rank, ep_size
+        self.E_local = cfg.n_experts // ep_size
+        self._dispatcher = None
+
+    def dense_specs(self) -> List[ParamSpec]:
+        c = self.cfg
+        return [s for s in super().param_specs() if s.name not in ("w_gate_up", "w_down")] + \
+            [ParamSpec("router", (c.n_experts, c.d_model), std=c.init_std)]
+
+    def expert_specs(self) -> List[ParamSpec]:
+        c = self.cfg
+        out_std = c.init_std / (2 * c.n_layers) ** 0.5
+        off = self.ep_rank * self.E_local
+        return [ParamSpec("w_gate_up", (self.E_local, 2 * c.ffn_dim, c.d_model), std=c.init_std,
+                          experts=self.E_local, expert_offset=off),
+                ParamSpec("w_down", (self.E_local, c.d_model, c.ffn_dim), std=out_std,
+                          experts=self.E_local, expert_offset=off)]
+
+    def dispatcher(self, ctx: StepContext) -> ExpertDispatcher:
+        if self._dispatcher is None:
+            self._dispatcher = ExpertDispatcher(ctx.ep_group if self.ep_size > 1 else None, self.cfg.n_experts)
+        return self._dispatcher
+
+    # ---------------------------------------------------------------- MoE FFN
+    def moe_forward(self, p: Params, hn2: torch.Tensor, ctx: StepContext):
+        c = self.cfg
+        T, E, K = hn2.shape[0], c.n_experts, c.top_k
+        logits = torch.mm(hn2, p["router"].t()).float()
+        probs = torch.softmax(logits, dim=-1)
+        topv, topi = logits.topk(K, dim=-1)
+        gates = torch.softmax(topv, dim=-1).contiguous()
+        flat = topi.reshape(-1)
+        order = torch.argsort(flat, stable=True)
+        counts = torch.bincount(flat, minlength=E)
+        tok = torch.div(order, K, rounding_mode="floor")
+        pos = torch.empty_like(order)
+        pos[order] = torch.arange(order.numel(), device=order.device)
+        pos = pos.view(T, K)
+        x_sorted = hn2.index_select(0, tok)
+        disp = self.dispatcher(ctx)
+        x_local, dctx = disp.dispatch(x_sorted, counts)
+        y_local, exp_saved = self._experts_fwd(p, x_local, dctx.local_counts)
+        y_sorted = disp.combine(y_local, dctx)
+        out = moe_combine(y_sorted, pos, gates)
+        f = counts.float() / float(T * K) * K  # fraction of tokens choosing each expert (summed over k)
+        ctx.aux.setdefault("moe_aux", []).append(float(E) * (f * probs.mean(0)).sum())
+        return out, (probs, topi, gates, pos, f, x_local, dctx, exp_saved, y_sorted)
+
+    def _experts_fwd(self, p: Params, x: torch.Tensor, counts: List[int]):
+        c = self.cfg
+        F = c.ffn_dim
+        M = x.shape[0]
+        gu_all = x.new_empty((M, 2 * F))
+        a_all = x.new_empty((M, F))
+        y = x.new_empty((M, c.d_model))
+        off = 0
+        for e, n in enumerate(counts):
+            if n:
+                xe = x.narrow(0, off, n)
+                gu = gu_all.narrow(0, off, n)
+                torch.mm(xe, p["w_gate_up"][e].t(), out=gu)
+                a_all.narrow(0, off, n).copy_(ops.swiglu_fwd(gu))
+                torch.mm(a_all.narrow(0, off, n), p["w_down"][e].t(), out=y.narrow(0, off, n))
+            off += n
+        return y, (gu_all, a_all, counts)
+
+    def _experts_bwd(self, p: Params, g: Params, x: torch.Tensor, dy: torch.Tensor, saved):
+        gu_all, a_all, counts = saved
+        dx = torch.empty_like(x)
+        off = 0
+        for e, n in enumerate(counts):
+            if n == 0:
+                g["w_down"][e].zero_()
+                g["w_gate_up"][e].zero_()
+                continue
+            dye = dy.narrow(0, off, n)
+            torch.mm(dye.t(), a_all.narrow(0, off, n), out=g["w_down"][e])
+            da = torch.mm(dye, p["w_down"][e])
+            dgu = ops.swiglu_bwd(da, gu_all.narrow(0, off, n))
+            torch.mm(dgu.t(), x.narrow(0, off, n), out=g["w_gate_up"][e])
+            torch.mm(dgu, p["w_gate_up"][e], out=dx.narrow(0, off, n))
+            off += n
+        return dx
+
+    def moe_backward(self, p: Params, g: Params, hn2: torch.Tensor, saved, dout: torch.Tensor, ctx: StepContext):
+        c = self.cfg
+        probs, topi, gates, pos, f, x_local, dctx, exp_saved, y_sorted = saved
+        T, E = probs.shape
+        disp = self.dispatcher(ctx)
+        dy_sorted, dgates = moe_combine_bwd(dout.contiguous(), y_sorted, pos, gates)
+        dy_local = disp.redispatch(dy_sorted, dctx)
+        dx_local = self._experts_bwd(p, g, x_local, dy_local, exp_saved)
+        dx_sorted = disp.combine(dx_local, dctx)
+        dhn2 = moe_combine(dx_sorted, pos, None)  # adjoint of the dispatch gather: sum the K slots per token
+        dtop = gates * (dgates - (gates * dgates).sum(-1, keepdim=True))
+        dlogits = torch.zeros(T, E, dtype=torch.float32, device=dout.device).scatter_(1, topi, dtop)
+        if c.router_aux_coef > 0:
+            # d(coef * mean_l aux_l)/d logits, times the micro-batch share of the loss (grad_scale * tokens)
+            scale = c.router_aux_coef * E / (c.n_layers * T) * ctx.grad_scale * ctx.tokens
+            dlogits += scale * probs * (f - (probs * f).sum(-1, keepdim=True))
+        dl = dlogits.to(hn2.dtype)
+        torch.mm(dl.t(), hn2, out=g["router"])
+        dhn2 = dhn2 + torch.mm(dl, p["router"])
+        return dhn2
+
+    # ---------------------------------------------------------------- unit API
+    def forward(self, p: Params, x_pair, ctx: StepContext):
+        c = self.cfg
+        saved_attn, o = self.attn_forward(p, x_pair, ctx)
+        x = saved_attn[0]
+        hn2, h, rstd2 = ops.rmsnorm_fwd(x, p["mlp_norm"], c.norm_eps, residual=o)
+        moe_out, moe_saved = self.moe_forward(p, hn2, ctx)
+        return (h, moe_out), (saved_attn, h, rstd2, hn2, moe_saved)
+
+    def backward(self, p: Params, g: Params, saved, dy: torch.Tensor, ctx: StepContext):
+        saved_attn, h, rstd2, hn2, moe_saved = saved
+        dhn2 = self.moe_backward(p, g, hn2, moe_saved, dy, ctx)
+        dh = ops.rmsnorm_bwd(dhn2, h, p["mlp_norm"], rstd2, g["mlp_norm"], dres=dy)
+        return self.attn_backward(p, g, saved_attn, dh, ctx)
+
+    def flops(self, ctx: StepContext) -> float:
+        c = self.cfg
+        T, S = ctx.tokens, ctx.seq_len
+        gemm = 2 * T * c.d_model * (c.qkv_dim + c.n_heads * c.head_dim + 3 * c.ffn_dim * c.top_k + c.n_experts)
+        return 3.0 * (gemm + 2 * T * S * c.n_heads * c.head_dim)
+
+
+def build(cfg: ModelConfig, ep_rank: int = 0, ep_size: int = 1):
+    """Groups: embed, then per layer (dense, experts), then head. Stages reference (dense, experts)."""
+    emb, head = LlamaEmbedding(cfg), LlamaHead(cfg)
+    groups: List[Tuple[str, List[ParamSpec], str]] = [("embed", emb.param_specs(), "dense")]
+    stages: List[Tuple[Unit, Any]] = [(emb, 0)]
+    for i in range(cfg.n_layers):
+        blk = MixtralBlock(cfg, i, ep_rank, ep_size)
+        groups.append((blk.name, blk.dense_specs(), "dense"))
+        groups.append((blk.name + ".experts", blk.expert_specs(), "expert"))
+        stages.append((blk, (len(groups) - 2, len(groups) - 1)))
+    groups.append(("head", head.param_specs(), "dense"))
+    stages.append((head, len(groups) - 1))
+    return groups, stages

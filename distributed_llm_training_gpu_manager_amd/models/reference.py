@@ -45,8 +45,8 @@ def moe_ref(x, p, prefix, cfg: ModelConfig):
     gates = torch.softmax(topv, dim=-1)
     out = torch.zeros_like(x)
     for e in range(E):
-        wgu = p[prefix + "w_gate_up"][e]
-        wd = p[prefix + "w_down"][e]
+        wgu = p[prefix + "experts.w_gate_up"][e]
+        wd = p[prefix + "experts.w_down"][e]
         sel = (topi == e)
         rows = sel.any(-1).nonzero().squeeze(-1)
         if rows.numel() == 0:

@@ -1,0 +1,32 @@
+"""MoE combine ops (kernel: csrc/kernels/moe.hip): gather-based, deterministic, no atomics."""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from .._native import hip_ops, use_native
+
+
+def moe_combine(y: torch.Tensor, pos: torch.Tensor, gates: Optional[torch.Tensor]) -> torch.Tensor:
+    """out[t] = sum_k gates[t,k] * y[pos[t,k]]  (gates=None -> plain sum)."""
+    if use_native(y):
+        return hip_ops().moe_combine_fwd(y, pos, gates)
+    T, K = pos.shape
+    rows = y.float()[pos.reshape(-1)].view(T, K, -1)
+    if gates is not None:
+        rows = rows * gates.float().unsqueeze(-1)
+    return rows.sum(1).to(y.dtype)
+
+
+def moe_combine_bwd(dout: torch.Tensor, y: torch.Tensor, pos: torch.Tensor,
+                    gates: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Adjoint of :func:`moe_combine` -> (dy [N, D], dgates [T, K] fp32)."""
+    if use_native(y):
+        return hip_ops().moe_combine_bwd(dout, y, pos, gates)
+    T, K = pos.shape
+    d = dout.float()
+    dy = torch.zeros_like(y, dtype=torch.float32)
+    dy[pos.reshape(-1)] = (d.unsqueeze(1) * gates.float().unsqueeze(-1)).reshape(T * K, -1)
+    dg = (d.unsqueeze(1) * y.float()[pos.reshape(-1)].view(T, K, -1)).sum(-1)
+    return dy.to(y.dtype), dg

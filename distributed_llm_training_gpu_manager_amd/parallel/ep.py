@@ -1,0 +1,101 @@
+"""Expert parallelism: process groups and the token all-to-all (BASELINE config 5).
+
+Layout: ``world = ep_size x expert_dp``. EP groups are contiguous rank blocks
+(``[0..ep-1], [ep..2ep-1], ...``) -- on one 8-GPU MI355X node with ep=8 the
+all-to-all runs over the full xGMI mesh, where every GPU pair has a direct link,
+which is exactly the traffic pattern a point-to-point fabric serves best (no
+ring). Expert-data-parallel groups hold the same experts (rank i, i+ep, ...) and
+carry the ZeRO partitioning of the expert weights.
+
+The dispatcher moves permuted token rows to the ranks that own their experts and
+back with ``all_to_all_single`` and uneven splits; the split sizes are exchanged
+first (one tiny all-to-all + one host read per MoE layer and direction).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from .comm import Comm
+
+
+def build_ep_comms(ep_size: int) -> Tuple[Optional[Comm], Optional[Comm]]:
+    """Return (ep_comm, expert_dp_comm) for this rank; every rank must call this collectively."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return None, None
+    world, rank = dist.get_world_size(), dist.get_rank()
+    assert world % ep_size == 0, "world size must be a multiple of expert_parallel_size"
+    ep_comm = edp_comm = None
+    for b in range(world // ep_size):
+        ranks = list(range(b * ep_size, (b + 1) * ep_size))
+        g = dist.new_group(ranks) if ep_size < world else dist.group.WORLD
+        if rank in ranks:
+            ep_comm = Comm(g)
+    dp = world // ep_size
+    for i in range(ep_size):
+        ranks = list(range(i, world, ep_size))
+        g = dist.new_group(ranks) if dp < world else dist.group.WORLD
+        if rank in ranks:
+            edp_comm = Comm(g)
+    return ep_comm, edp_comm
+
+
+@dataclass
+class DispatchCtx:
+    send_splits: List[int]
+    recv_splits: List[int]
+    regroup: Optional[torch.Tensor]  # recv order -> local-expert-major order
+    local_counts: List[int]
+
+
+class ExpertDispatcher:
+    def __init__(self, ep_comm: Optional[Comm], n_experts: int):
+        self.comm = ep_comm
+        self.W = ep_comm.world if ep_comm is not None else 1
+        self.rank = ep_comm.rank if ep_comm is not None else 0
+        self.E = n_experts
+        assert n_experts % self.W == 0, "n_experts must be divisible by the EP size"
+        self.El = n_experts // self.W
+
+    def dispatch(self, x_sorted: torch.Tensor, counts: torch.Tensor) -> Tuple[torch.Tensor, DispatchCtx]:
+        """x_sorted: rows grouped by global expert id (counts[e] rows each)."""
+        if self.W == 1:
+            lc = counts.tolist()
+            return x_sorted, DispatchCtx([x_sorted.shape[0]], [x_sorted.shape[0]], None, lc)
+        recv = torch.empty_like(counts)
+        self.comm.all_to_all_single(recv, counts.contiguous())  # [src, local expert] counts
+        c_send = counts.view(self.W, self.El).sum(1).tolist()
+        mat = recv.view(self.W, self.El).cpu()
+        c_recv = mat.sum(1).tolist()
+        out = x_sorted.new_empty((sum(c_recv), x_sorted.shape[1]))
+        self.comm.all_to_all_single(out, x_sorted.contiguous(), c_recv, c_send)
+        # received rows are [src][local expert]; regroup to [local expert][src]
+        offs = torch.zeros(self.W, self.El, dtype=torch.long)
+        flat = mat.reshape(-1)
+        starts = torch.cumsum(flat, 0) - flat
+        offs = starts.view(self.W, self.El)
+        idx = [torch.arange(int(offs[s, e]), int(offs[s, e] + mat[s, e])) for e in range(self.El) for s in range(self.W)]
+        regroup = torch.cat(idx).to(x_sorted.device) if idx else torch.zeros(0, dtype=torch.long, device=x_sorted.device)
+        ctx = DispatchCtx(c_send, c_recv, regroup, mat.sum(0).tolist())
+        return out.index_select(0, regroup), ctx
+
+    def redispatch(self, rows_sorted: torch.Tensor, ctx: DispatchCtx) -> torch.Tensor:
+        """Send another [N, D] tensor laid out like the dispatched rows (backward: d outputs)."""
+        if self.W == 1:
+            return rows_sorted
+        out = rows_sorted.new_empty((sum(ctx.recv_splits), rows_sorted.shape[1]))
+        self.comm.all_to_all_single(out, rows_sorted.contiguous(), ctx.recv_splits, ctx.send_splits)
+        return out.index_select(0, ctx.regroup)
+
+    def combine(self, y_local: torch.Tensor, ctx: DispatchCtx) -> torch.Tensor:
+        """Inverse of dispatch: local-expert-major rows back to the source ranks, expert-sorted order."""
+        if self.W == 1:
+            return y_local
+        y_recv = torch.empty_like(y_local)
+        y_recv.index_copy_(0, ctx.regroup, y_local)
+        out = y_local.new_empty((sum(ctx.send_splits), y_local.shape[1]))
+        self.comm.all_to_all_single(out, y_recv, ctx.send_splits, ctx.recv_splits)
+        return out

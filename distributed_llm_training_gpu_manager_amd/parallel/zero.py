@@ -72,6 +72,7 @@ class EngineConfig:
     cpu_checkpointing: bool = False
     prefetch: bool = True
     seed: int = 1234
+    expert_parallel_size: int = 1
     offload_optimizer: str = "none"  # none | cpu (ZeRO-Offload parity path, C++ AVX2 AdamW on pinned host state)
     init_device: str = "auto"  # "cpu" gives bit-identical init on any device (tests); auto: cpu below 1e9 params
     fp16: bool = False  # dynamic loss scaling path (reference fp16 block)
@@ -89,8 +90,10 @@ class EngineConfig:
 class FlatGroup:
     """One parameter group (= one unit) as a flat, ALIGN-padded, W-divisible segment."""
 
-    def __init__(self, idx: int, name: str, specs: List[ParamSpec], part_world: int):
+    def __init__(self, idx: int, name: str, specs: List[ParamSpec], part_world: int, kind: str = "dense",
+                 comm: Optional[Comm] = None):
         self.idx, self.name, self.specs = idx, name, specs
+        self.kind, self.P, self.comm = kind, part_world, comm
         self.layout: Dict[str, Tuple[int, Tuple[int, ...]]] = {}
         off = 0
         for s in specs:
@@ -161,13 +164,34 @@ class ZeroEngine:
                  ep_comm: Optional[Comm] = None):
         self.mcfg, self.cfg, self.device = model_cfg, cfg, device
         self.comm = comm or Comm()
-        self.ep_comm = ep_comm
         self.W, self.rank = self.comm.world, self.comm.rank
         self.stage = cfg.zero_stage
         assert self.stage in (0, 1, 2, 3), "ZeRO stage must be 0..3"
         self.P = 1 if self.stage == 0 else self.W
-        groups, self.stages = build_model(model_cfg)
-        self.groups = [FlatGroup(i, n, s, self.P) for i, (n, s) in enumerate(groups)]
+        # expert parallelism: experts live on EP ranks, sharded (ZeRO) only over expert-data-parallel ranks
+        self.ep_size = max(1, cfg.expert_parallel_size) if model_cfg.n_experts else 1
+        if self.ep_size > 1 and self.W > 1:
+            from .ep import build_ep_comms
+            self.ep_comm, self.edp_comm = build_ep_comms(self.ep_size)
+        else:
+            self.ep_size = 1
+            self.ep_comm, self.edp_comm = None, self.comm
+        ep_comm = ep_comm or self.ep_comm
+        self.ep_comm = ep_comm
+        ep_rank = self.ep_comm.rank if self.ep_comm is not None else 0
+        groups, stages = build_model(model_cfg, ep_rank, self.ep_size)
+        self.stages = [(u, tuple(gi) if isinstance(gi, (tuple, list)) else (gi,)) for u, gi in stages]
+        self.groups = []
+        for i, grp in enumerate(groups):
+            name, specs = grp[0], grp[1]
+            kind = grp[2] if len(grp) > 2 else "dense"
+            if kind == "expert":
+                comm_g = self.edp_comm if self.edp_comm is not None else Comm()
+                P_g = 1 if self.stage == 0 else comm_g.world
+            else:
+                comm_g, P_g = self.comm, self.P
+            self.groups.append(FlatGroup(i, name, specs, P_g, kind, comm_g))
+        self.has_experts = any(g.kind == "expert" for g in self.groups)
         soff = foff = 0
         for g in self.groups:
             g.shard_off, g.full_off = soff, foff
@@ -191,8 +215,9 @@ class ZeroEngine:
             self.rope = None
         # group visit bookkeeping (tied weights appear twice)
         self._bwd_last_visit: Dict[int, int] = {}
-        for si, (_, gi) in enumerate(self.stages):
-            self._bwd_last_visit[gi] = min(si, self._bwd_last_visit.get(gi, si))
+        for si, (_, gis) in enumerate(self.stages):
+            for gi in gis:
+                self._bwd_last_visit[gi] = min(si, self._bwd_last_visit.get(gi, si))
         self._live: Dict[int, Tuple[torch.Tensor, Handle]] = {}
         self._gbuf_pool: Dict[int, List[torch.Tensor]] = {}
         self.fault_inject_nan = False  # fault injection: poison one gradient element on the next micro-step
@@ -226,11 +251,12 @@ class ZeroEngine:
         for g in self.groups:
             full = torch.zeros(g.numel, dtype=torch.float32, device=init_dev)
             views = g.views(full)
-            gen.manual_seed(self.cfg.seed * 1000003 + g.idx)
+            gseed = self.cfg.seed * 1000003 + g.idx
+            gen.manual_seed(gseed)
             for s in g.specs:
-                init_param(s, views[s.name], gen)
+                init_param(s, views[s.name], gen, gseed)
             full = full.to(self.device)
-            r0 = (self.rank if self.P > 1 else 0) * g.shard_numel
+            r0 = (g.comm.rank if g.P > 1 else 0) * g.shard_numel
             self.master.narrow(0, g.shard_off, g.shard_numel).copy_(full.narrow(0, r0, g.shard_numel))
             if self.p16_full is not None and self.p16_full is not self.p16_shard:
                 self.p16_full.narrow(0, g.full_off, g.numel).copy_(full)
@@ -249,21 +275,29 @@ class ZeroEngine:
         if self.stage < 3:
             flat = self.p16_full.narrow(0, g.full_off, g.numel)
             self._live[gi] = (flat, DONE)
-        elif self.W == 1:
+        elif g.P == 1:
             self._live[gi] = (self._shard16(g), DONE)
         else:
             buf = torch.empty(g.numel, dtype=self.dtype, device=self.device)
-            self._live[gi] = (buf, self.comm.all_gather(buf, self._shard16(g), async_op=True))
+            self._live[gi] = (buf, g.comm.all_gather(buf, self._shard16(g), async_op=True))
 
-    def fetch(self, gi: int) -> Dict[str, torch.Tensor]:
-        self._issue_gather(gi)
-        flat, h = self._live[gi]
-        h.wait()
-        return self.groups[gi].views(flat)
+    def _issue_gathers(self, gis) -> None:
+        for gi in gis:
+            self._issue_gather(gi)
 
-    def release(self, gi: int) -> None:
+    def fetch(self, gis) -> Dict[str, torch.Tensor]:
+        out: Dict[str, torch.Tensor] = {}
+        for gi in (gis if isinstance(gis, tuple) else (gis,)):
+            self._issue_gather(gi)
+            flat, h = self._live[gi]
+            h.wait()
+            out.update(self.groups[gi].views(flat))
+        return out
+
+    def release(self, gis) -> None:
         if self.stage == 3:
-            self._live.pop(gi, None)
+            for gi in (gis if isinstance(gis, tuple) else (gis,)):
+                self._live.pop(gi, None)
 
     # ------------------------------------------------------------------ grads
     def _grad_target_full(self, g: FlatGroup) -> Optional[torch.Tensor]:
@@ -277,22 +311,25 @@ class ZeroEngine:
                            pending: List[Tuple[Handle, Any]]) -> None:
         g = self.groups[gi]
         beta = 0.0 if first_micro else 1.0
+        # an expert sees the tokens of every EP rank, each scaled by 1/(its own tokens): divide by the EP
+        # size so expert grads are the global mean like the dense grads (which are AVG-reduced)
+        alpha = 1.0 / self.ep_size if g.kind == "expert" else 1.0
         if self.stage in (0, 1):
             tgt = self._grad_target_full(g)
-            ops.accumulate_(tgt, gbuf, 1.0, beta)
+            ops.accumulate_(tgt, gbuf, alpha, beta)
             self._release_gbuf(gbuf)
             if last_micro:
                 if self.stage == 0:
-                    h = self.comm.all_reduce(tgt, avg=True, async_op=True)
+                    h = g.comm.all_reduce(tgt, avg=True, async_op=True)
                     pending.append((h, None))
                 else:
                     out = self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
-                    h = self.comm.reduce_scatter(out, tgt, avg=True, async_op=True)
+                    h = g.comm.reduce_scatter(out, tgt, avg=True, async_op=True)
                     pending.append((h, tgt))
             return
         shard_tgt = self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
-        if self.W == 1:
-            ops.accumulate_(shard_tgt, gbuf, 1.0, beta)
+        if g.comm.world == 1:
+            ops.accumulate_(shard_tgt, gbuf, alpha, beta)
             self._release_gbuf(gbuf)
             return
         src = gbuf
@@ -300,8 +337,8 @@ class ZeroEngine:
             src = gbuf.to(self.cfg.comm_dtype)
             self._release_gbuf(gbuf)
         out = torch.empty(g.shard_numel, dtype=src.dtype, device=self.device)
-        h = self.comm.reduce_scatter(out, src, avg=True, async_op=True)
-        pending.append((h, (shard_tgt, out, beta, src)))
+        h = g.comm.reduce_scatter(out, src, avg=True, async_op=True)
+        pending.append((h, (shard_tgt, out, beta, src, alpha)))
 
     def _acquire_gbuf(self, numel: int) -> torch.Tensor:
         # flat bf16 gradient scratch, pooled per size and zeroed ONCE: units write only their
@@ -320,8 +357,8 @@ class ZeroEngine:
             h, payload = pending.pop(0)
             h.wait()
             if isinstance(payload, tuple):
-                shard_tgt, out, beta, src = payload
-                ops.accumulate_(shard_tgt, out, 1.0, beta)
+                shard_tgt, out, beta, src, alpha = payload
+                ops.accumulate_(shard_tgt, out, alpha, beta)
                 if src is not None and src.dtype == self.dtype:
                     self._release_gbuf(src)
 
@@ -341,17 +378,17 @@ class ZeroEngine:
         x: Any = None
         ckpt = self.cfg.activation_checkpointing
         # ---- forward
-        for si, (unit, gi) in enumerate(self.stages):
-            p = self.fetch(gi)
+        last_gis = self.stages[-1][1]
+        for si, (unit, gis) in enumerate(self.stages):
+            p = self.fetch(gis)
             if self.cfg.prefetch and si + 1 < n:
-                self._issue_gather(self.stages[si + 1][1])
+                self._issue_gathers(self.stages[si + 1][1])
             if ckpt and si < n - 1:
                 y, _ = unit.forward(p, x, ctx)
                 saved[si] = ("ckpt", x)
             else:
                 y, saved[si] = unit.forward(p, x, ctx)
-            if gi != self.stages[-1][1]:
-                self.release(gi)  # the head's params stay gathered: backward starts with it
+            self.release(tuple(gi for gi in gis if gi not in last_gis))  # the head stays gathered for backward
             x = y
         loss = x
         # ---- backward
@@ -359,48 +396,71 @@ class ZeroEngine:
         pending: List[Tuple[Handle, Any]] = []
         gbufs: Dict[int, torch.Tensor] = {}
         for si in range(n - 1, -1, -1):
-            unit, gi = self.stages[si]
-            p = self.fetch(gi)
+            unit, gis = self.stages[si]
+            p = self.fetch(gis)
             if self.cfg.prefetch and si > 0:
-                self._issue_gather(self.stages[si - 1][1])
-            g = self.groups[gi]
-            if gi not in gbufs:
-                gbufs[gi] = self._acquire_gbuf(g.numel)
-            gv = g.views(gbufs[gi])
+                self._issue_gathers(self.stages[si - 1][1])
+            gv: Dict[str, torch.Tensor] = {}
+            for gi in gis:
+                if gi not in gbufs:
+                    gbufs[gi] = self._acquire_gbuf(self.groups[gi].numel)
+                gv.update(self.groups[gi].views(gbufs[gi]))
             sv = saved[si]
             if isinstance(sv, tuple) and len(sv) == 2 and isinstance(sv[0], str) and sv[0] == "ckpt":
                 _, sv = unit.forward(p, sv[1], ctx)
             dy = unit.backward(p, gv, sv, dy, ctx)
             saved[si] = None
             if self.fault_inject_nan:
-                gbufs[gi][0] = float("nan")
+                gbufs[gis[0]][0] = float("nan")
                 self.fault_inject_nan = False
-            if self._bwd_last_visit[gi] == si:
-                self._reduce_group_grad(gi, gbufs.pop(gi), first, last, pending)
-                self.release(gi)
-                self._drain(pending, keep=1)
+            for gi in gis:
+                if self._bwd_last_visit[gi] == si:
+                    self._reduce_group_grad(gi, gbufs.pop(gi), first, last, pending)
+                    self.release((gi,))
+            self._drain(pending, keep=1)
         self._drain(pending, keep=0)
-        self._live.clear() if self.stage == 3 else None
+        if self.stage == 3:
+            self._live.clear()
+        self.last_aux = ctx.aux
         return loss
 
     def sync_params_from_master(self) -> None:
         """Recompute the bf16 compute copies from the fp32 master (after restore / external edits)."""
         ops.cast_f32_bf16_(self.p16_shard, self.master)
         if self.stage in (1, 2):
-            hs = [self.comm.all_gather(self.p16_full.narrow(0, g.full_off, g.numel), self._shard16(g), async_op=True)
+            hs = [g.comm.all_gather(self.p16_full.narrow(0, g.full_off, g.numel), self._shard16(g), async_op=True)
                   for g in self.groups]
             for h in hs:
                 h.wait()
         self._live.clear()
+
+    def _global_grad_stats(self) -> None:
+        """stats = [sum g^2, #non-finite] over the whole model, each element counted once."""
+        if not self.has_experts:
+            ops.grad_stats([self.grad_shard], self.stats)
+            if self.P > 1:
+                self.comm.all_reduce(self.stats, async_op=False).wait()
+            return
+        sl = lambda g: self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
+        dense = torch.zeros(2, dtype=torch.float32, device=self.device)
+        exp = torch.zeros(2, dtype=torch.float32, device=self.device)
+        ops.grad_stats([sl(g) for g in self.groups if g.kind != "expert"], dense)
+        ops.grad_stats([sl(g) for g in self.groups if g.kind == "expert"], exp)
+        if self.P > 1:
+            self.comm.all_reduce(dense, async_op=False).wait()
+        if self.ep_comm is not None and self.ep_comm.world > 1:
+            self.ep_comm.all_reduce(exp, async_op=False).wait()
+        eg = next(g for g in self.groups if g.kind == "expert")
+        if eg.P > 1:
+            eg.comm.all_reduce(exp, async_op=False).wait()
+        self.stats.copy_(dense + exp)
 
     def optimizer_step(self) -> Dict[str, Any]:
         for hk in self.pre_step_hooks:
             hk(self)
         self.step_count += 1
         cfg = self.cfg
-        ops.grad_stats([self.grad_shard], self.stats)
-        if self.P > 1:
-            self.comm.all_reduce(self.stats, async_op=False).wait()
+        self._global_grad_stats()
         lr = lr_at(cfg, self.step_count)
         inv_scale = 1.0 / self.scaler.scale if self.scaler else 1.0
         ops.adamw_step_(self.master, self.exp_avg, self.exp_avg_sq, self.grad_shard,
@@ -412,8 +472,8 @@ class ZeroEngine:
         if self.stage in (1, 2):
             hs = []
             for g in self.groups:
-                hs.append(self.comm.all_gather(self.p16_full.narrow(0, g.full_off, g.numel), self._shard16(g),
-                                               async_op=True))
+                hs.append(g.comm.all_gather(self.p16_full.narrow(0, g.full_off, g.numel), self._shard16(g),
+                                            async_op=True))
             for h in hs:
                 h.wait()
         if self.scaler is not None:
@@ -442,17 +502,32 @@ class ZeroEngine:
 
     # ------------------------------------------------------------------ helpers
     def full_params(self) -> Dict[str, torch.Tensor]:
-        """Gather all parameters (fp32 master) -- for tests / consolidated checkpoints."""
+        """Gather all parameters (fp32 master) -- for tests / consolidated checkpoints.
+
+        Expert tensors are concatenated over the expert-parallel ranks (global expert order).
+        """
+        return self._gather_flat(self.master)
+
+    def full_grads(self) -> Dict[str, torch.Tensor]:
+        """Gather the accumulated fp32 gradient partition (tests / debugging)."""
+        return self._gather_flat(self.grad_shard)
+
+    def _gather_flat(self, buf: torch.Tensor) -> Dict[str, torch.Tensor]:
         out = {}
         for g in self.groups:
-            shard = self.master.narrow(0, g.shard_off, g.shard_numel)
-            if self.P > 1:
+            shard = buf.narrow(0, g.shard_off, g.shard_numel)
+            if g.P > 1:
                 full = torch.empty(g.numel, dtype=torch.float32, device=self.device)
-                self.comm.all_gather(full, shard, async_op=False).wait()
+                g.comm.all_gather(full, shard, async_op=False).wait()
             else:
                 full = shard
             for k, v in g.views(full).items():
-                out[f"{g.name}.{k}"] = v.clone()
+                v = v.clone()
+                if g.kind == "expert" and self.ep_comm is not None and self.ep_comm.world > 1:
+                    parts = torch.empty((self.ep_comm.world, *v.shape), dtype=v.dtype, device=v.device)
+                    self.ep_comm.all_gather(parts.view(-1), v.reshape(-1), async_op=False).wait()
+                    v = parts.reshape(-1, *v.shape[1:])
+                out[f"{g.name}.{k}"] = v
         return out
 
     def memory_report(self) -> Dict[str, float]:

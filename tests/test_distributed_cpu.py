@@ -117,3 +117,43 @@ def test_zero3_world2_bf16_comm_gradients(tmp_path):
         got = torch.cat([shards[r].narrow(0, g.shard_off // 2, half) for r in range(2)])
         err = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-8))
         assert err < 2e-2, (g.name, err)
+
+
+def _ep_worker(rank, world, port, stage, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = _cfg(stage, 1)
+    cfg.expert_parallel_size = world
+    eng = ZeroEngine(get_config("mixtral-tiny"), cfg, torch.device("cpu"), Comm())
+    init = eng.full_params()
+    t = _data("mixtral-tiny", 1, world)[0][rank]
+    eng.micro_step(t[:, :-1], t[:, 1:], first=True, last=True)
+    grads = eng.full_grads()
+    if rank == 0:
+        torch.save({"params": init, "grads": grads}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("stage", [1, 3])
+def test_mixtral_expert_parallel_world2_matches_single(tmp_path, stage):
+    """BASELINE config 5 plumbing: EP=2 all-to-all dispatch/combine == single-process MoE gradients.
+
+    Init is identical (experts seeded by global index), and the accumulated gradients of every
+    parameter -- dense ones reduce-scattered over the world, expert ones computed on the EP rank
+    that owns them from tokens of both ranks -- match the single-process 2-micro-batch run.
+    """
+    out = str(tmp_path / "ep.pt")
+    mp.spawn(_ep_worker, args=(2, _free_port(), stage, out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    eng = ZeroEngine(get_config("mixtral-tiny"), _cfg(stage, 2), torch.device("cpu"))
+    ref_init = eng.full_params()
+    for k, v in ref_init.items():
+        assert torch.equal(got["params"][k], v), k
+    for i, t in enumerate(_data("mixtral-tiny", 1, 2)[0]):
+        eng.micro_step(t[:, :-1], t[:, 1:], first=i == 0, last=i == 1)
+    ref = eng.full_grads()
+    assert set(got["grads"]) == set(ref)
+    for k, v in ref.items():
+        err = float((got["grads"][k] - v).abs().max() / v.abs().max().clamp_min(1e-8))
+        assert err < 2e-2, (k, err)

@@ -193,3 +193,23 @@ def test_flash_attention_rescale_branch():
     o_ref, _ = attn_ops._ref_fwd(q, k, v, scale, True)
     o, _ = ops.flash_attn_fwd(q.to(DEV), k.to(DEV), v.to(DEV), scale, True)
     assert rel_err(o, o_ref) < 2e-2
+
+
+@pytest.mark.parametrize("K", [1, 2, 4])
+def test_moe_combine_fwd_bwd(K):
+    from distributed_llm_training_gpu_manager_amd.ops.moe import moe_combine, moe_combine_bwd
+
+    torch.manual_seed(0)
+    T, D = 133, 512
+    N = T * K
+    y = torch.randn(N, D, dtype=torch.bfloat16)
+    pos = torch.randperm(N).view(T, K)
+    gates = torch.softmax(torch.randn(T, K), -1)
+    ref = moe_combine(y, pos, gates)
+    out = moe_combine(y.to(DEV), pos.to(DEV), gates.to(DEV))
+    assert rel_err(out, ref) < 1e-2
+    assert rel_err(moe_combine(y.to(DEV), pos.to(DEV), None), moe_combine(y, pos, None)) < 1e-2
+    dout = torch.randn(T, D, dtype=torch.bfloat16)
+    dy_ref, dg_ref = moe_combine_bwd(dout, y, pos, gates)
+    dy, dg = moe_combine_bwd(dout.to(DEV), y.to(DEV), pos.to(DEV), gates.to(DEV))
+    assert rel_err(dy, dy_ref) < 1e-2 and rel_err(dg, dg_ref) < 1e-3
