@@ -55,6 +55,7 @@ class StepContext:
     rope: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
     ep_group: Any = None
     aux: Dict[str, Any] = field(default_factory=dict)
+    grad_acc: bool = False  # backward ADDS into the gradient views (later micro-batch / tied second visit)
 
     @property
     def tokens(self) -> int:
@@ -74,7 +75,10 @@ class Unit:
         raise NotImplementedError
 
     def backward(self, p: Params, g: Params, saved: Any, dy: Any, ctx: StepContext) -> Any:
-        """Write parameter grads into ``g`` (views; overwrite, not accumulate) and return d input."""
+        """Write (``ctx.grad_acc`` False) or add (True) parameter grads into the views ``g``; return d input.
+
+        ``g`` views are bf16 scratch (reduce-scattered per micro-batch) or fp32 slices of the
+        gradient partition itself (accumulated in place, see ops.gemm.grad_mm)."""
         raise NotImplementedError
 
     # Units whose parameters are needed again at a second position (tied weights)
@@ -124,7 +128,10 @@ class AutogradUnit(Unit):
                 y.backward(dy)
         for k, leaf in leaves.items():
             if leaf.grad is None:
-                g[k].zero_()
+                if not ctx.grad_acc:
+                    g[k].zero_()
+            elif ctx.grad_acc:
+                g[k].add_(leaf.grad.to(g[k].dtype))
             else:
                 g[k].copy_(leaf.grad)
         if isinstance(xin, torch.Tensor) and xin.requires_grad:

@@ -51,11 +51,9 @@ class GPT2Embed(Unit):
 
     def backward(self, p: Params, g: Params, saved, dy, ctx: StepContext):
         ids, pos = saved
-        # second backward visit of the tied group: the head already wrote d(wte) and d(ln_f)
-        g["wpe"].zero_()
-        g["wpe"].index_put_((pos,), dy, accumulate=True)
-        if not self.cfg.tie_embeddings:
-            g["wte"].zero_()
+        # second backward visit of the tied group: the head already wrote (or added) d(wte) and d(ln_f);
+        # ctx.grad_acc is True here, so every write below accumulates
+        g["wpe"].index_put_((pos,), dy.to(g["wpe"].dtype), accumulate=True)
         g["wte"].index_put_((ids,), dy.to(g["wte"].dtype), accumulate=True)
         return None
 

@@ -29,6 +29,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import ops
+from ..ops.gemm import grad_mm
 from .common import ParamSpec, Params, StepContext, Unit
 from .config import ModelConfig
 
@@ -56,8 +57,9 @@ class LlamaEmbedding(Unit):
     def backward(self, p: Params, g: Params, saved, dy, ctx: StepContext):
         ids = saved
         gt = g["tok_embeddings"]
-        gt.zero_()
-        gt.index_put_((ids,), dy.reshape(-1, gt.shape[1]), accumulate=True)
+        if not ctx.grad_acc:
+            gt.zero_()
+        gt.index_put_((ids,), dy.reshape(-1, gt.shape[1]).to(gt.dtype), accumulate=True)
         return None
 
 
@@ -112,16 +114,17 @@ class LlamaBlock(Unit):
         T = B * S
         x, rstd1, hn1, qkv, attn, lse = saved_attn
         attn2d = attn.view(T, c.n_heads * c.head_dim)
-        torch.mm(dh.t(), attn2d, out=g["wo"])
+        acc = ctx.grad_acc
+        grad_mm(g["wo"], dh.t(), attn2d, acc)
         dattn = torch.mm(dh, p["wo"]).view_as(attn)
         q, k, v = self._split(qkv, B, S)
         dq, dk, dv = ops.flash_attn_bwd(dattn, q, k, v, attn, lse, causal=True)
         dqkv = torch.cat([dq.view(T, -1), dk.view(T, -1), dv.view(T, -1)], dim=1)
         cos, sin = ctx.rope
         ops.rope_(dqkv, cos, sin, c.n_heads + c.n_kv_heads, c.head_dim, S, inverse=True)
-        torch.mm(dqkv.t(), hn1, out=g["wqkv"])
+        grad_mm(g["wqkv"], dqkv.t(), hn1, acc)
         dhn1 = torch.mm(dqkv, p["wqkv"])
-        return ops.rmsnorm_bwd(dhn1, x, p["attn_norm"], rstd1, g["attn_norm"], dres=dh)
+        return ops.rmsnorm_bwd(dhn1, x, p["attn_norm"], rstd1, g["attn_norm"], dres=dh, accumulate_dw=acc)
 
     # -- unit API --------------------------------------------------------------------
     def forward(self, p: Params, x_pair, ctx: StepContext):
@@ -137,14 +140,15 @@ class LlamaBlock(Unit):
     def backward(self, p: Params, g: Params, saved, dy: torch.Tensor, ctx: StepContext):
         c = self.cfg
         saved_attn, h, rstd2, hn2, gu, a = saved
-        torch.mm(dy.t(), a, out=g["w_down"])
+        acc = ctx.grad_acc
+        grad_mm(g["w_down"], dy.t(), a, acc)
         da = torch.mm(dy, p["w_down"])
         dgu = ops.swiglu_bwd(da, gu)
         del da
-        torch.mm(dgu.t(), hn2, out=g["w_gate_up"])
+        grad_mm(g["w_gate_up"], dgu.t(), hn2, acc)
         dhn2 = torch.mm(dgu, p["w_gate_up"])
         del dgu
-        dh = ops.rmsnorm_bwd(dhn2, h, p["mlp_norm"], rstd2, g["mlp_norm"], dres=dy)
+        dh = ops.rmsnorm_bwd(dhn2, h, p["mlp_norm"], rstd2, g["mlp_norm"], dres=dy, accumulate_dw=acc)
         return self.attn_backward(p, g, saved_attn, dh, ctx)
 
     def flops(self, ctx: StepContext) -> float:
@@ -180,9 +184,9 @@ class LlamaHead(Unit):
 
     def backward(self, p: Params, g: Params, saved, dy, ctx: StepContext):
         x, rstd, hn, dlogits = saved
-        torch.mm(dlogits.t(), hn, out=g["lm_head"])
+        grad_mm(g["lm_head"], dlogits.t(), hn, ctx.grad_acc)
         dhn = torch.mm(dlogits, p["lm_head"])
-        return ops.rmsnorm_bwd(dhn, x, p["norm"], rstd, g["norm"])
+        return ops.rmsnorm_bwd(dhn, x, p["norm"], rstd, g["norm"], accumulate_dw=ctx.grad_acc)
 
     def flops(self, ctx: StepContext) -> float:
         return 3.0 * 2 * ctx.tokens * self.cfg.d_model * self.cfg.vocab_size

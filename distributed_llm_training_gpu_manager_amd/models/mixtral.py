@@ -26,6 +26,7 @@ from typing import Any, List, Tuple
 import torch
 
 from .. import ops
+from ..ops.gemm import grad_mm
 from ..ops.moe import moe_combine, moe_combine_bwd
 from ..parallel.ep import ExpertDispatcher
 from .common import ParamSpec, Params, StepContext, Unit
@@ -102,20 +103,21 @@ class MixtralBlock(LlamaBlock):
             off += n
         return y, (gu_all, a_all, counts)
 
-    def _experts_bwd(self, p: Params, g: Params, x: torch.Tensor, dy: torch.Tensor, saved):
+    def _experts_bwd(self, p: Params, g: Params, x: torch.Tensor, dy: torch.Tensor, saved, acc: bool):
         gu_all, a_all, counts = saved
         dx = torch.empty_like(x)
         off = 0
         for e, n in enumerate(counts):
             if n == 0:
-                g["w_down"][e].zero_()
-                g["w_gate_up"][e].zero_()
+                if not acc:
+                    g["w_down"][e].zero_()
+                    g["w_gate_up"][e].zero_()
                 continue
             dye = dy.narrow(0, off, n)
-            torch.mm(dye.t(), a_all.narrow(0, off, n), out=g["w_down"][e])
+            grad_mm(g["w_down"][e], dye.t(), a_all.narrow(0, off, n), acc)
             da = torch.mm(dye, p["w_down"][e])
             dgu = ops.swiglu_bwd(da, gu_all.narrow(0, off, n))
-            torch.mm(dgu.t(), x.narrow(0, off, n), out=g["w_gate_up"][e])
+            grad_mm(g["w_gate_up"][e], dgu.t(), x.narrow(0, off, n), acc)
             torch.mm(dgu, p["w_gate_up"][e], out=dx.narrow(0, off, n))
             off += n
         return dx
@@ -127,7 +129,7 @@ class MixtralBlock(LlamaBlock):
         disp = self.dispatcher(ctx)
         dy_sorted, dgates = moe_combine_bwd(dout.contiguous(), y_sorted, pos, gates)
         dy_local = disp.redispatch(dy_sorted, dctx)
-        dx_local = self._experts_bwd(p, g, x_local, dy_local, exp_saved)
+        dx_local = self._experts_bwd(p, g, x_local, dy_local, exp_saved, ctx.grad_acc)
         dx_sorted = disp.combine(dx_local, dctx)
         dhn2 = moe_combine(dx_sorted, pos, None)  # adjoint of the dispatch gather: sum the K slots per token
         dtop = gates * (dgates - (gates * dgates).sum(-1, keepdim=True))
@@ -137,7 +139,7 @@ class MixtralBlock(LlamaBlock):
             scale = c.router_aux_coef * E / (c.n_layers * T) * ctx.grad_scale * ctx.tokens
             dlogits += scale * probs * (f - (probs * f).sum(-1, keepdim=True))
         dl = dlogits.to(hn2.dtype)
-        torch.mm(dl.t(), hn2, out=g["router"])
+        grad_mm(g["router"], dl.t(), hn2, ctx.grad_acc)
         dhn2 = dhn2 + torch.mm(dl, p["router"])
         return dhn2
 
@@ -153,7 +155,7 @@ class MixtralBlock(LlamaBlock):
     def backward(self, p: Params, g: Params, saved, dy: torch.Tensor, ctx: StepContext):
         saved_attn, h, rstd2, hn2, moe_saved = saved
         dhn2 = self.moe_backward(p, g, hn2, moe_saved, dy, ctx)
-        dh = ops.rmsnorm_bwd(dhn2, h, p["mlp_norm"], rstd2, g["mlp_norm"], dres=dy)
+        dh = ops.rmsnorm_bwd(dhn2, h, p["mlp_norm"], rstd2, g["mlp_norm"], dres=dy, accumulate_dw=ctx.grad_acc)
         return self.attn_backward(p, g, saved_attn, dh, ctx)
 
     def flops(self, ctx: StepContext) -> float:

@@ -22,10 +22,11 @@ Schedule (one micro-batch)
     forward : for each unit  -> wait gather(unit) [stage 3], prefetch gather(next),
               unit.forward, free gathered params (the head's are kept for backward)
     backward: for each unit in reverse -> wait gather, prefetch gather(prev),
-              unit.backward writes bf16 grads into a flat scratch segment,
-              async reduce-scatter(avg) of that segment (stage 2/3) whose fp32
-              accumulation is deferred by one unit so RCCL overlaps the next
-              unit's backward
+              unit.backward either accumulates fp32 grads straight into the
+              gradient partition (P == 1, ZeRO-0/1: "direct", GEMM beta = 1) or
+              writes bf16 grads into a flat scratch segment that is async
+              reduce-scattered(avg) (ZeRO-2/3, P > 1) with the fp32 accumulation
+              deferred by one unit so RCCL overlaps the next unit's backward
     step    : grad_stats (sum g^2, #non-finite) -> all_reduce(2 floats) ->
               fused AdamW reading clip coef / overflow flag on device ->
               (stage 1/2) all-gather updated bf16 params
@@ -300,38 +301,40 @@ class ZeroEngine:
                 self._live.pop(gi, None)
 
     # ------------------------------------------------------------------ grads
-    def _grad_target_full(self, g: FlatGroup) -> Optional[torch.Tensor]:
-        if self.stage == 0:
+    def _direct_target(self, g: FlatGroup) -> Optional[torch.Tensor]:
+        """fp32 storage the unit backward writes / accumulates into directly, or None (bf16 scratch path).
+
+        Direct whenever the group's gradient is not reduce-scattered per micro-batch: every group on
+        a single rank (P == 1: the whole 1-GPU bench), ZeRO-0 (all-reduce at the boundary) and ZeRO-1
+        (reduce-scatter of the local fp32 accumulator at the boundary). The weight-gradient GEMMs then
+        run bf16 x bf16 -> fp32 with beta = 1 (ops.gemm.grad_mm): no bf16 rounding of per-micro-batch
+        gradients, no scratch buffer and no separate accumulate pass.
+        """
+        if g.P == 1:
             return self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
         if self.stage == 1:
             return self.grad_full.narrow(0, g.full_off, g.numel)
         return None
 
-    def _reduce_group_grad(self, gi: int, gbuf: torch.Tensor, first_micro: bool, last_micro: bool,
+    def _finish_direct(self, g: FlatGroup, tgt: torch.Tensor, pending: List[Tuple[Handle, Any]]) -> None:
+        """Boundary work for a direct group after its last backward visit of the last micro-batch."""
+        if g.kind == "expert" and self.ep_size > 1:
+            # an expert sees the tokens of every EP rank, each scaled by 1/(its own tokens): divide by the
+            # EP size so expert grads are the global mean like the dense grads (which are AVG-reduced)
+            tgt.mul_(1.0 / self.ep_size)
+        if g.P > 1:  # ZeRO-1: reduce-scatter the local accumulator into this rank's shard
+            out = self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
+            pending.append((g.comm.reduce_scatter(out, tgt, avg=True, async_op=True), tgt))
+        elif g.comm.world > 1:  # ZeRO-0: plain data parallel
+            pending.append((g.comm.all_reduce(tgt, avg=True, async_op=True), None))
+
+    def _reduce_group_grad(self, gi: int, gbuf: torch.Tensor, first_micro: bool,
                            pending: List[Tuple[Handle, Any]]) -> None:
+        """Scratch path (ZeRO-2/3, P > 1): reduce-scatter this micro-batch's bf16 gradient segment now."""
         g = self.groups[gi]
         beta = 0.0 if first_micro else 1.0
-        # an expert sees the tokens of every EP rank, each scaled by 1/(its own tokens): divide by the EP
-        # size so expert grads are the global mean like the dense grads (which are AVG-reduced)
         alpha = 1.0 / self.ep_size if g.kind == "expert" else 1.0
-        if self.stage in (0, 1):
-            tgt = self._grad_target_full(g)
-            ops.accumulate_(tgt, gbuf, alpha, beta)
-            self._release_gbuf(gbuf)
-            if last_micro:
-                if self.stage == 0:
-                    h = g.comm.all_reduce(tgt, avg=True, async_op=True)
-                    pending.append((h, None))
-                else:
-                    out = self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
-                    h = g.comm.reduce_scatter(out, tgt, avg=True, async_op=True)
-                    pending.append((h, tgt))
-            return
         shard_tgt = self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
-        if g.comm.world == 1:
-            ops.accumulate_(shard_tgt, gbuf, alpha, beta)
-            self._release_gbuf(gbuf)
-            return
         src = gbuf
         if self.cfg.comm_dtype != gbuf.dtype:
             src = gbuf.to(self.cfg.comm_dtype)
@@ -395,27 +398,49 @@ class ZeroEngine:
         dy: Any = None
         pending: List[Tuple[Handle, Any]] = []
         gbufs: Dict[int, torch.Tensor] = {}
+        visited: set = set()
         for si in range(n - 1, -1, -1):
             unit, gis = self.stages[si]
             p = self.fetch(gis)
             if self.cfg.prefetch and si > 0:
                 self._issue_gathers(self.stages[si - 1][1])
+            # per group: direct fp32 target or bf16 scratch, and whether this visit adds to what is there
+            # (direct: any micro-batch after the first; both: the second visit of a tied group)
             gv: Dict[str, torch.Tensor] = {}
+            want = {}
             for gi in gis:
-                if gi not in gbufs:
-                    gbufs[gi] = self._acquire_gbuf(self.groups[gi].numel)
-                gv.update(self.groups[gi].views(gbufs[gi]))
+                g = self.groups[gi]
+                tgt = self._direct_target(g)
+                if tgt is None:
+                    if gi not in gbufs:
+                        gbufs[gi] = self._acquire_gbuf(g.numel)
+                    tgt = gbufs[gi]
+                    want[gi] = gi in visited
+                else:
+                    want[gi] = gi in visited or not first
+                gv.update(g.views(tgt))
+            ctx.grad_acc = any(want.values())
+            if ctx.grad_acc:
+                for gi, w in want.items():  # mixed stage (e.g. direct experts + scratch dense): start from 0
+                    if not w:
+                        for v in self.groups[gi].views(gbufs[gi] if gi in gbufs else self._direct_target(
+                                self.groups[gi])).values():
+                            v.zero_()
             sv = saved[si]
             if isinstance(sv, tuple) and len(sv) == 2 and isinstance(sv[0], str) and sv[0] == "ckpt":
                 _, sv = unit.forward(p, sv[1], ctx)
             dy = unit.backward(p, gv, sv, dy, ctx)
             saved[si] = None
+            visited.update(gis)
             if self.fault_inject_nan:
-                gbufs[gis[0]][0] = float("nan")
+                next(iter(gv.values())).view(-1)[0] = float("nan")
                 self.fault_inject_nan = False
             for gi in gis:
                 if self._bwd_last_visit[gi] == si:
-                    self._reduce_group_grad(gi, gbufs.pop(gi), first, last, pending)
+                    if gi in gbufs:
+                        self._reduce_group_grad(gi, gbufs.pop(gi), first, pending)
+                    elif last:
+                        self._finish_direct(self.groups[gi], self._direct_target(self.groups[gi]), pending)
                     self.release((gi,))
             self._drain(pending, keep=1)
         self._drain(pending, keep=0)

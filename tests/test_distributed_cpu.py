@@ -40,25 +40,42 @@ def _worker(rank, world, port, model, stage, steps, out_path, comm_dtype=torch.f
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.manual_seed(0)
     eng = ZeroEngine(get_config(model), _cfg(stage, 1, comm_dtype), torch.device("cpu"), Comm())
-    losses = []
+    losses, grads0 = [], None
     for mbs in _data(model, steps, world):
         t = mbs[rank]
         m = eng.train_step([(t[:, :-1], t[:, 1:])])
         losses.append(float(m["loss"]))
+        if grads0 is None:
+            grads0 = eng.full_grads()
     params = eng.full_params()
     if rank == 0:
-        torch.save({"params": params, "losses": losses}, out_path)
+        torch.save({"params": params, "losses": losses, "grads0": grads0}, out_path)
     dist.barrier()
     dist.destroy_process_group()
 
 
 def _single(model, stage, steps):
     eng = ZeroEngine(get_config(model), _cfg(stage, 2), torch.device("cpu"))
-    losses = []
+    losses, grads0 = [], None
     for mbs in _data(model, steps, 2):
         m = eng.train_step([(t[:, :-1], t[:, 1:]) for t in mbs])
         losses.append(float(m["loss"]))
-    return eng.full_params(), losses
+        if grads0 is None:
+            grads0 = eng.full_grads()
+    return eng.full_params(), losses, grads0
+
+
+def _compare(got, ref_params, ref_grads0, steps, lr=1e-2):
+    """Step-1 gradients must match tightly. Parameters after `steps` Adam steps are compared
+    robustly: W=2 reduces bf16 per-rank gradients while W=1 accumulates fp32 in the GEMM, and Adam
+    turns a sign flip of a near-zero gradient element into a full +-lr step."""
+    for k, v in ref_grads0.items():
+        err = float((got["grads0"][k] - v).abs().max() / v.abs().max().clamp_min(1e-8))
+        assert err < 2e-2, ("grad", k, err)
+    for k, v in ref_params.items():
+        d = (got["params"][k] - v).abs()
+        assert float(d.max()) <= 2 * lr * steps + 1e-3, ("param max", k, float(d.max()))
+        assert float((d > 0.1 * lr).float().mean()) < 0.05, ("param frac", k)
 
 
 @pytest.mark.parametrize("stage", [0, 1, 2, 3])
@@ -67,11 +84,9 @@ def test_zero_stage_world2_matches_single(tmp_path, stage, model):
     out = str(tmp_path / "w2.pt")
     mp.spawn(_worker, args=(2, _free_port(), model, stage, 2, out), nprocs=2, join=True)
     got = torch.load(out, weights_only=True)
-    ref_params, ref_losses = _single(model, stage, 2)
-    # the world-2 loss is rank 0's own micro-batch; compare the parameters, which see both
-    for k, v in ref_params.items():
-        err = float((got["params"][k] - v).abs().max() / v.abs().max().clamp_min(1e-6))
-        assert err < 2e-2, (k, err)
+    ref_params, _, ref_grads0 = _single(model, stage, 2)
+    # the world-2 loss is rank 0's own micro-batch; compare gradients and parameters, which see both
+    _compare(got, ref_params, ref_grads0, 2)
 
 
 def test_gpt2_zero1_world2(tmp_path):
@@ -79,10 +94,8 @@ def test_gpt2_zero1_world2(tmp_path):
     out = str(tmp_path / "g.pt")
     mp.spawn(_worker, args=(2, _free_port(), "gpt2-tiny", 1, 2, out), nprocs=2, join=True)
     got = torch.load(out, weights_only=True)
-    ref_params, _ = _single("gpt2-tiny", 1, 2)
-    for k, v in ref_params.items():
-        err = float((got["params"][k] - v).abs().max() / v.abs().max().clamp_min(1e-6))
-        assert err < 2e-2, (k, err)
+    ref_params, _, ref_grads0 = _single("gpt2-tiny", 1, 2)
+    _compare(got, ref_params, ref_grads0, 2)
 
 
 def _grad_worker(rank, world, port, out_path):
