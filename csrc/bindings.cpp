@@ -39,7 +39,8 @@ std::tuple<at::Tensor, at::Tensor> dlgm_flash_attn_fwd(const at::Tensor& q, cons
 std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Tensor& dout, const at::Tensor& q,
                                                                    const at::Tensor& k, const at::Tensor& v,
                                                                    const at::Tensor& out, const at::Tensor& lse,
-                                                                   double softmax_scale, bool causal);
+                                                                   double softmax_scale, bool causal,
+                                                                   const c10::optional<at::Tensor>& dqkv);
 
 // moe.hip
 at::Tensor dlgm_moe_combine_fwd(const at::Tensor& y, const at::Tensor& pos, const c10::optional<at::Tensor>& gates);
@@ -60,7 +61,7 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("flash_attn_fwd(Tensor q, Tensor k, Tensor v, float softmax_scale, bool causal) -> (Tensor, Tensor)");
   m.def("moe_combine_fwd(Tensor y, Tensor pos, Tensor? gates) -> Tensor");
   m.def("moe_combine_bwd(Tensor dout, Tensor y, Tensor pos, Tensor gates) -> (Tensor, Tensor)");
-  m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, float softmax_scale, bool causal) -> (Tensor, Tensor, Tensor)");
+  m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, float softmax_scale, bool causal, Tensor? dqkv=None) -> (Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(dlgm, CUDA, m) {

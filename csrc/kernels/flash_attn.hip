@@ -318,6 +318,8 @@ struct BwdParams {
   int64_t k_sb, k_ss, k_sh;
   int64_t v_sb, v_ss, v_sh;
   int64_t do_sb, do_ss, do_sh;
+  int64_t dq_ss, dkv_ss;  // token (row) strides of the dq and dk/dv outputs: Hq*D / Hkv*D, or the fused
+                          // [T, (Hq + 2 Hkv) D] dQKV row when the caller hands over one buffer
   int B, S, Hq, Hkv;
   float scale;       // softmax scale
   float scale_log2;  // scale * log2(e)
@@ -489,8 +491,8 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
   }
   if (key >= p.S) return;
   if (group == 1) {
-    bf16* dkr = p.dk + (((int64_t)b * p.S + key) * p.Hkv + hk) * D;
-    bf16* dvr = p.dv + (((int64_t)b * p.S + key) * p.Hkv + hk) * D;
+    bf16* dkr = p.dk + ((int64_t)b * p.S + key) * p.dkv_ss + hk * D;
+    bf16* dvr = p.dv + ((int64_t)b * p.S + key) * p.dkv_ss + hk * D;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -520,9 +522,10 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
 
 // Sum the per-q-head fp32 partials of the GQA group (fixed order: deterministic) -> bf16.
 __global__ __launch_bounds__(256) void gqa_reduce_kernel(const float* __restrict__ part, bf16* __restrict__ out,
-                                                         int group, int64_t n) {
+                                                         int group, int64_t n, int row_len, int64_t out_stride) {
   const int64_t nv = n >> 3;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = (i * 8) / row_len, col = (i * 8) - row * row_len;
     f32x8 s = (f32x8)(0.f);
     for (int gq = 0; gq < group; ++gq) {
       const float* src = part + gq * n + i * 8;
@@ -530,7 +533,7 @@ __global__ __launch_bounds__(256) void gqa_reduce_kernel(const float* __restrict
       f32x4 c = *reinterpret_cast<const f32x4*>(src + 4);
       s += (f32x8){a[0], a[1], a[2], a[3], c[0], c[1], c[2], c[3]};
     }
-    store8f(out + i * 8, s);
+    store8f(out + row * out_stride + col, s);
   }
 }
 
@@ -650,7 +653,7 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams p
     __syncthreads();
   }
   if (qcol < p.S) {
-    bf16* orow = p.dq + (((int64_t)b * p.S + qcol) * p.Hq + hq) * D;
+    bf16* orow = p.dq + ((int64_t)b * p.S + qcol) * p.dq_ss + hq * D;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -706,7 +709,8 @@ std::tuple<at::Tensor, at::Tensor> dlgm_flash_attn_fwd(const at::Tensor& q, cons
 std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Tensor& dout, const at::Tensor& q,
                                                                    const at::Tensor& k, const at::Tensor& v,
                                                                    const at::Tensor& out, const at::Tensor& lse,
-                                                                   double softmax_scale, bool causal) {
+                                                                   double softmax_scale, bool causal,
+                                                                   const c10::optional<at::Tensor>& dqkv) {
   check_qkv(q, "q");
   check_qkv(k, "k");
   check_qkv(v, "v");
@@ -718,9 +722,25 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
   TORCH_CHECK(out.is_contiguous() && out.sizes() == q.sizes(), "flash_attn_bwd: out must be contiguous [B,S,Hq,D]");
   TORCH_CHECK(lse.is_contiguous() && lse.numel() == (int64_t)B * Hq * S, "flash_attn_bwd: bad lse");
   TORCH_CHECK(dout.sizes() == q.sizes(), "flash_attn_bwd: dout shape mismatch");
-  auto dk = at::empty({B, S, Hkv, D}, q.options());
-  auto dv = at::empty({B, S, Hkv, D}, q.options());
-  auto dq = at::empty({B, S, Hq, D}, q.options());
+  at::Tensor dq, dk, dv;
+  int64_t dq_ss = (int64_t)Hq * D, dkv_ss = (int64_t)Hkv * D;
+  if (dqkv.has_value()) {
+    // one fused [B*S, (Hq + 2 Hkv) D] gradient: the layout of the QKV projection output, so the
+    // caller's inverse RoPE and dW/dX GEMMs read it without a concatenation pass
+    const int64_t C = (int64_t)(Hq + 2 * Hkv) * D;
+    const at::Tensor& f = *dqkv;
+    TORCH_CHECK(f.is_cuda() && f.scalar_type() == at::kBFloat16 && f.is_contiguous() && f.numel() == (int64_t)B * S * C,
+                "flash_attn_bwd: dqkv must be a contiguous bf16 [B*S, (Hq+2Hkv)*D] tensor");
+    auto f3 = f.view({B, S, C});
+    dq = f3.narrow(2, 0, (int64_t)Hq * D).unflatten(2, {Hq, D});
+    dk = f3.narrow(2, (int64_t)Hq * D, (int64_t)Hkv * D).unflatten(2, {Hkv, D});
+    dv = f3.narrow(2, (int64_t)(Hq + Hkv) * D, (int64_t)Hkv * D).unflatten(2, {Hkv, D});
+    dq_ss = dkv_ss = C;
+  } else {
+    dk = at::empty({B, S, Hkv, D}, q.options());
+    dv = at::empty({B, S, Hkv, D}, q.options());
+    dq = at::empty({B, S, Hq, D}, q.options());
+  }
   if (B == 0 || S == 0) return {dq.zero_(), dk.zero_(), dv.zero_()};
   auto delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
   at::Tensor dk_part, dv_part;
@@ -745,8 +765,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
               reinterpret_cast<bf16*>(dq.data_ptr()), group > 1 ? dk_part.data_ptr<float>() : nullptr,
               group > 1 ? dv_part.data_ptr<float>() : nullptr, reinterpret_cast<bf16*>(dk.data_ptr()),
               reinterpret_cast<bf16*>(dv.data_ptr()), q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1),
-              k.stride(2), v.stride(0), v.stride(1), v.stride(2), dout.stride(0), dout.stride(1), dout.stride(2), B, S,
-              Hq, Hkv, (float)softmax_scale, (float)(softmax_scale * kLog2e), causal};
+              k.stride(2), v.stride(0), v.stride(1), v.stride(2), dout.stride(0), dout.stride(1), dout.stride(2), dq_ss,
+              dkv_ss, B, S, Hq, Hkv, (float)softmax_scale, (float)(softmax_scale * kLog2e), causal};
   const int64_t kv_blocks = (int64_t)B * Hq * ((S + kKvBKV - 1) / kKvBKV);
   const int64_t dq_blocks = (int64_t)B * Hq * ((S + kDqBQ - 1) / kDqBQ);
   if (D == 128) {
@@ -761,9 +781,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
     const int64_t n = (int64_t)B * S * Hkv * D;
     const int64_t grid = std::min<int64_t>((n / 8 + 255) / 256, 4096);
     gqa_reduce_kernel<<<grid, 256, 0, stream>>>(dk_part.data_ptr<float>(), reinterpret_cast<bf16*>(dk.data_ptr()),
-                                                group, n);
+                                                group, n, Hkv * D, dkv_ss);
     gqa_reduce_kernel<<<grid, 256, 0, stream>>>(dv_part.data_ptr<float>(), reinterpret_cast<bf16*>(dv.data_ptr()),
-                                                group, n);
+                                                group, n, Hkv * D, dkv_ss);
     DLGM_CHECK_HIP(hipGetLastError());
   }
   return {dq, dk, dv};

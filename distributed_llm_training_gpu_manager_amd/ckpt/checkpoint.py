@@ -96,8 +96,8 @@ class AsyncCheckpointer:
 
     # ------------------------------------------------------------------ policy
     def _pick_mode(self, mode: str) -> str:
-        if not self.cuda:
-            return "host"
+        if not self.cuda or getattr(self.engine, "offload", None) is not None:
+            return "host"  # offloaded optimizer state already lives in host memory
         if mode != "auto":
             return mode
         free, _ = torch.cuda.mem_get_info(self.dev)

@@ -60,6 +60,7 @@ def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, **overri
         hysteresis=int(ds.get("fp16", {}).get("hysteresis", 2)),
         min_loss_scale=float(ds.get("fp16", {}).get("min_loss_scale", 1.0)),
         offload_optimizer=off_o,
+        nvme_path=zo.get("offload_optimizer", {}).get("nvme_path"),
     )
     for k, v in overrides.items():
         setattr(cfg, k, v)

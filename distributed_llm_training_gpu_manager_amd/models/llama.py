@@ -118,8 +118,8 @@ class LlamaBlock(Unit):
         grad_mm(g["wo"], dh.t(), attn2d, acc)
         dattn = torch.mm(dh, p["wo"]).view_as(attn)
         q, k, v = self._split(qkv, B, S)
-        dq, dk, dv = ops.flash_attn_bwd(dattn, q, k, v, attn, lse, causal=True)
-        dqkv = torch.cat([dq.view(T, -1), dk.view(T, -1), dv.view(T, -1)], dim=1)
+        dqkv = torch.empty_like(qkv).view(T, -1)
+        ops.flash_attn_bwd(dattn, q, k, v, attn, lse, causal=True, dqkv=dqkv)
         cos, sin = ctx.rope
         ops.rope_(dqkv, cos, sin, c.n_heads + c.n_kv_heads, c.head_dim, S, inverse=True)
         grad_mm(g["wqkv"], dqkv.t(), hn1, acc)

@@ -71,12 +71,25 @@ def flash_attn_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, softmax_sc
     return _ref_fwd(q, k, v, scale, causal)
 
 
-def flash_attn_bwd(dout, q, k, v, out, lse, softmax_scale: Optional[float] = None, causal: bool = True):
+def flash_attn_bwd(dout, q, k, v, out, lse, softmax_scale: Optional[float] = None, causal: bool = True,
+                   dqkv: Optional[torch.Tensor] = None):
+    """(dq, dk, dv). With ``dqkv`` (contiguous [B*S, (Hq+2Hkv)*D]) the three gradients are written
+    straight into that fused buffer (the QKV projection layout) and returned as views of it."""
     scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(q.shape[-1])
     if use_native(q):
         return hip_ops().flash_attn_bwd(dout.contiguous() if dout.stride(-1) != 1 else dout, q, k, v, out, lse,
-                                        scale, causal)
-    return _ref_bwd(dout, q, k, v, out, lse, scale, causal)
+                                        scale, causal, dqkv)
+    dq, dk, dv = _ref_bwd(dout, q, k, v, out, lse, scale, causal)
+    if dqkv is None:
+        return dq, dk, dv
+    B, S = q.shape[:2]
+    f = dqkv.view(B, S, -1)
+    nq, nk = dq.shape[2] * dq.shape[3], dk.shape[2] * dk.shape[3]
+    f[..., :nq].copy_(dq.reshape(B, S, nq))
+    f[..., nq:nq + nk].copy_(dk.reshape(B, S, nk))
+    f[..., nq + nk:].copy_(dv.reshape(B, S, nk))
+    return (f[..., :nq].unflatten(2, dq.shape[2:]), f[..., nq:nq + nk].unflatten(2, dk.shape[2:]),
+            f[..., nq + nk:].unflatten(2, dv.shape[2:]))
 
 
 def sdpa_fwd_bwd_reference(q, k, v, dout, causal=True):

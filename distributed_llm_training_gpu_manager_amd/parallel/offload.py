@@ -1,0 +1,192 @@
+"""ZeRO-Offload: the fp32 optimizer partition in host memory, updated by the C++ AdamW.
+
+Parity path for the reference's ``offload_optimizer`` knob
+(``ai_engine/deepspeed_launcher.py:197-212``; default ``OffloadDevice.CPU`` at ``:39``;
+presets 7b/13b/70b at ``:372-407``) -- SURVEY.md §2.5 N2/N3, §2.7 C9. On MI355X the
+288 GB of HBM3E holds the full Llama-3-70B optimizer partition at W = 8, so this is
+not the hot path; it exists so that every reference config runs.
+
+Layout
+    master, exp_avg, exp_avg_sq  fp32 [shard_total]   pinned host RAM ("cpu"), or
+                                                        file-backed mmap under nvme_path ("nvme")
+    grad_shard, p16_shard         stay on the GPU
+
+Step (one HIP side stream, two pinned staging slots per direction)
+    D2H  grad chunk i+1      (copy engine)
+    CPU  AdamW chunk i       (csrc/host/ckpt_io.cpp dlgm_cpu_adamw: AVX2/FMA, OpenMP)
+    H2D  bf16 params chunk i-1
+so PCIe traffic in both directions overlaps the host update.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional
+
+import torch
+
+from .. import _host
+
+CHUNK_ELEMS = 32 << 20  # 128 MiB of fp32 gradient per staging slot
+
+
+class HostOffloadOptimizer:
+    def __init__(self, numel: int, device: torch.device, kind: str = "cpu", nvme_path: Optional[str] = None,
+                 rank: int = 0, chunk_elems: int = CHUNK_ELEMS):
+        assert kind in ("cpu", "nvme"), kind
+        if _host.lib() is None:
+            raise RuntimeError("optimizer offload needs the host runtime (_dlgm_host.so); run build()")
+        self.n, self.device, self.kind = numel, device, kind
+        self.cuda = device.type == "cuda"
+        self.chunk = max(1, min(chunk_elems, numel))
+        self.files: List[str] = []
+        if kind == "nvme":
+            root = nvme_path or os.environ.get("DLGM_NVME_PATH", "/tmp/dlgm_nvme")
+            os.makedirs(root, exist_ok=True)
+            self.master, self.exp_avg, self.exp_avg_sq = (self._mmap(root, rank, nm) for nm in
+                                                          ("master", "exp_avg", "exp_avg_sq"))
+        else:
+            mk = lambda: torch.zeros(numel, dtype=torch.float32, pin_memory=self.cuda)  # noqa: E731
+            self.master, self.exp_avg, self.exp_avg_sq = mk(), mk(), mk()
+        if self.cuda:
+            self.stream = torch.cuda.Stream(device)
+            self.gslot = [torch.empty(self.chunk, dtype=torch.float32, pin_memory=True) for _ in range(2)]
+            self.pslot = [torch.empty(self.chunk, dtype=torch.bfloat16, pin_memory=True) for _ in range(2)]
+
+    def _mmap(self, root: str, rank: int, name: str) -> torch.Tensor:
+        path = os.path.join(root, f"zero_offload_r{rank}.{name}.f32")
+        with open(path, "wb") as f:
+            f.truncate(self.n * 4)  # sparse file: zeros
+        self.files.append(path)
+        return torch.from_file(path, shared=True, size=self.n, dtype=torch.float32)
+
+    def host_bytes(self) -> int:
+        return 3 * self.n * 4
+
+    # ------------------------------------------------------------------ params
+    def push_params(self, p16_shard: torch.Tensor) -> None:
+        """p16_shard <- bf16(master) (initialisation / restore)."""
+        for off in range(0, self.n, self.chunk):
+            ln = min(self.chunk, self.n - off)
+            p16_shard.narrow(0, off, ln).copy_(self.master.narrow(0, off, ln).to(torch.bfloat16))
+
+    # ------------------------------------------------------------------ step
+    def step(self, grad_shard: torch.Tensor, p16_shard: torch.Tensor, *, lr: float, beta1: float, beta2: float,
+             eps: float, weight_decay: float, step: int, gscale: float) -> None:
+        bc1 = 1.0 - beta1 ** step
+        bc2 = 1.0 - beta2 ** step
+        hyper = (lr, beta1, beta2, eps, weight_decay, bc1, bc2, gscale)
+        if not self.cuda:
+            _host.cpu_adamw_(self.master, self.exp_avg, self.exp_avg_sq, grad_shard,
+                             p16_shard if p16_shard.dtype == torch.bfloat16 else None, *hyper)
+            if p16_shard.dtype != torch.bfloat16:
+                p16_shard.copy_(self.master)
+            return
+        chunks = [(off, min(self.chunk, self.n - off)) for off in range(0, self.n, self.chunk)]
+        cur = torch.cuda.current_stream(self.device)
+        s = self.stream
+        s.wait_stream(cur)  # gradients final
+        d2h: List[Optional[torch.cuda.Event]] = [None] * len(chunks)
+        h2d: List[Optional[torch.cuda.Event]] = [None, None]
+
+        def issue_d2h(i: int) -> None:
+            off, ln = chunks[i]
+            with torch.cuda.stream(s):
+                self.gslot[i % 2][:ln].copy_(grad_shard.narrow(0, off, ln), non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(s)
+            d2h[i] = ev
+
+        issue_d2h(0)
+        for i, (off, ln) in enumerate(chunks):
+            if i + 1 < len(chunks):
+                issue_d2h(i + 1)  # slot (i+1)%2 was consumed by the host update of chunk i-1
+            d2h[i].synchronize()
+            slot = i % 2
+            if h2d[slot] is not None:
+                h2d[slot].synchronize()  # the H2D of chunk i-2 has drained this bf16 staging slot
+            _host.cpu_adamw_(self.master.narrow(0, off, ln), self.exp_avg.narrow(0, off, ln),
+                             self.exp_avg_sq.narrow(0, off, ln), self.gslot[slot][:ln], self.pslot[slot][:ln], *hyper)
+            with torch.cuda.stream(s):
+                p16_shard.narrow(0, off, ln).copy_(self.pslot[slot][:ln], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(s)
+            h2d[slot] = ev
+        cur.wait_stream(s)  # compute resumes on the updated bf16 params
+
+    def close(self) -> None:
+        for p in self.files:
+            try:
+                os.remove(p)
+            except OSError:
+                pass
+
+
+class ActivationOffloader:
+    """``cpu_checkpointing`` (reference ``activation_checkpointing.cpu_checkpointing``, 70b preset,
+    ``deepspeed_launcher.py:215-223, :403``): the per-unit checkpointed inputs kept for recompute
+    are streamed to pinned host memory on a side HIP stream during the forward and streamed back,
+    one unit ahead, during the backward."""
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.cuda = device.type == "cuda"
+        self.stream = torch.cuda.Stream(device) if self.cuda else None
+        self._pool: dict = {}
+
+    def _host_buf(self, t: torch.Tensor) -> torch.Tensor:
+        key = (tuple(t.shape), t.dtype)
+        free = self._pool.setdefault(key, [])
+        return free.pop() if free else torch.empty(t.shape, dtype=t.dtype, pin_memory=self.cuda)
+
+    def _map(self, x, fn):
+        if x is None:
+            return None
+        if isinstance(x, torch.Tensor):
+            return fn(x)
+        return tuple(self._map(e, fn) for e in x)
+
+    def push(self, x):
+        """Start the D2H copy of `x` (tensor / tuple of tensors / None); returns a handle."""
+        if not self.cuda:
+            return ("host", self._map(x, lambda t: self._host_buf(t).copy_(t)), None, None)
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            host = self._map(x, lambda t: self._host_buf(t).copy_(t, non_blocking=True))
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        return ("host", host, ev, x)  # keep the device tensors alive until the copy has drained
+
+    def release_device(self, h):
+        """Drop the device copy once its D2H has finished (call after the next unit's forward)."""
+        if h[0] != "host" or h[3] is None:
+            return h
+        h[2].synchronize()
+        return ("host", h[1], None, None)
+
+    def prefetch(self, h):
+        """Start the H2D copy back; returns a handle for :meth:`get`."""
+        if h[0] != "host":
+            return h
+        host = h[1]
+        if not self.cuda:
+            return ("dev", host, None, host)
+        if h[2] is not None:
+            self.stream.wait_event(h[2])
+        with torch.cuda.stream(self.stream):
+            dev = self._map(host, lambda t: t.to(self.device, non_blocking=True))
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        return ("dev", dev, ev, host)
+
+    def get(self, h):
+        if h[0] == "host":
+            h = self.prefetch(h)
+        _, dev, ev, host = h
+        if ev is not None:
+            cur = torch.cuda.current_stream(self.device)
+            cur.wait_event(ev)
+            self._map(dev, lambda t: t.record_stream(cur))  # allocated on the side stream, consumed here
+            ev.synchronize()  # the host staging buffers may be reused after this
+        self._map(host, lambda t: self._pool.setdefault((tuple(t.shape), t.dtype), []).append(t))
+        return dev

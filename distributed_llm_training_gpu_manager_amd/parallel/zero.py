@@ -74,7 +74,8 @@ class EngineConfig:
     prefetch: bool = True
     seed: int = 1234
     expert_parallel_size: int = 1
-    offload_optimizer: str = "none"  # none | cpu (ZeRO-Offload parity path, C++ AVX2 AdamW on pinned host state)
+    offload_optimizer: str = "none"  # none | cpu | nvme (ZeRO-Offload parity path: parallel/offload.py)
+    nvme_path: Optional[str] = None
     init_device: str = "auto"  # "cpu" gives bit-identical init on any device (tests); auto: cpu below 1e9 params
     fp16: bool = False  # dynamic loss scaling path (reference fp16 block)
     loss_scale: float = 0.0  # 0 = dynamic
@@ -221,6 +222,7 @@ class ZeroEngine:
                 self._bwd_last_visit[gi] = min(si, self._bwd_last_visit.get(gi, si))
         self._live: Dict[int, Tuple[torch.Tensor, Handle]] = {}
         self._gbuf_pool: Dict[int, List[torch.Tensor]] = {}
+        self._act_offload = None
         self.fault_inject_nan = False  # fault injection: poison one gradient element on the next micro-step
         self.timers: Dict[str, float] = {}
         self.hooks: List[Any] = []  # callables(engine, metrics) after each step (NaN trap, monitors)
@@ -230,9 +232,16 @@ class ZeroEngine:
     def _alloc(self) -> None:
         dev, n = self.device, self.shard_total
         f32 = dict(dtype=torch.float32, device=dev)
-        self.master = torch.zeros(n, **f32)
-        self.exp_avg = torch.zeros(n, **f32)
-        self.exp_avg_sq = torch.zeros(n, **f32)
+        self.offload = None
+        if self.cfg.offload_optimizer in ("cpu", "nvme"):
+            from .offload import HostOffloadOptimizer
+            self.offload = HostOffloadOptimizer(n, dev, self.cfg.offload_optimizer, self.cfg.nvme_path, self.rank)
+            self.master, self.exp_avg, self.exp_avg_sq = (self.offload.master, self.offload.exp_avg,
+                                                          self.offload.exp_avg_sq)
+        else:
+            self.master = torch.zeros(n, **f32)
+            self.exp_avg = torch.zeros(n, **f32)
+            self.exp_avg_sq = torch.zeros(n, **f32)
         self.grad_shard = torch.zeros(n, **f32)
         self.p16_shard = torch.zeros(n, dtype=self.dtype, device=dev)
         self.p16_full = None
@@ -262,7 +271,14 @@ class ZeroEngine:
             if self.p16_full is not None and self.p16_full is not self.p16_shard:
                 self.p16_full.narrow(0, g.full_off, g.numel).copy_(full)
             del full
-        ops.cast_f32_bf16_(self.p16_shard, self.master) if self.dtype == torch.bfloat16 else \
+        self._p16_from_master()
+
+    def _p16_from_master(self) -> None:
+        if self.offload is not None:
+            self.offload.push_params(self.p16_shard)
+        elif self.dtype == torch.bfloat16:
+            ops.cast_f32_bf16_(self.p16_shard, self.master)
+        else:
             self.p16_shard.copy_(self.master)
 
     # ------------------------------------------------------------------ params
@@ -380,6 +396,12 @@ class ZeroEngine:
         saved: List[Any] = [None] * n
         x: Any = None
         ckpt = self.cfg.activation_checkpointing
+        act = None
+        if ckpt and self.cfg.cpu_checkpointing:
+            if self._act_offload is None:
+                from .offload import ActivationOffloader
+                self._act_offload = ActivationOffloader(self.device)
+            act = self._act_offload
         # ---- forward
         last_gis = self.stages[-1][1]
         for si, (unit, gis) in enumerate(self.stages):
@@ -388,7 +410,9 @@ class ZeroEngine:
                 self._issue_gathers(self.stages[si + 1][1])
             if ckpt and si < n - 1:
                 y, _ = unit.forward(p, x, ctx)
-                saved[si] = ("ckpt", x)
+                saved[si] = ("ckpt", act.push(x) if act is not None else x)
+                if act is not None and si > 0:
+                    saved[si - 1] = ("ckpt", act.release_device(saved[si - 1][1]))
             else:
                 y, saved[si] = unit.forward(p, x, ctx)
             self.release(tuple(gi for gi in gis if gi not in last_gis))  # the head stays gathered for backward
@@ -428,7 +452,12 @@ class ZeroEngine:
                             v.zero_()
             sv = saved[si]
             if isinstance(sv, tuple) and len(sv) == 2 and isinstance(sv[0], str) and sv[0] == "ckpt":
-                _, sv = unit.forward(p, sv[1], ctx)
+                xin = sv[1]
+                if act is not None:
+                    xin = act.get(xin)
+                    if si > 0 and isinstance(saved[si - 1], tuple) and saved[si - 1][0] == "ckpt":
+                        saved[si - 1] = ("ckpt", act.prefetch(saved[si - 1][1]))  # one unit ahead
+                _, sv = unit.forward(p, xin, ctx)
             dy = unit.backward(p, gv, sv, dy, ctx)
             saved[si] = None
             visited.update(gis)
@@ -451,7 +480,7 @@ class ZeroEngine:
 
     def sync_params_from_master(self) -> None:
         """Recompute the bf16 compute copies from the fp32 master (after restore / external edits)."""
-        ops.cast_f32_bf16_(self.p16_shard, self.master)
+        self._p16_from_master()
         if self.stage in (1, 2):
             hs = [g.comm.all_gather(self.p16_full.narrow(0, g.full_off, g.numel), self._shard16(g), async_op=True)
                   for g in self.groups]
@@ -488,12 +517,15 @@ class ZeroEngine:
         self._global_grad_stats()
         lr = lr_at(cfg, self.step_count)
         inv_scale = 1.0 / self.scaler.scale if self.scaler else 1.0
-        ops.adamw_step_(self.master, self.exp_avg, self.exp_avg_sq, self.grad_shard,
-                        self.p16_shard if self.dtype == torch.bfloat16 else None, self.stats, lr=lr,
-                        beta1=cfg.betas[0], beta2=cfg.betas[1], eps=cfg.eps, weight_decay=cfg.weight_decay,
-                        step=self.step_count, grad_scale=inv_scale, max_norm=cfg.grad_clip)
-        if self.dtype != torch.bfloat16:
-            self.p16_shard.copy_(self.master)
+        if self.offload is not None:
+            self._offload_step(lr, inv_scale)
+        else:
+            ops.adamw_step_(self.master, self.exp_avg, self.exp_avg_sq, self.grad_shard,
+                            self.p16_shard if self.dtype == torch.bfloat16 else None, self.stats, lr=lr,
+                            beta1=cfg.betas[0], beta2=cfg.betas[1], eps=cfg.eps, weight_decay=cfg.weight_decay,
+                            step=self.step_count, grad_scale=inv_scale, max_norm=cfg.grad_clip)
+            if self.dtype != torch.bfloat16:
+                self.p16_shard.copy_(self.master)
         if self.stage in (1, 2):
             hs = []
             for g in self.groups:
@@ -504,6 +536,20 @@ class ZeroEngine:
         if self.scaler is not None:
             self.scaler.update(bool(self.stats[1].item() > 0))
         return {"lr": lr, "stats": self.stats}
+
+    def _offload_step(self, lr: float, inv_scale: float) -> None:
+        """Host AdamW over the offloaded partition; the clip / overflow decision needs the stats on the host
+        (same formula as the device kernel, csrc/kernels/optim.hip clip_coef)."""
+        cfg = self.cfg
+        sumsq, nonfinite = (float(x) for x in self.stats.tolist())
+        if nonfinite > 0:
+            return
+        coef = inv_scale
+        if cfg.grad_clip > 0:
+            norm = math.sqrt(sumsq) * inv_scale
+            coef *= min(1.0, cfg.grad_clip / (norm + 1e-6))
+        self.offload.step(self.grad_shard, self.p16_shard, lr=lr, beta1=cfg.betas[0], beta2=cfg.betas[1],
+                          eps=cfg.eps, weight_decay=cfg.weight_decay, step=self.step_count, gscale=coef)
 
     def train_step(self, micro_batches: Sequence[Tuple[torch.Tensor, torch.Tensor]]) -> Dict[str, Any]:
         """Run len(micro_batches) == grad_accum micro-batches and one optimizer step.
@@ -541,6 +587,8 @@ class ZeroEngine:
         out = {}
         for g in self.groups:
             shard = buf.narrow(0, g.shard_off, g.shard_numel)
+            if shard.device != self.device:  # offloaded optimizer state: collectives run on device tensors
+                shard = shard.to(self.device)
             if g.P > 1:
                 full = torch.empty(g.numel, dtype=torch.float32, device=self.device)
                 g.comm.all_gather(full, shard, async_op=False).wait()
@@ -558,7 +606,8 @@ class ZeroEngine:
     def memory_report(self) -> Dict[str, float]:
         gb = 1024 ** 3
         rep = {
-            "optimizer_state_GiB": 3 * self.shard_total * 4 / gb,
+            "optimizer_state_GiB": 0.0 if self.offload is not None else 3 * self.shard_total * 4 / gb,
+            "optimizer_state_host_GiB": 3 * self.shard_total * 4 / gb if self.offload is not None else 0.0,
             "grad_shard_GiB": self.shard_total * 4 / gb,
             "param_shard_GiB": self.shard_total * 2 / gb,
             "param_full_GiB": (self.full_total * 2 / gb) if self.p16_full is not None else 0.0,

@@ -213,3 +213,25 @@ def test_moe_combine_fwd_bwd(K):
     dy_ref, dg_ref = moe_combine_bwd(dout, y, pos, gates)
     dy, dg = moe_combine_bwd(dout.to(DEV), y.to(DEV), pos.to(DEV), gates.to(DEV))
     assert rel_err(dy, dy_ref) < 1e-2 and rel_err(dg, dg_ref) < 1e-3
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(4, 4), (8, 2)])
+def test_flash_attention_bwd_fused_dqkv_output(Hq, Hkv):
+    """dq/dk/dv written straight into one [T, (Hq+2Hkv)D] buffer == the separate outputs."""
+    torch.manual_seed(0)
+    B, S, D = 2, 192, 128
+    qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, dtype=torch.bfloat16, device=DEV)
+    base = qkv.view(B, S, -1)
+    q = base[..., : Hq * D].unflatten(2, (Hq, D))
+    k = base[..., Hq * D:(Hq + Hkv) * D].unflatten(2, (Hkv, D))
+    v = base[..., (Hq + Hkv) * D:].unflatten(2, (Hkv, D))
+    scale = 1 / math.sqrt(D)
+    o, lse = ops.flash_attn_fwd(q, k, v, scale, True)
+    do = torch.randn(B, S, Hq, D, dtype=torch.bfloat16, device=DEV)
+    dq, dk, dv = ops.flash_attn_bwd(do, q, k, v, o, lse, scale, True)
+    fused = torch.full_like(qkv, float("nan"))
+    fq, fk, fv = ops.flash_attn_bwd(do, q, k, v, o, lse, scale, True, dqkv=fused)
+    assert not torch.isnan(fused).any()
+    assert torch.equal(fq, dq) and torch.equal(fk, dk) and torch.equal(fv, dv)
+    ref = torch.cat([dq.reshape(B * S, -1), dk.reshape(B * S, -1), dv.reshape(B * S, -1)], 1)
+    assert torch.equal(fused, ref)

@@ -1,0 +1,93 @@
+"""Tune the Llama-3 GEMM shapes with PyTorch TunableOp (hipBLASLt + rocBLAS solution search).
+
+Writes the winning solutions to ``distributed_llm_training_gpu_manager_amd/tuned/`` (loaded by
+``utils.gemm_tuning.enable_tuned_gemms``) and prints default-vs-tuned times per shape.
+
+    python tools/tune_gemms.py --model llama3-8b --tokens 8192
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from distributed_llm_training_gpu_manager_amd.models import get_config  # noqa: E402
+
+
+def shapes(cfg, T):
+    ws = {"wqkv": (cfg.qkv_dim, cfg.d_model), "wo": (cfg.d_model, cfg.n_heads * cfg.head_dim),
+          "w_gate_up": (2 * cfg.ffn_dim, cfg.d_model), "w_down": (cfg.d_model, cfg.ffn_dim),
+          "lm_head": (cfg.vocab_size, cfg.d_model)}
+    return ws
+
+
+def bench(fn, iters=10):
+    fn()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) / iters * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--tokens", type=int, default=8192)
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--max-ms", type=int, default=30)
+    a = ap.parse_args()
+    cfg = get_config(a.model)
+    T = a.tokens
+    dev = "cuda"
+    out_dir = a.out or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "distributed_llm_training_gpu_manager_amd", "tuned")
+    os.makedirs(out_dir, exist_ok=True)
+    cases = []
+    for name, (N, K) in shapes(cfg, T).items():
+        x = torch.randn(T, K, device=dev, dtype=torch.bfloat16)
+        w = torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02
+        dy = torch.randn(T, N, device=dev, dtype=torch.bfloat16)
+        g32 = torch.zeros(N, K, device=dev, dtype=torch.float32)
+        g16 = torch.empty(N, K, device=dev, dtype=torch.bfloat16)
+        fl = 2.0 * T * N * K
+        cases += [
+            (name + ".fwd", fl, lambda x=x, w=w: torch.mm(x, w.t())),
+            (name + ".dx", fl, lambda dy=dy, w=w: torch.mm(dy, w)),
+            (name + ".dw_bf16", fl, lambda dy=dy, x=x, g=g16: torch.mm(dy.t(), x, out=g)),
+            (name + ".dw_f32acc", fl, lambda dy=dy, x=x, g=g32: torch.addmm(g, dy.t(), x, beta=1.0,
+                                                                            out_dtype=torch.float32, out=g)),
+        ]
+    res = {}
+    for n, fl, fn in cases:
+        res[n] = {"default_ms": bench(fn)}
+    tun = torch.cuda.tunable
+    tun.enable(True)
+    tun.tuning_enable(True)
+    tun.set_max_tuning_duration(a.max_ms)
+    fname = os.path.join(out_dir, f"tunableop_{a.model}_T{T}.csv")
+    tun.set_filename(fname)
+    for n, fl, fn in cases:
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        res[n]["tune_s"] = time.perf_counter() - t0
+        print(f"tuned {n} in {res[n]['tune_s']:.1f}s", flush=True)
+    tun.write_file()
+    tun.tuning_enable(False)
+    for n, fl, fn in cases:
+        res[n]["tuned_ms"] = bench(fn)
+        res[n]["default_TF"] = fl / res[n]["default_ms"] / 1e9
+        res[n]["tuned_TF"] = fl / res[n]["tuned_ms"] / 1e9
+        print(f"{n:22s} default {res[n]['default_ms']:7.3f} ms {res[n]['default_TF']:7.1f} TF | "
+              f"tuned {res[n]['tuned_ms']:7.3f} ms {res[n]['tuned_TF']:7.1f} TF", flush=True)
+    print(json.dumps({"file": fname, "results": res}))
+
+
+if __name__ == "__main__":
+    main()
