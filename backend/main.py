@@ -58,3 +58,14 @@ def root():
 @app.get("/health")
 def health_check():
     return {"status": "healthy"}
+
+
+@app.get("/metrics")
+def prometheus_metrics():
+    """Prometheus scrape endpoint: training gauges (fed by /api/v1/monitoring/ingest) + GPU fleet."""
+    from fastapi import Response
+
+    from distributed_llm_training_gpu_manager_amd.utils import metrics as prom
+
+    prom.observe_fleet(gpu.manager._snapshot)
+    return Response(prom.render(), media_type=prom.CONTENT_TYPE_LATEST)

@@ -15,6 +15,8 @@ from pydantic import BaseModel
 from distributed_llm_training_gpu_manager_amd.health.loss_monitor import (
     LossSpikeMonitor, MonitorConfig, TrainingMetrics, json_safe)
 
+from distributed_llm_training_gpu_manager_amd.utils import metrics as prom
+
 router = APIRouter()
 _monitors: Dict[str, LossSpikeMonitor] = {}
 _lock = threading.Lock()
@@ -74,6 +76,9 @@ def ingest_metrics(request: MetricsIngestRequest):
     alerts = []
     for m in request.metrics:
         alerts.extend(monitor.ingest(m))
+        _observe(request.job_id, m)
+    for a in alerts:
+        prom.observe_alert(request.job_id, str(getattr(a, "alert_type", "unknown")))
     return _safe({"job_id": request.job_id, "ingested": len(request.metrics), "alerts_triggered": len(alerts),
                   "alerts": [a.model_dump() for a in alerts]})
 
@@ -81,12 +86,22 @@ def ingest_metrics(request: MetricsIngestRequest):
 @router.post("/ingest/single")
 def ingest_single_metric(request: SingleMetricRequest):
     monitor = _get_or_create_monitor(request.job_id)
-    alerts = monitor.ingest(TrainingMetrics(
+    m = TrainingMetrics(
         step=request.step, loss=request.loss, learning_rate=request.learning_rate,
         gradient_norm=request.gradient_norm, throughput_samples_per_sec=request.throughput_samples_per_sec,
-        gpu_memory_used_mib=request.gpu_memory_used_mib))
+        gpu_memory_used_mib=request.gpu_memory_used_mib)
+    alerts = monitor.ingest(m)
+    _observe(request.job_id, m)
+    for a in alerts:
+        prom.observe_alert(request.job_id, str(getattr(a, "alert_type", "unknown")))
     return _safe({"job_id": request.job_id, "step": request.step, "alerts": [a.model_dump() for a in alerts],
                   "healthy": len(alerts) == 0})
+
+
+def _observe(job_id: str, m: TrainingMetrics) -> None:
+    prom.observe_training(job_id, {"loss": m.loss, "grad_norm": m.gradient_norm, "learning_rate": m.learning_rate,
+                                   "throughput": m.throughput_samples_per_sec, "step": m.step,
+                                   "gpu_memory_used": (m.gpu_memory_used_mib or 0) / 1024.0})
 
 
 def _require(job_id: str) -> LossSpikeMonitor:

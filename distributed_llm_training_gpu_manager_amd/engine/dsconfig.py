@@ -61,6 +61,7 @@ def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, **overri
         min_loss_scale=float(ds.get("fp16", {}).get("min_loss_scale", 1.0)),
         offload_optimizer=off_o,
         nvme_path=zo.get("offload_optimizer", {}).get("nvme_path"),
+        wall_clock_breakdown=bool(ds.get("wall_clock_breakdown", False)),
     )
     for k, v in overrides.items():
         setattr(cfg, k, v)

@@ -91,6 +91,8 @@ class Trainer:
                                                  seed=args.seed), []
         if args.lr_scale != 1.0:
             self.ecfg.lr *= args.lr_scale
+        if getattr(args, "wall_clock_breakdown", False):
+            self.ecfg.wall_clock_breakdown = True
         self.engine = ZeroEngine(self.mcfg, self.ecfg, self.env.device, self.comm)
         self.monitor = LossSpikeMonitor(MonitorConfig())
         self.trap = NanTrap(self.env.device, self.monitor)
@@ -157,6 +159,8 @@ class Trainer:
                 self.pusher.push({"step": step, "loss": loss if math.isfinite(loss) else 1e30,
                                   "learning_rate": m["lr"], "gradient_norm": rec["grad_norm"]
                                   if math.isfinite(rec["grad_norm"]) else 1e30})
+                if step % a.log_interval == 0 and self.engine.timers.enabled:
+                    rec["wall_clock_breakdown_ms"] = {k: v["total_ms"] for k, v in self.engine.timers.summary().items()}
                 if step % a.log_interval == 0 or alerts:
                     self._say(json.dumps(rec) + ("" if not alerts else f" alerts={[x.alert_type for x in alerts]}"))
             first_attempt = os.environ.get("DLGM_RESTART", "0") == "0"
@@ -220,6 +224,7 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--job-id", default="local")
     ap.add_argument("--log-interval", type=int, default=1)
     ap.add_argument("--log-json", default=None)
+    ap.add_argument("--wall-clock-breakdown", action="store_true", help="per-phase HIP-event timers in the log")
     a, unknown = ap.parse_known_args(argv)
     return a
 

@@ -247,3 +247,48 @@ def write_status(step: int, **kw) -> None:
     with open(tmp, "w") as f:
         json.dump(rec, f)
     os.replace(tmp, path)
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    """``python -m ...launcher.supervisor [opts] -- <training command ...>``
+
+    Runs the command under a :class:`Supervisor` in the foreground (container entry point / CLI);
+    exits with the job's final code. SIGTERM/SIGINT cancel the job (the rank tree gets SIGTERM).
+    """
+    import argparse
+    import sys
+
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if "--" not in argv:
+        print("usage: supervisor [--max-restarts N] [--job-id ID] [--run-dir D] [--save-dir D] "
+              "[--heartbeat-timeout S] [--restart-on-preempt] -- <command ...>", file=sys.stderr)
+        return 2
+    cut = argv.index("--")
+    ap = argparse.ArgumentParser(prog="supervisor")
+    ap.add_argument("--max-restarts", type=int, default=3)
+    ap.add_argument("--job-id", default=f"job_{int(time.time())}")
+    ap.add_argument("--run-dir", default=None)
+    ap.add_argument("--save-dir", default=None)
+    ap.add_argument("--heartbeat-timeout", type=float, default=0.0)
+    ap.add_argument("--restart-on-preempt", action="store_true")
+    ap.add_argument("--no-auto-resume", action="store_true")
+    a = ap.parse_args(argv[:cut])
+    cmd = argv[cut + 1:]
+    spec = JobSpec(job_id=a.job_id, argv=cmd, auto_resume=not a.no_auto_resume, max_restarts=a.max_restarts,
+                   save_dir=a.save_dir, run_dir=a.run_dir, heartbeat_timeout_s=a.heartbeat_timeout,
+                   restart_on_preempt=a.restart_on_preempt)
+    job = Job(spec)
+    sup = Supervisor(job)
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, lambda *_: job._cancel.set())
+    sup.start()
+    while sup.is_alive():
+        sup.join(0.5)
+    print(json.dumps(job.to_dict(), default=str), flush=True)
+    if job.status == "succeeded":
+        return 0
+    return job.exit_codes[-1] if job.exit_codes and job.exit_codes[-1] > 0 else 1
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

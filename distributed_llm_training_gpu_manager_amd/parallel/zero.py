@@ -76,6 +76,7 @@ class EngineConfig:
     expert_parallel_size: int = 1
     offload_optimizer: str = "none"  # none | cpu | nvme (ZeRO-Offload parity path: parallel/offload.py)
     nvme_path: Optional[str] = None
+    wall_clock_breakdown: bool = False  # per-phase HIP-event timers (utils/timers.py)
     init_device: str = "auto"  # "cpu" gives bit-identical init on any device (tests); auto: cpu below 1e9 params
     fp16: bool = False  # dynamic loss scaling path (reference fp16 block)
     loss_scale: float = 0.0  # 0 = dynamic
@@ -224,7 +225,8 @@ class ZeroEngine:
         self._gbuf_pool: Dict[int, List[torch.Tensor]] = {}
         self._act_offload = None
         self.fault_inject_nan = False  # fault injection: poison one gradient element on the next micro-step
-        self.timers: Dict[str, float] = {}
+        from ..utils.timers import PhaseTimers
+        self.timers = PhaseTimers(device, enabled=cfg.wall_clock_breakdown)
         self.hooks: List[Any] = []  # callables(engine, metrics) after each step (NaN trap, monitors)
         self.pre_step_hooks: List[Any] = []  # callables(engine) before the optimizer touches master/m/v
 
@@ -403,6 +405,7 @@ class ZeroEngine:
                 self._act_offload = ActivationOffloader(self.device)
             act = self._act_offload
         # ---- forward
+        t_fwd = self.timers.mark()
         last_gis = self.stages[-1][1]
         for si, (unit, gis) in enumerate(self.stages):
             p = self.fetch(gis)
@@ -419,6 +422,7 @@ class ZeroEngine:
             x = y
         loss = x
         # ---- backward
+        t_bwd = self.timers.mark()
         dy: Any = None
         pending: List[Tuple[Handle, Any]] = []
         gbufs: Dict[int, torch.Tensor] = {}
@@ -473,6 +477,9 @@ class ZeroEngine:
                     self.release((gi,))
             self._drain(pending, keep=1)
         self._drain(pending, keep=0)
+        t_end = self.timers.mark()
+        self.timers.span("forward", t_fwd, t_bwd)
+        self.timers.span("backward+reduce", t_bwd, t_end)
         if self.stage == 3:
             self._live.clear()
         self.last_aux = ctx.aux
@@ -510,6 +517,12 @@ class ZeroEngine:
         self.stats.copy_(dense + exp)
 
     def optimizer_step(self) -> Dict[str, Any]:
+        t0 = self.timers.mark()
+        out = self._optimizer_step()
+        self.timers.span("optimizer_step", t0, self.timers.mark())
+        return out
+
+    def _optimizer_step(self) -> Dict[str, Any]:
         for hk in self.pre_step_hooks:
             hk(self)
         self.step_count += 1

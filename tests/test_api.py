@@ -94,3 +94,19 @@ def test_jobs_endpoints():
     assert client.get("/api/v1/training/jobs/none").status_code == 404
     assert client.post("/api/v1/training/jobs/none/cancel").status_code == 404
     assert client.post("/api/v1/training/jobs/none/preempt").status_code == 404
+
+
+def test_prometheus_metrics_endpoint():
+    from fastapi.testclient import TestClient
+
+    from backend.main import app
+
+    c = TestClient(app)
+    r = c.post("/api/v1/monitoring/ingest/single", json={"job_id": "prom-job", "step": 3, "loss": 2.5,
+                                                          "learning_rate": 1e-4, "gradient_norm": 0.7})
+    assert r.status_code == 200
+    r = c.get("/metrics")
+    assert r.status_code == 200
+    body = r.text
+    assert 'dlgm_train_loss{job="prom-job"} 2.5' in body
+    assert 'dlgm_train_step{job="prom-job"} 3.0' in body

@@ -143,3 +143,20 @@ def test_supervised_sigkill_auto_resume_mttr(tmp_path):
     assert job.exit_codes[0] == -signal.SIGKILL and job.restarts == 1
     assert "resumed from step 4" in log
     assert len(job.mttr_s) == 1 and job.mttr_s[0] > 0
+
+
+def test_wall_clock_breakdown_timers():
+    import torch
+
+    from distributed_llm_training_gpu_manager_amd.models import get_config
+    from distributed_llm_training_gpu_manager_amd.parallel.zero import EngineConfig, ZeroEngine
+
+    mc = get_config("llama-tiny")
+    eng = ZeroEngine(mc, EngineConfig(zero_stage=2, micro_batch_size=1, seq_len=16, grad_accum=2, init_device="cpu",
+                                      wall_clock_breakdown=True), torch.device("cpu"))
+    t = torch.randint(0, mc.vocab_size, (1, 17))
+    eng.train_step([(t[:, :-1], t[:, 1:])] * 2)
+    s = eng.timers.summary()
+    assert s["forward"]["count"] == 2 and s["backward+reduce"]["count"] == 2 and s["optimizer_step"]["count"] == 1
+    assert all(v["total_ms"] > 0 for v in s.values())
+    assert eng.timers.summary() == {}

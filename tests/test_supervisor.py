@@ -78,3 +78,25 @@ def test_heartbeat_loss_triggers_restart(tmp_path):
                              heartbeat_timeout_s=1.0, run_dir=str(tmp_path / "r4")))
     assert _wait(job, ("succeeded", "failed")) == "succeeded"
     assert job.restarts == 1 and any(e["event"] == "heartbeat_lost" for e in job.events)
+
+
+def test_supervisor_cli_restarts_then_succeeds(tmp_path):
+    """CLI entry point (infra/train-job.yaml): a command failing once is resumed and succeeds."""
+    import subprocess
+    import sys
+
+    marker = tmp_path / "failed_once"
+    script = tmp_path / "flaky.py"
+    script.write_text(
+        "import os, sys\n"
+        f"m = {str(marker)!r}\n"
+        "if not os.path.exists(m):\n"
+        "    open(m, 'w').close(); sys.exit(7)\n"
+        "assert '--resume=auto' in sys.argv\n")
+    r = subprocess.run([sys.executable, "-m", "distributed_llm_training_gpu_manager_amd.launcher.supervisor",
+                        "--max-restarts", "2", "--run-dir", str(tmp_path / "run"), "--",
+                        sys.executable, str(script)], capture_output=True, text=True, timeout=120,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stderr
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rec["status"] == "succeeded" and rec["restarts"] == 1 and rec["exit_codes"] == [7, 0]
