@@ -46,6 +46,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
 at::Tensor dlgm_moe_combine_fwd(const at::Tensor& y, const at::Tensor& pos, const c10::optional<at::Tensor>& gates);
 std::tuple<at::Tensor, at::Tensor> dlgm_moe_combine_bwd(const at::Tensor& dout, const at::Tensor& y,
                                                         const at::Tensor& pos, const at::Tensor& gates);
+// transpose.hip
+at::Tensor dlgm_transpose(const at::Tensor& x, const c10::optional<at::Tensor>& out);
 
 TORCH_LIBRARY(dlgm, m) {
   m.def("rmsnorm_fwd(Tensor x, Tensor? residual, Tensor w, float eps) -> (Tensor, Tensor, Tensor)");
@@ -61,6 +63,7 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("flash_attn_fwd(Tensor q, Tensor k, Tensor v, float softmax_scale, bool causal) -> (Tensor, Tensor)");
   m.def("moe_combine_fwd(Tensor y, Tensor pos, Tensor? gates) -> Tensor");
   m.def("moe_combine_bwd(Tensor dout, Tensor y, Tensor pos, Tensor gates) -> (Tensor, Tensor)");
+  m.def("transpose(Tensor x, Tensor(a!)? out=None) -> Tensor");
   m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, float softmax_scale, bool causal, Tensor? dqkv=None) -> (Tensor, Tensor, Tensor)");
 }
 
@@ -79,4 +82,5 @@ TORCH_LIBRARY_IMPL(dlgm, CUDA, m) {
   m.impl("flash_attn_bwd", &dlgm_flash_attn_bwd);
   m.impl("moe_combine_fwd", &dlgm_moe_combine_fwd);
   m.impl("moe_combine_bwd", &dlgm_moe_combine_bwd);
+  m.impl("transpose", &dlgm_transpose);
 }

@@ -77,6 +77,9 @@ class EngineConfig:
     offload_optimizer: str = "none"  # none | cpu | nvme (ZeRO-Offload parity path: parallel/offload.py)
     nvme_path: Optional[str] = None
     wall_clock_breakdown: bool = False  # per-phase HIP-event timers (utils/timers.py)
+    # parameter all-gathers on their own communicator (own RCCL stream), so a prefetch gather of the
+    # next block and the reduce-scatter of the previous block's gradients run concurrently on xGMI
+    separate_gather_comm: bool = True
     init_device: str = "auto"  # "cpu" gives bit-identical init on any device (tests); auto: cpu below 1e9 params
     fp16: bool = False  # dynamic loss scaling path (reference fp16 block)
     loss_scale: float = 0.0  # 0 = dynamic
@@ -104,6 +107,7 @@ class FlatGroup:
             off += _round_up(s.numel, ALIGN)
         self.numel = _round_up(max(off, 1), ALIGN * part_world)
         self.shard_numel = self.numel // part_world
+        self.gcomm = comm  # communicator for parameter all-gathers (the engine may give it its own)
         self.real_numel = sum(s.numel for s in specs)
         self.shard_off = 0
         self.full_off = 0
@@ -182,6 +186,10 @@ class ZeroEngine:
         ep_comm = ep_comm or self.ep_comm
         self.ep_comm = ep_comm
         ep_rank = self.ep_comm.rank if self.ep_comm is not None else 0
+        self.gather_comm = self.comm
+        if cfg.separate_gather_comm and self.W > 1 and self.stage > 0:
+            import torch.distributed as dist
+            self.gather_comm = Comm(dist.new_group(list(range(self.W))))
         groups, stages = build_model(model_cfg, ep_rank, self.ep_size)
         self.stages = [(u, tuple(gi) if isinstance(gi, (tuple, list)) else (gi,)) for u, gi in stages]
         self.groups = []
@@ -193,7 +201,9 @@ class ZeroEngine:
                 P_g = 1 if self.stage == 0 else comm_g.world
             else:
                 comm_g, P_g = self.comm, self.P
-            self.groups.append(FlatGroup(i, name, specs, P_g, kind, comm_g))
+            fg = FlatGroup(i, name, specs, P_g, kind, comm_g)
+            fg.gcomm = self.gather_comm if kind != "expert" else comm_g
+            self.groups.append(fg)
         self.has_experts = any(g.kind == "expert" for g in self.groups)
         soff = foff = 0
         for g in self.groups:
@@ -298,7 +308,7 @@ class ZeroEngine:
             self._live[gi] = (self._shard16(g), DONE)
         else:
             buf = torch.empty(g.numel, dtype=self.dtype, device=self.device)
-            self._live[gi] = (buf, g.comm.all_gather(buf, self._shard16(g), async_op=True))
+            self._live[gi] = (buf, g.gcomm.all_gather(buf, self._shard16(g), async_op=True))
 
     def _issue_gathers(self, gis) -> None:
         for gi in gis:
@@ -489,7 +499,7 @@ class ZeroEngine:
         """Recompute the bf16 compute copies from the fp32 master (after restore / external edits)."""
         self._p16_from_master()
         if self.stage in (1, 2):
-            hs = [g.comm.all_gather(self.p16_full.narrow(0, g.full_off, g.numel), self._shard16(g), async_op=True)
+            hs = [g.gcomm.all_gather(self.p16_full.narrow(0, g.full_off, g.numel), self._shard16(g), async_op=True)
                   for g in self.groups]
             for h in hs:
                 h.wait()
@@ -542,8 +552,8 @@ class ZeroEngine:
         if self.stage in (1, 2):
             hs = []
             for g in self.groups:
-                hs.append(g.comm.all_gather(self.p16_full.narrow(0, g.full_off, g.numel), self._shard16(g),
-                                            async_op=True))
+                hs.append(g.gcomm.all_gather(self.p16_full.narrow(0, g.full_off, g.numel), self._shard16(g),
+                                             async_op=True))
             for h in hs:
                 h.wait()
         if self.scaler is not None:

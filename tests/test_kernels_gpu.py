@@ -235,3 +235,36 @@ def test_flash_attention_bwd_fused_dqkv_output(Hq, Hkv):
     assert torch.equal(fq, dq) and torch.equal(fk, dk) and torch.equal(fv, dv)
     ref = torch.cat([dq.reshape(B * S, -1), dk.reshape(B * S, -1), dv.reshape(B * S, -1)], 1)
     assert torch.equal(fused, ref)
+
+
+@pytest.mark.parametrize("R,C", [(8192, 4096), (136, 72), (64, 8)])
+def test_transpose(R, C):
+    from distributed_llm_training_gpu_manager_amd.ops.gemm import transpose
+
+    x = torch.randn(R, C + 16, dtype=torch.bfloat16, device=DEV)[:, :C]  # row-strided view
+    assert torch.equal(transpose(x), x.t().contiguous())
+
+
+@pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 14336), (1000, 256)])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+def test_grad_mm_layouts(N, K, out_dtype):
+    """dW (+)= dy^T x through every operand-layout plan == fp32 reference."""
+    from distributed_llm_training_gpu_manager_amd.ops import gemm
+
+    torch.manual_seed(0)
+    T = 512
+    dy = torch.randn(T, N, dtype=torch.bfloat16, device=DEV)
+    x = torch.randn(T, K, dtype=torch.bfloat16, device=DEV)
+    ref = dy.float().t() @ x.float()
+    for plan in ("NN", "A", "B", "TN"):
+        orig = gemm._plan
+        gemm._plan = lambda a, b, p=plan: p
+        try:
+            out = torch.zeros(N, K, dtype=out_dtype, device=DEV)
+            gemm.grad_mm(out, dy.t(), x, acc=False)
+            assert rel_err(out, ref) < 1e-2, plan
+            if out_dtype == torch.float32:
+                gemm.grad_mm(out, dy.t(), x, acc=True)
+                assert rel_err(out, 2 * ref) < 1e-5 * 100, plan
+        finally:
+            gemm._plan = orig
