@@ -39,6 +39,16 @@ typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
+// Deferred rescale (forward): the running max used for exponentiation is only raised when a
+// row's new max exceeds it by more than 2^kRescaleLog2 -- P stays <= 256, exact in fp32 sums.
+constexpr float kRescaleLog2 = 8.f;
+
+// v_exp_f32 as is: exp2f() adds a denormal range fix-up (cmp + cndmask + ldexp per element) that
+// softmax does not need (arguments are <= 0 up to the deferred-rescale slack; underflow -> 0).
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// A condition the caller knows is wave-uniform, made provably so (scalar branch, no exec masking).
+__device__ __forceinline__ bool uniform(bool c) { return __builtin_amdgcn_readfirstlane((int)c) != 0; }
 
 __device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -199,7 +209,7 @@ __global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams p) 
     }
 
     // ---- masking (only on diagonal / tail tiles)
-    const bool need_mask = (p.causal && kv0 + kFwdBKV - 1 > q0w) || (kv0 + kFwdBKV > p.S);
+    const bool need_mask = uniform((p.causal && kv0 + kFwdBKV - 1 > q0w) || (kv0 + kFwdBKV > p.S));
     if (need_mask) {
 #pragma unroll
       for (int u = 0; u < 2; ++u)
@@ -216,20 +226,24 @@ __global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams p) 
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[u][i]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx * p.scale_log2);
-    const float m_use = m_new == -INFINITY ? 0.f : m_new;
-    const float alpha = exp2f(m_run - m_use);
-    m_run = m_new;
-    l_run *= alpha;
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * p.scale_log2;
+    // raise the reference max only when some row of the wave outgrew it by > 2^kRescaleLog2
+    // (wave-uniform branch: the common case skips the O / l rescale entirely)
+    if (__any(mx > m_run + kRescaleLog2)) {
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = m_new == -INFINITY ? 1.f : fast_exp2(m_run - m_new);
+      m_run = m_new;
+      l_run *= alpha;
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+      for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+    }
+    const float m_use = m_run == -INFINITY ? 0.f : m_run;
     bf16x8 pf[2][2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float e = exp2f(s[u][i] * p.scale_log2 - m_use);
+        const float e = fast_exp2(s[u][i] * p.scale_log2 - m_use);
         s[u][i] = e;
         l_run += e;
       }
@@ -321,8 +335,9 @@ struct BwdParams {
   int64_t dq_ss, dkv_ss;  // token (row) strides of the dq and dk/dv outputs: Hq*D / Hkv*D, or the fused
                           // [T, (Hq + 2 Hkv) D] dQKV row when the caller hands over one buffer
   int B, S, Hq, Hkv;
-  float scale;       // softmax scale
-  float scale_log2;  // scale * log2(e)
+  float scale;          // softmax scale
+  float scale_log2;     // scale * log2(e)
+  float neg_inv_scale;  // -1 / scale (kernel argument: a scalar register, not a VGPR)
   bool causal;
 };
 
@@ -341,14 +356,14 @@ __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" :
 // Stage ROWS x D bf16 rows (row r at base + r*row_stride, r clamped to < nrows_valid) into an
 // LDS image swizzled by SWZ, using LDS-DMA pieces issued by `wave` of `nwaves`. The image is
 // lane-linear per piece; the swizzle is applied to the global SOURCE address (involution).
-template <int D, int ROWS, int SWZ>  // SWZ: 0 = row image, 1 = dual image
+template <int D, int ROWS, int SWZ, int NW = 4>  // SWZ: 0 = row image, 1 = dual image; NW waves share it
 __device__ __forceinline__ void stage_rows(bf16* img, const bf16* base, int64_t row_stride, int row0, int nvalid,
-                                           int wave, int nwaves, int lane) {
+                                           int wave, int lane) {
   constexpr int CH = D / 8;
   constexpr int PR = 64 / CH;               // rows per 1 KiB piece
   constexpr int NP = ROWS / PR;             // pieces
   const int rin = lane / CH, phys = lane % CH;
-  for (int pc = wave; pc < NP; pc += nwaves) {
+  for (int pc = wave; pc < NP; pc += NW) {
     const int row = pc * PR + rin;
     const int logical = SWZ ? swz_dual<D>(row, phys) : swz_row<D>(row, phys);
     int grow = row0 + row;
@@ -399,7 +414,7 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
     const bool ok = key < p.S;
     kf[kk] = ok ? *reinterpret_cast<const bf16x8*>(kb + (int64_t)key * p.k_ss + 16 * kk + 8 * h) : (bf16x8)((bf16)0.f);
   }
-  stage_rows<D, kKvBKV, 0>(vimg, vb, p.v_ss, k0, p.S, w, 4, lane);
+  stage_rows<D, kKvBKV, 0>(vimg, vb, p.v_ss, k0, p.S, w, lane);
   f32x16 dkt[DT], dvt[DT];  // dK^T, dV^T : [d][key]
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) {
@@ -412,8 +427,8 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
   auto stage = [&](int buf, int t) {
     const int q0 = t * kKvBQ;
     bf16* img = smem + buf * 2 * QT;
-    stage_rows<D, kKvBQ, 1>(img, qb, p.q_ss, q0, p.S, w, 4, lane);
-    stage_rows<D, kKvBQ, 1>(img + QT, dob, p.do_ss, q0, p.S, w, 4, lane);
+    stage_rows<D, kKvBQ, 1>(img, qb, p.q_ss, q0, p.S, w, lane);
+    stage_rows<D, kKvBQ, 1>(img + QT, dob, p.do_ss, q0, p.S, w, lane);
     if (w == 0) {
       int q = q0 + (lane & 31);
       q = q < p.S ? q : p.S - 1;
@@ -428,7 +443,7 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
     const int buf = (t - t0) & 1;
     if (t + 1 < nqt) stage(buf ^ 1, t + 1);
     const int q0 = t * kKvBQ;
-    const bool active = !(p.causal && q0 + kKvBQ - 1 < kw0);
+    const bool active = uniform(!(p.causal && q0 + kKvBQ - 1 < kw0));
     if (active) {
       const bf16* qi = smem + buf * 2 * QT;
       const bf16* di = qi + QT;
@@ -436,7 +451,7 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int qr = (i & 3) + 8 * (i >> 2) + 4 * h;
-        sacc[i] = -rc[buf][qr] / p.scale;  // S' = S - lse/scale  ->  p = exp2(S' * scale * log2e)
+        sacc[i] = rc[buf][qr] * p.neg_inv_scale;  // S' = S - lse/scale  ->  p = exp2(S' * scale * log2e)
         dpacc[i] = -rc[buf][32 + qr];
       }
 #pragma unroll
@@ -451,13 +466,17 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
         bf16x8 vv = lds_read_b128(vimg + vrow * D + swz_row<D>(vrow, 2 * kk + h) * 8);
         dpacc = mfma32(a, vv, dpacc);
       }
+      // dS = P (dP - delta); the softmax scale is applied once to dK at the end
+      const bool need_mask = uniform((p.causal && q0 < kw0 + 31) || q0 + kKvBQ > p.S || kw0 + 32 > p.S);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int q = q0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-        float pv = exp2f(sacc[i] * p.scale_log2);
-        if (key >= p.S || q >= p.S || (p.causal && key > q)) pv = 0.f;
+        float pv = fast_exp2(sacc[i] * p.scale_log2);
+        if (need_mask) {
+          const int q = q0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (key >= p.S || q >= p.S || (p.causal && key > q)) pv = 0.f;
+        }
         sacc[i] = pv;
-        dpacc[i] = pv * dpacc[i] * p.scale;
+        dpacc[i] *= pv;
       }
       bf16x8 pfr[2], dsf[2];
 #pragma unroll
@@ -490,6 +509,8 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
     __syncthreads();
   }
   if (key >= p.S) return;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) dkt[dt] *= p.scale;
   if (group == 1) {
     bf16* dkr = p.dk + ((int64_t)b * p.S + key) * p.dkv_ss + hk * D;
     bf16* dvr = p.dv + ((int64_t)b * p.S + key) * p.dkv_ss + hk * D;
@@ -591,8 +612,8 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams p
   const int nt = (kv_end + kDqBKV - 1) / kDqBKV;
   auto stage = [&](int buf, int t) {
     bf16* img = smem + buf * 2 * TILE;
-    stage_rows<D, kDqBKV, 1>(img, kb, p.k_ss, t * kDqBKV, p.S, w, 4, lane);
-    stage_rows<D, kDqBKV, 0>(img + TILE, vb, p.v_ss, t * kDqBKV, p.S, w, 4, lane);
+    stage_rows<D, kDqBKV, 1>(img, kb, p.k_ss, t * kDqBKV, p.S, w, lane);
+    stage_rows<D, kDqBKV, 0>(img + TILE, vb, p.v_ss, t * kDqBKV, p.S, w, lane);
   };
   stage(0, 0);
   vm_drain();
@@ -618,14 +639,17 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams p
         }
       }
       bf16x8 dsf[2][2];
+      const bool need_mask = uniform((p.causal && kv0 + kDqBKV - 1 > q0w) || kv0 + kDqBKV > p.S);
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const int kv = kv0 + 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
-          float pv = exp2f(s[u][i] * p.scale_log2 - lse2);
-          if (kv >= p.S || (p.causal && kv > qcol)) pv = 0.f;
-          s[u][i] = pv * dp[u][i] * p.scale;
+          float pv = fast_exp2(s[u][i] * p.scale_log2 - lse2);
+          if (need_mask) {
+            const int kv = kv0 + 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
+            if (kv >= p.S || (p.causal && kv > qcol)) pv = 0.f;
+          }
+          s[u][i] = pv * dp[u][i];
         }
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2)
@@ -654,6 +678,8 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams p
   }
   if (qcol < p.S) {
     bf16* orow = p.dq + ((int64_t)b * p.S + qcol) * p.dq_ss + hq * D;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) dqt[dt] *= p.scale;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -766,7 +792,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
               group > 1 ? dv_part.data_ptr<float>() : nullptr, reinterpret_cast<bf16*>(dk.data_ptr()),
               reinterpret_cast<bf16*>(dv.data_ptr()), q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1),
               k.stride(2), v.stride(0), v.stride(1), v.stride(2), dout.stride(0), dout.stride(1), dout.stride(2), dq_ss,
-              dkv_ss, B, S, Hq, Hkv, (float)softmax_scale, (float)(softmax_scale * kLog2e), causal};
+              dkv_ss, B, S, Hq, Hkv, (float)softmax_scale, (float)(softmax_scale * kLog2e),
+              (float)(-1.0 / softmax_scale), causal};
   const int64_t kv_blocks = (int64_t)B * Hq * ((S + kKvBKV - 1) / kKvBKV);
   const int64_t dq_blocks = (int64_t)B * Hq * ((S + kDqBQ - 1) / kDqBQ);
   if (D == 128) {
