@@ -3,6 +3,7 @@
 W=2 ranks x GA=1 (each rank a different micro-batch) must produce the same
 parameters as W=1 x GA=2 over the same two micro-batches, for every ZeRO stage.
 """
+import json
 import os
 import socket
 
@@ -170,3 +171,28 @@ def test_mixtral_expert_parallel_world2_matches_single(tmp_path, stage):
     for k, v in ref.items():
         err = float((got["grads"][k] - v).abs().max() / v.abs().max().clamp_min(1e-8))
         assert err < 2e-2, (k, err)
+
+
+def _comm_bench_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location(
+        "comm_bench", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "comm_bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    rows = mod.main(["--min-mb", "0.0625", "--max-mb", "0.125", "--iters", "2", "--warmup", "1", "--dtype", "fp32"])
+    if rank == 0:
+        with open(out_path, "w") as f:
+            json.dump(rows, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_comm_bench_gloo_world2(tmp_path):
+    out = str(tmp_path / "cb.json")
+    mp.spawn(_comm_bench_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    with open(out) as f:
+        rows = json.load(f)
+    assert {r["op"] for r in rows} == {"all_gather", "reduce_scatter", "all_reduce", "all_to_all"}
+    assert all(r["busbw_GBps"] > 0 and r["world"] == 2 for r in rows)
