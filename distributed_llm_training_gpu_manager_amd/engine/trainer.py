@@ -82,7 +82,10 @@ class Trainer:
         self.args = args
         self.env = init_distributed(args.device)
         self.comm = Comm()
-        self.mcfg = get_config(args.model, **({"max_seq_len": max(args.seq_len, 1)} if args.seq_len else {}))
+        over = {"max_seq_len": max(args.seq_len, 1)} if args.seq_len else {}
+        if getattr(args, "n_layers", 0):
+            over["n_layers"] = args.n_layers  # drills on a box: the named architecture, fewer blocks
+        self.mcfg = get_config(args.model, **over)
         if args.deepspeed_config:
             self.ecfg, self.notes = engine_config_from_ds(args.deepspeed_config, args.seq_len, seed=args.seed)
         else:
@@ -224,6 +227,7 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--job-id", default="local")
     ap.add_argument("--log-interval", type=int, default=1)
     ap.add_argument("--log-json", default=None)
+    ap.add_argument("--n-layers", type=int, default=0, help="override the preset's depth (drills only)")
     ap.add_argument("--wall-clock-breakdown", action="store_true", help="per-phase HIP-event timers in the log")
     a, unknown = ap.parse_known_args(argv)
     return a

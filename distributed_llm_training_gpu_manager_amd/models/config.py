@@ -80,6 +80,9 @@ PRESETS: Dict[str, ModelConfig] = {
                               rope_theta=500000.0, norm_eps=1e-5),
     "mixtral-8x7b": ModelConfig("mixtral-8x7b", "mixtral", 32000, 4096, 32, 32, 8, 14336, max_seq_len=32768,
                                 rope_theta=1e6, norm_eps=1e-5, n_experts=8, top_k=2),
+    # Llama-3.2-1B shape (untied head): resilience drills that must fit a single box's scratch disk
+    "llama3-1b": ModelConfig("llama3-1b", "llama", 128256, 2048, 16, 32, 8, 8192, max_seq_len=8192,
+                             rope_theta=500000.0, norm_eps=1e-5),
     # small shapes for tests / smoke runs
     "llama-tiny": ModelConfig("llama-tiny", "llama", 512, 256, 2, 4, 2, 512, max_seq_len=256, rope_theta=10000.0),
     "llama-small": ModelConfig("llama-small", "llama", 32768, 1024, 4, 8, 8, 2816, max_seq_len=2048),

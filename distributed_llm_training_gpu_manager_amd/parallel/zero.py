@@ -80,6 +80,7 @@ class EngineConfig:
     # parameter all-gathers on their own communicator (own RCCL stream), so a prefetch gather of the
     # next block and the reduce-scatter of the previous block's gradients run concurrently on xGMI
     separate_gather_comm: bool = True
+    tuned_gemms: bool = True  # load TunableOp results for this model if present (utils/gemm_tuning.py)
     init_device: str = "auto"  # "cpu" gives bit-identical init on any device (tests); auto: cpu below 1e9 params
     fp16: bool = False  # dynamic loss scaling path (reference fp16 block)
     loss_scale: float = 0.0  # 0 = dynamic
@@ -214,6 +215,10 @@ class ZeroEngine:
         # MI355X compute dtype is bf16 (fp16 requests keep the loss-scaler path but compute in bf16)
         self.dtype = torch.bfloat16
         self.is_cuda = device.type == "cuda"
+        self.tuned_gemm_files: List[str] = []
+        if self.is_cuda and cfg.tuned_gemms:
+            from ..utils.gemm_tuning import enable_tuned_gemms
+            self.tuned_gemm_files = enable_tuned_gemms(model_cfg.name)
         self._alloc()
         self._init_params()
         self.step_count = 0

@@ -28,7 +28,7 @@ from distributed_llm_training_gpu_manager_amd.launcher.supervisor import JobRegi
 def train_argv(a, extra):
     return [sys.executable, "-m", "distributed_llm_training_gpu_manager_amd.train", "--model", a.model,
             "--seq-len", str(a.seq), "--micro-batch", "1", "--grad-accum", str(a.ga), "--zero-stage", "3",
-            "--lr", "3e-5", *extra]
+            "--lr", "3e-5", *(["--n-layers", str(a.n_layers)] if a.n_layers else []), *extra]
 
 
 def run(argv, timeout):
@@ -87,6 +87,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--drills", default="nan,sigkill,spot")
     ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--n-layers", type=int, default=0)
     ap.add_argument("--seq", type=int, default=8192)
     ap.add_argument("--ga", type=int, default=1)
     ap.add_argument("--k", type=int, default=3)
@@ -96,7 +97,8 @@ def main():
     ap.add_argument("--work", default=None)
     a = ap.parse_args()
     work = a.work or tempfile.mkdtemp(prefix="dlgm_drill_")
-    res = {"model": a.model, "seq": a.seq, "ga": a.ga}
+    res = {"model": a.model, "n_layers": a.n_layers or "preset", "seq": a.seq, "ga": a.ga,
+           "data": "synthetic token ids, random-init weights"}
     for d in a.drills.split(","):
         t0 = time.time()
         res[d] = {"nan": drill_nan, "sigkill": drill_sigkill, "spot": drill_spot}[d](a, work)
@@ -105,6 +107,8 @@ def main():
         os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
         with open(a.out, "w") as f:
             json.dump(res, f, indent=1)
+        for sub in ("ck", "ck_spot"):  # the box's scratch disk holds one drill's checkpoints at a time
+            shutil.rmtree(os.path.join(work, sub), ignore_errors=True)
     shutil.rmtree(work, ignore_errors=True)
 
 
