@@ -25,6 +25,17 @@ def shapes(cfg, T):
     return ws
 
 
+def _write(fname: str) -> None:
+    """TunableOp results file: validator lines, then op,params,solution,ms lines."""
+    tun = torch.cuda.tunable
+    lines = [f"Validator,{k},{v}" for k, v in tun.get_validators()]
+    lines += [",".join(str(x) for x in r) for r in tun.get_results()]
+    tmp = fname + ".tmp"
+    with open(tmp, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    os.replace(tmp, fname)
+
+
 def bench(fn, iters=10):
     fn()
     torch.cuda.synchronize()
@@ -76,7 +87,7 @@ def main():
         torch.cuda.synchronize()
         res[n]["tune_s"] = time.perf_counter() - t0
         print(f"tuned {n} in {res[n]['tune_s']:.1f}s", flush=True)
-        tun.write_file()  # keep what is tuned so far
+        _write(fname)  # keep what is tuned so far (TunableOp itself only writes at process exit)
     tun.tuning_enable(False)
     for n, fl, fn in cases:
         res[n]["tuned_ms"] = bench(fn)
