@@ -25,7 +25,7 @@ from typing import Any, Dict, List, Optional, Tuple
 import torch
 
 from ..ckpt.checkpoint import AsyncCheckpointer, export_consolidated
-from ..health.loss_monitor import LossSpikeMonitor, MonitorConfig, TrainingMetrics
+from ..health.loss_monitor import json_safe, LossSpikeMonitor, MonitorConfig, TrainingMetrics
 from ..health.nan_trap import NanTrap
 from ..launcher.supervisor import EXIT_NAN_HALT, EXIT_PREEMPTED, write_status
 from ..models import get_config
@@ -193,8 +193,11 @@ class Trainer:
         self.trap.close()
         if a.log_json and self.env.rank == 0:
             with open(a.log_json, "w") as f:
-                json.dump({"log": self.log, "ckpt": self.ckpt.history if self.ckpt else [],
-                           "trap": self.trap.records}, f)
+                json.dump(json_safe({"log": self.log, "ckpt": self.ckpt.history if self.ckpt else [],
+                                     "trap": self.trap.records, "monitor": self.monitor.get_summary(),
+                                     "engine": {"zero_stage": self.ecfg.zero_stage, "world": self.env.world,
+                                                "backend": self.env.backend, "device": str(self.env.device),
+                                                "notes": self.notes}}), f)
         if torch.distributed.is_initialized():
             torch.distributed.destroy_process_group()
         return rc

@@ -69,7 +69,9 @@ def init_distributed(device_type: str = "auto", timeout_s: int = 1800) -> DistEn
     else:
         device = torch.device("cpu")
     backend = "nccl" if device_type == "cuda" else "gloo"
-    if world > 1 and not dist.is_initialized():
+    # under torchrun a process group is formed even for one rank (gloo on CPU: BASELINE config 1)
+    launched = "TORCHELASTIC_RUN_ID" in os.environ
+    if (world > 1 or launched) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
@@ -79,7 +81,7 @@ def init_distributed(device_type: str = "auto", timeout_s: int = 1800) -> DistEn
     if dist.is_initialized():
         backend = dist.get_backend()
         rank, world = dist.get_rank(), dist.get_world_size()
-    return DistEnv(rank, world, local_rank, backend if world > 1 else "none", device)
+    return DistEnv(rank, world, local_rank, backend if dist.is_initialized() else "none", device)
 
 
 class Comm:
