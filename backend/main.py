@@ -7,13 +7,24 @@ xGMI via amdsmi), responses are JSON-safe for NaN/Inf (A14), and the GPU
 telemetry is served from a background-polled snapshot (A27).
 """
 import os
+from contextlib import asynccontextmanager
 
 from fastapi import FastAPI
 from fastapi.middleware.cors import CORSMiddleware
 
 from backend.routers import gpu, monitoring, topology, training
 
+@asynccontextmanager
+async def _lifespan(_app):
+    # amdsmi telemetry is polled on a background thread; handlers serve the latest snapshot
+    interval = float(os.environ.get("DLGM_TELEMETRY_INTERVAL_S", "5"))
+    if interval > 0:
+        gpu.manager.start_polling(interval)
+    yield
+
+
 app = FastAPI(
+    lifespan=_lifespan,
     title="MLOps Platform API",
     description="GPU fleet management, ZeRO distributed training on AMD Instinct MI355X, and training health monitoring",
     version="1.0.0",
@@ -32,13 +43,6 @@ app.include_router(training.router, prefix="/api/v1/training", tags=["distribute
 app.include_router(monitoring.router, prefix="/api/v1/monitoring", tags=["loss-monitoring"])
 app.include_router(topology.router, prefix="/api/v1", tags=["topology"])
 app.include_router(topology.router, tags=["topology"])  # reference path /topology
-
-
-@app.on_event("startup")
-def _start_telemetry() -> None:
-    interval = float(os.environ.get("DLGM_TELEMETRY_INTERVAL_S", "5"))
-    if interval > 0:
-        gpu.manager.start_polling(interval)
 
 
 @app.get("/")

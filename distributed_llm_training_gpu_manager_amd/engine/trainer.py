@@ -226,8 +226,8 @@ def parse_args(argv=None) -> argparse.Namespace:
                     "(first attempt only)")
     ap.add_argument("--preempt-at-step", type=int, default=-1, help="spot drill: deliver SIGUSR1 after the step")
     ap.add_argument("--halt-on-nan", type=int, default=1)
-    ap.add_argument("--metrics-url", default=None)
-    ap.add_argument("--job-id", default="local")
+    ap.add_argument("--metrics-url", default=os.environ.get("DLGM_METRICS_URL"))
+    ap.add_argument("--job-id", default=os.environ.get("DLGM_JOB_ID", "local"))
     ap.add_argument("--log-interval", type=int, default=1)
     ap.add_argument("--log-json", default=None)
     ap.add_argument("--n-layers", type=int, default=0, help="override the preset's depth (drills only)")
