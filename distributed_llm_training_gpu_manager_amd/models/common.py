@@ -38,6 +38,7 @@ class ParamSpec:
     weight_decay: bool = True
     experts: int = 0  # >0: leading dim indexes experts; each expert is seeded by its GLOBAL index
     expert_offset: int = 0
+    tcache: bool = False  # 2-D weight whose transpose the engine may cache (fast dX GEMM layout)
 
     @property
     def numel(self) -> int:

@@ -29,7 +29,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import ops
-from ..ops.gemm import grad_mm
+from ..ops.gemm import dx_mm, grad_mm
 from .common import ParamSpec, Params, StepContext, Unit
 from .config import ModelConfig
 
@@ -74,11 +74,11 @@ class LlamaBlock(Unit):
         out_std = c.init_std / (2 * c.n_layers) ** 0.5
         return [
             ParamSpec("attn_norm", (c.d_model,), init="ones", weight_decay=False),
-            ParamSpec("wqkv", (c.qkv_dim, c.d_model), std=c.init_std),
-            ParamSpec("wo", (c.d_model, c.n_heads * c.head_dim), std=out_std),
+            ParamSpec("wqkv", (c.qkv_dim, c.d_model), std=c.init_std, tcache=True),
+            ParamSpec("wo", (c.d_model, c.n_heads * c.head_dim), std=out_std, tcache=True),
             ParamSpec("mlp_norm", (c.d_model,), init="ones", weight_decay=False),
-            ParamSpec("w_gate_up", (2 * c.ffn_dim, c.d_model), std=c.init_std),
-            ParamSpec("w_down", (c.d_model, c.ffn_dim), std=out_std),
+            ParamSpec("w_gate_up", (2 * c.ffn_dim, c.d_model), std=c.init_std, tcache=True),
+            ParamSpec("w_down", (c.d_model, c.ffn_dim), std=out_std, tcache=True),
         ]
 
     # -- attention sub-block helpers (shared with Mixtral) --------------------------
@@ -116,14 +116,14 @@ class LlamaBlock(Unit):
         attn2d = attn.view(T, c.n_heads * c.head_dim)
         acc = ctx.grad_acc
         grad_mm(g["wo"], dh.t(), attn2d, acc)
-        dattn = torch.mm(dh, p["wo"]).view_as(attn)
+        dattn = dx_mm(dh, p, "wo").view_as(attn)
         q, k, v = self._split(qkv, B, S)
         dqkv = torch.empty_like(qkv).view(T, -1)
         ops.flash_attn_bwd(dattn, q, k, v, attn, lse, causal=True, dqkv=dqkv)
         cos, sin = ctx.rope
         ops.rope_(dqkv, cos, sin, c.n_heads + c.n_kv_heads, c.head_dim, S, inverse=True)
         grad_mm(g["wqkv"], dqkv.t(), hn1, acc)
-        dhn1 = torch.mm(dqkv, p["wqkv"])
+        dhn1 = dx_mm(dqkv, p, "wqkv")
         return ops.rmsnorm_bwd(dhn1, x, p["attn_norm"], rstd1, g["attn_norm"], dres=dh, accumulate_dw=acc)
 
     # -- unit API --------------------------------------------------------------------
@@ -142,11 +142,11 @@ class LlamaBlock(Unit):
         saved_attn, h, rstd2, hn2, gu, a = saved
         acc = ctx.grad_acc
         grad_mm(g["w_down"], dy.t(), a, acc)
-        da = torch.mm(dy, p["w_down"])
+        da = dx_mm(dy, p, "w_down")
         dgu = ops.swiglu_bwd(da, gu)
         del da
         grad_mm(g["w_gate_up"], dgu.t(), hn2, acc)
-        dhn2 = torch.mm(dgu, p["w_gate_up"])
+        dhn2 = dx_mm(dgu, p, "w_gate_up")
         del dgu
         dh = ops.rmsnorm_bwd(dhn2, h, p["mlp_norm"], rstd2, g["mlp_norm"], dres=dy, accumulate_dw=acc)
         return self.attn_backward(p, g, saved_attn, dh, ctx)
@@ -170,7 +170,7 @@ class LlamaHead(Unit):
     def param_specs(self) -> List[ParamSpec]:
         c = self.cfg
         return [ParamSpec("norm", (c.d_model,), init="ones", weight_decay=False),
-                ParamSpec("lm_head", (c.vocab_size, c.d_model), std=c.init_std)]
+                ParamSpec("lm_head", (c.vocab_size, c.d_model), std=c.init_std, tcache=True)]
 
     def forward(self, p: Params, x_pair, ctx: StepContext):
         c = self.cfg
@@ -185,7 +185,7 @@ class LlamaHead(Unit):
     def backward(self, p: Params, g: Params, saved, dy, ctx: StepContext):
         x, rstd, hn, dlogits = saved
         grad_mm(g["lm_head"], dlogits.t(), hn, ctx.grad_acc)
-        dhn = torch.mm(dlogits, p["lm_head"])
+        dhn = dx_mm(dlogits, p, "lm_head")
         return ops.rmsnorm_bwd(dhn, x, p["norm"], rstd, g["norm"], accumulate_dw=ctx.grad_acc)
 
     def flops(self, ctx: StepContext) -> float:

@@ -71,10 +71,21 @@ def grad_copy(out: torch.Tensor, src: torch.Tensor, acc: bool) -> None:
 
 def transpose(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Contiguous x^T for a 2-D bf16 tensor (register-blocked HIP kernel on the GPU)."""
-    if use_native(x):
+    if use_native(x) and x.dtype == torch.bfloat16 and x.shape[0] % 8 == 0 and x.shape[1] % 8 == 0 \
+            and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0:
         return hip_ops().transpose(x, out)
     y = x.t().contiguous()
     if out is not None:
         out.copy_(y)
         return out
     return y
+
+
+def dx_mm(dy: torch.Tensor, p: dict, name: str) -> torch.Tensor:
+    """Input gradient dy @ W for a weight stored [out, in]. When the engine supplies the cached
+    transpose ``p[name + ".T"]`` ([in, out], refreshed once per optimizer step) the GEMM runs as
+    dy @ (W^T)^T -- both operands K-contiguous, hipBLASLt's fastest layout on gfx950."""
+    wt = p.get(name + ".T")
+    if wt is not None:
+        return torch.mm(dy, wt.t())
+    return torch.mm(dy, p[name])

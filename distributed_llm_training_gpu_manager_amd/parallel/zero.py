@@ -81,6 +81,9 @@ class EngineConfig:
     # next block and the reduce-scatter of the previous block's gradients run concurrently on xGMI
     separate_gather_comm: bool = True
     tuned_gemms: bool = True  # load TunableOp results for this model if present (utils/gemm_tuning.py)
+    # keep W^T of the big 2-D weights while the compute copy is stationary (P == 1, ZeRO-0/1/2): the
+    # input-gradient GEMMs then run with both operands K-contiguous (refreshed once per optimizer step)
+    transposed_weight_cache: bool = True
     init_device: str = "auto"  # "cpu" gives bit-identical init on any device (tests); auto: cpu below 1e9 params
     fp16: bool = False  # dynamic loss scaling path (reference fp16 block)
     loss_scale: float = 0.0  # 0 = dynamic
@@ -221,6 +224,15 @@ class ZeroEngine:
             self.tuned_gemm_files = enable_tuned_gemms(model_cfg.name)
         self._alloc()
         self._init_params()
+        self._pver = 0  # bumped whenever the bf16 compute copy changes
+        self._tcache: Dict[int, Tuple[int, Dict[str, torch.Tensor]]] = {}
+        self._tnames: Dict[int, List[Tuple[str, Tuple[int, ...]]]] = {}
+        if cfg.transposed_weight_cache:
+            for g in self.groups:
+                if self.stage < 3 or g.P == 1:
+                    names = [(sp.name, tuple(sp.shape)) for sp in g.specs if sp.tcache and len(sp.shape) == 2]
+                    if names:
+                        self._tnames[g.idx] = names
         self.step_count = 0
         self.scaler = LossScaler(cfg, device) if cfg.fp16 else None
         self.stats = torch.zeros(2, dtype=torch.float32, device=device)
@@ -291,6 +303,7 @@ class ZeroEngine:
         self._p16_from_master()
 
     def _p16_from_master(self) -> None:
+        self._pver = getattr(self, "_pver", 0) + 1
         if self.offload is not None:
             self.offload.push_params(self.p16_shard)
         elif self.dtype == torch.bfloat16:
@@ -325,8 +338,24 @@ class ZeroEngine:
             self._issue_gather(gi)
             flat, h = self._live[gi]
             h.wait()
-            out.update(self.groups[gi].views(flat))
+            views = self.groups[gi].views(flat)
+            out.update(views)
+            if gi in self._tnames:
+                out.update(self._transposed(gi, views))
         return out
+
+    def _transposed(self, gi: int, views: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        """name + ".T" -> cached [in, out] copy of the stationary compute weight (rebuilt per step)."""
+        ver, cache = self._tcache.get(gi, (-1, None))
+        if cache is None:
+            cache = {n: torch.empty((shp[1], shp[0]), dtype=self.dtype, device=self.device)
+                     for n, shp in self._tnames[gi]}
+        if ver != self._pver:
+            from ..ops.gemm import transpose
+            for n, _ in self._tnames[gi]:
+                transpose(views[n], out=cache[n])
+            self._tcache[gi] = (self._pver, cache)
+        return {n + ".T": t for n, t in cache.items()}
 
     def release(self, gis) -> None:
         if self.stage == 3:
@@ -554,6 +583,7 @@ class ZeroEngine:
                             step=self.step_count, grad_scale=inv_scale, max_norm=cfg.grad_clip)
             if self.dtype != torch.bfloat16:
                 self.p16_shard.copy_(self.master)
+        self._pver += 1  # the compute copy changes below: transposed caches are stale
         if self.stage in (1, 2):
             hs = []
             for g in self.groups:
@@ -640,6 +670,8 @@ class ZeroEngine:
             "param_shard_GiB": self.shard_total * 2 / gb,
             "param_full_GiB": (self.full_total * 2 / gb) if self.p16_full is not None else 0.0,
             "grad_full_GiB": (self.full_total * 4 / gb) if self.grad_full is not None else 0.0,
+            "weight_T_cache_GiB": sum(t.numel() * t.element_size() for _, c in self._tcache.values()
+                                      for t in c.values()) / gb,
         }
         if self.is_cuda:
             rep["allocated_GiB"] = torch.cuda.memory_allocated(self.device) / gb

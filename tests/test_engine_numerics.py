@@ -120,3 +120,34 @@ def test_engine_gpu_matches_cpu_training():
         losses[dev] = [float(eng.train_step(mb)["loss"]) for _ in range(4)]
     for a, b in zip(losses["cpu"], losses["cuda"]):
         assert abs(a - b) < 3e-2 * max(1.0, abs(a)), losses
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("stage", [1, 3])
+def test_transposed_weight_cache_is_transparent(device, stage):
+    """dX through the cached W^T (refreshed after every optimizer step) == dX through W."""
+    mc = get_config("llama-tiny")
+    res = {}
+    for on in (False, True):
+        ec = EngineConfig(zero_stage=stage, micro_batch_size=2, seq_len=32, grad_accum=2, lr=1e-2,
+                          scheduler="constant", init_device="cpu", transposed_weight_cache=on)
+        eng = ZeroEngine(mc, ec, torch.device(device))
+        assert bool(eng._tnames) == on
+        g = torch.Generator().manual_seed(9)
+        losses = []
+        for _ in range(3):
+            mbs = []
+            for _ in range(2):
+                t = torch.randint(0, mc.vocab_size, (2, 33), generator=g).to(device)
+                mbs.append((t[:, :-1], t[:, 1:]))
+            losses.append(float(eng.train_step(mbs)["loss"]))
+        if on:
+            assert eng.memory_report()["weight_T_cache_GiB"] > 0
+        res[on] = (losses, {k: v.float().cpu() for k, v in eng.full_params().items()})
+    assert res[False][0][0] == res[True][0][0]
+    for a, b in zip(res[False][0], res[True][0]):
+        assert abs(a - b) < 1e-3 * max(1.0, abs(a))
+    for k, v in res[False][1].items():
+        d = (res[True][1][k] - v).abs()
+        assert float(d.max()) <= 2 * 1e-2 * 3 + 1e-3, k
+        assert float((d > 1e-3).float().mean()) < 0.02, k

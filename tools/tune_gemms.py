@@ -1,5 +1,10 @@
 """Tune the Llama-3 GEMM shapes with PyTorch TunableOp (hipBLASLt + rocBLAS solution search).
 
+WARNING: the exhaustive search launches every candidate solution; on ROCm 7.0 / gfx950 one
+candidate for the [8192 x 28672] x [28672 x 4096] input-gradient GEMM faulted the GPU
+("unspecified launch failure"). Do not run this on shared machines; the framework does not
+depend on tuned files (utils/gemm_tuning.py loads them only if present).
+
 Writes the winning solutions to ``distributed_llm_training_gpu_manager_amd/tuned/`` (loaded by
 ``utils.gemm_tuning.enable_tuned_gemms``) and prints default-vs-tuned times per shape.
 
