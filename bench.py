@@ -27,6 +27,11 @@ if ROOT not in sys.path:
 METRIC = "tokens/sec (node) Llama-3-8B ZeRO-3"
 
 
+def _knob(v: str):
+    """A ZeRO-3 residency knob from the command line: 'hbm' or a number."""
+    return v if v in ("hbm", "auto") else float(v)
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -38,6 +43,9 @@ def main() -> int:
     ap.add_argument("--ga", type=int, default=8, help="gradient accumulation steps (reference default 8)")
     ap.add_argument("--zero", type=int, default=3)
     ap.add_argument("--ckpt", action="store_true", help="activation checkpointing (recompute)")
+    ap.add_argument("--live-params", default="hbm",
+                    help="ZeRO-3 stage3_max_live_parameters: a number, or 'hbm' = sized to the GPU's memory")
+    ap.add_argument("--reuse-distance", default="hbm", help="ZeRO-3 stage3_max_reuse_distance (number or 'hbm')")
     ap.add_argument("--profile-steps", type=int, default=0)
     args = ap.parse_args()
 
@@ -55,7 +63,8 @@ def main() -> int:
     mcfg = get_config(args.model)
     ecfg = EngineConfig(zero_stage=args.zero, micro_batch_size=args.mbs, seq_len=args.seq, grad_accum=args.ga,
                         lr=3e-5, warmup_steps=100, total_steps=10000, grad_clip=1.0,
-                        activation_checkpointing=args.ckpt)
+                        activation_checkpointing=args.ckpt, max_live_parameters=_knob(args.live_params),
+                        max_reuse_distance=_knob(args.reuse_distance))
     t0 = time.time()
     eng = ZeroEngine(mcfg, ecfg, env.device, comm)
     if env.device.type == "cuda":
@@ -114,6 +123,8 @@ def main() -> int:
                 "seq_len": args.seq,
                 "parallelism": f"zero{args.zero}-dp{env.world}",
                 "activation_checkpointing": args.ckpt,
+                "stage3_max_live_parameters": args.live_params,
+                "stage3_max_reuse_distance": args.reuse_distance,
             },
             "extra": {
                 "tokens_per_sec_per_gpu": round(tps / env.world, 2),
@@ -122,6 +133,8 @@ def main() -> int:
                 "final_loss": round(loss, 4),
                 "init_s": round(init_s, 1),
                 "params": eng.num_params(),
+                "zero3_allgathers_per_step": eng.live_plan.gathers_per_step(args.ga),
+                "zero3_resident_gathered_params": eng.live_plan.resident_params,
                 "mem": {k: round(v, 1) for k, v in eng.memory_report().items()},
             },
         }

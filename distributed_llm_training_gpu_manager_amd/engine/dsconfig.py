@@ -62,6 +62,10 @@ def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, **overri
         offload_optimizer=off_o,
         nvme_path=zo.get("offload_optimizer", {}).get("nvme_path"),
         wall_clock_breakdown=bool(ds.get("wall_clock_breakdown", False)),
+        # ZeRO-3 residency (parallel/residency.py); a number, or "hbm" to size the budget to the GPU
+        max_live_parameters=zo.get("stage3_max_live_parameters", 1e9),
+        max_reuse_distance=zo.get("stage3_max_reuse_distance", 1e9),
+        prefetch_bucket_size=float(zo.get("stage3_prefetch_bucket_size", 5e8)),
     )
     for k, v in overrides.items():
         setattr(cfg, k, v)

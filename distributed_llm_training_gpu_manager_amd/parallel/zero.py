@@ -44,6 +44,7 @@ from .. import ops
 from ..models import ModelConfig, StepContext, build_model
 from ..models.common import ParamSpec, init_param
 from .comm import Comm, DONE, Handle
+from .residency import ResidencyPlan, resolve_limit
 
 ALIGN = 64  # elements; keeps every param / shard view 128-byte aligned (bf16) for the HIP kernels
 
@@ -72,6 +73,18 @@ class EngineConfig:
     activation_checkpointing: bool = False
     cpu_checkpointing: bool = False
     prefetch: bool = True
+    # ZeRO-3 gathered-parameter residency, DeepSpeed semantics (reference config keys
+    # stage3_max_live_parameters / stage3_max_reuse_distance / stage3_prefetch_bucket_size,
+    # ai_engine/deepspeed_launcher.py:188-190): a gathered unit stays resident after a visit when the
+    # parameters fetched before its next visit are <= max_reuse_distance and the resident set stays
+    # <= max_live_parameters. "hbm" sizes both to this GPU (live_hbm_fraction of its HBM), so on a
+    # 288 GB MI355X a whole Llama-3-8B stays gathered across the micro-batches of a step: one
+    # all-gather per unit per optimizer step instead of two per micro-batch. Persistent state
+    # (bf16 params, fp32 master/m/v, fp32 grads) stays partitioned 1/W either way.
+    max_live_parameters: Any = 1e9
+    max_reuse_distance: Any = 1e9
+    prefetch_bucket_size: float = 5e8
+    live_hbm_fraction: float = 0.12
     seed: int = 1234
     expert_parallel_size: int = 1
     offload_optimizer: str = "none"  # none | cpu | nvme (ZeRO-Offload parity path: parallel/offload.py)
@@ -249,6 +262,7 @@ class ZeroEngine:
             for gi in gis:
                 self._bwd_last_visit[gi] = min(si, self._bwd_last_visit.get(gi, si))
         self._live: Dict[int, Tuple[torch.Tensor, Handle]] = {}
+        self._build_live_plan()
         self._gbuf_pool: Dict[int, List[torch.Tensor]] = {}
         self._act_offload = None
         self.fault_inject_nan = False  # fault injection: poison one gradient element on the next micro-step
@@ -362,6 +376,41 @@ class ZeroEngine:
             for gi in (gis if isinstance(gis, tuple) else (gis,)):
                 self._live.pop(gi, None)
 
+    # ------------------------------------------------------------------ ZeRO-3 residency
+    def _build_live_plan(self) -> None:
+        """Visits of one micro-step (forward stages, then backward stages reversed) and the plan of
+        which gathered groups stay resident between them (parallel/residency.py)."""
+        n = len(self.stages)
+        visits = [self.stages[si][1] for si in range(n)] + [self.stages[si][1] for si in range(n - 1, -1, -1)]
+        hbm = lambda: (self.cfg.live_hbm_fraction * torch.cuda.get_device_properties(self.device).total_memory  # noqa: E731
+                       / self.p16_shard.element_size()) if self.is_cuda else math.inf
+        max_live = resolve_limit(self.cfg.max_live_parameters, hbm)
+        max_reuse = resolve_limit(self.cfg.max_reuse_distance, hbm, unbounded_for_hbm=True)
+        gathered = [self.stage == 3 and g.P > 1 for g in self.groups]
+        self.live_plan = ResidencyPlan(visits, [g.numel for g in self.groups], gathered, max_live, max_reuse)
+
+    def _after_visit(self, v: int, gis, last_micro: bool) -> None:
+        """Drop the gathered copies the residency plan does not keep past visit v (ZeRO-3)."""
+        if self.stage == 3:
+            for gi in gis:
+                if not self.live_plan.keep(v, gi, last_micro):
+                    self._live.pop(gi, None)
+
+    def _prefetch(self, si: int, step: int) -> None:
+        """Issue the all-gathers of the stages after `si` (direction `step`): at least one stage, then
+        more while the parameters in flight stay within prefetch_bucket_size (stage3_prefetch_bucket_size)."""
+        if self.stage != 3 or not self.cfg.prefetch:
+            return
+        acc, j = 0, si + step
+        while 0 <= j < len(self.stages):
+            gis = self.stages[j][1]
+            size = sum(self.groups[gi].numel for gi in gis if gi not in self._live and self.groups[gi].P > 1)
+            if j != si + step and acc + size > self.cfg.prefetch_bucket_size:
+                break
+            self._issue_gathers(gis)
+            acc += size
+            j += step
+
     # ------------------------------------------------------------------ grads
     def _direct_target(self, g: FlatGroup) -> Optional[torch.Tensor]:
         """fp32 storage the unit backward writes / accumulates into directly, or None (bf16 scratch path).
@@ -450,11 +499,9 @@ class ZeroEngine:
             act = self._act_offload
         # ---- forward
         t_fwd = self.timers.mark()
-        last_gis = self.stages[-1][1]
         for si, (unit, gis) in enumerate(self.stages):
             p = self.fetch(gis)
-            if self.cfg.prefetch and si + 1 < n:
-                self._issue_gathers(self.stages[si + 1][1])
+            self._prefetch(si, +1)
             if ckpt and si < n - 1:
                 y, _ = unit.forward(p, x, ctx)
                 saved[si] = ("ckpt", act.push(x) if act is not None else x)
@@ -462,7 +509,7 @@ class ZeroEngine:
                     saved[si - 1] = ("ckpt", act.release_device(saved[si - 1][1]))
             else:
                 y, saved[si] = unit.forward(p, x, ctx)
-            self.release(tuple(gi for gi in gis if gi not in last_gis))  # the head stays gathered for backward
+            self._after_visit(si, gis, last)  # e.g. the head stays gathered for its backward right after
             x = y
         loss = x
         # ---- backward
@@ -474,8 +521,7 @@ class ZeroEngine:
         for si in range(n - 1, -1, -1):
             unit, gis = self.stages[si]
             p = self.fetch(gis)
-            if self.cfg.prefetch and si > 0:
-                self._issue_gathers(self.stages[si - 1][1])
+            self._prefetch(si, -1)
             # per group: direct fp32 target or bf16 scratch, and whether this visit adds to what is there
             # (direct: any micro-batch after the first; both: the second visit of a tied group)
             gv: Dict[str, torch.Tensor] = {}
@@ -518,14 +564,14 @@ class ZeroEngine:
                         self._reduce_group_grad(gi, gbufs.pop(gi), first, pending)
                     elif last:
                         self._finish_direct(self.groups[gi], self._direct_target(self.groups[gi]), pending)
-                    self.release((gi,))
+            self._after_visit(2 * n - 1 - si, gis, last)
             self._drain(pending, keep=1)
         self._drain(pending, keep=0)
         t_end = self.timers.mark()
         self.timers.span("forward", t_fwd, t_bwd)
         self.timers.span("backward+reduce", t_bwd, t_end)
-        if self.stage == 3:
-            self._live.clear()
+        if self.stage == 3 and last:
+            self._live.clear()  # nothing outlives the step: the optimizer changes the parameters
         self.last_aux = ctx.aux
         return loss
 
@@ -584,6 +630,8 @@ class ZeroEngine:
             if self.dtype != torch.bfloat16:
                 self.p16_shard.copy_(self.master)
         self._pver += 1  # the compute copy changes below: transposed caches are stale
+        if self.stage == 3:
+            self._live.clear()  # (micro_step(last=True) already dropped them; direct callers may not have)
         if self.stage in (1, 2):
             hs = []
             for g in self.groups:
@@ -672,6 +720,7 @@ class ZeroEngine:
             "grad_full_GiB": (self.full_total * 4 / gb) if self.grad_full is not None else 0.0,
             "weight_T_cache_GiB": sum(t.numel() * t.element_size() for _, c in self._tcache.values()
                                       for t in c.values()) / gb,
+            "zero3_resident_gathered_GiB": self.live_plan.resident_params * self.p16_shard.element_size() / gb,
         }
         if self.is_cuda:
             rep["allocated_GiB"] = torch.cuda.memory_allocated(self.device) / gb
