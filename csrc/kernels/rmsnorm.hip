@@ -65,6 +65,10 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_fwd_kernel(
 
 // Backward. Grid-strided over rows: wave `gw` handles rows gw, gw+NW, ...
 // dx = rstd * (dy*w - xhat * mean(dy*w*xhat)) (+ dres);   dw_partial[block] = sum dy*xhat
+// Register budget is what sets this kernel's speed (HBM-bound, one memory round trip per row):
+// the row is held as raw bf16 (4 VGPRs per 8 elements, widened on use), w is re-read from L1
+// instead of pinned in 64 VGPRs, and the residual-gradient row is loaded together with dy and h,
+// so a row costs ONE dependent HBM latency and 3 waves fit per SIMD (was 1-2, ~2.2 TB/s).
 template <int MAXC, bool DRES>
 __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(
     const bf16* __restrict__ dy, const bf16* __restrict__ hin, const bf16* __restrict__ w,
@@ -75,28 +79,32 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(
   const int nch = D >> 3;
   const int nw = gridDim.x * kWaves;
   f32x8 acc[MAXC];
-  f32x8 wv[MAXC];
 #pragma unroll
-  for (int c = 0; c < MAXC; ++c) {
-    acc[c] = (f32x8)(0.f);
-    const int ch = lane + c * 64;
-    wv[c] = ch < nch ? load8f(w + ch * 8) : (f32x8)(0.f);
-  }
+  for (int c = 0; c < MAXC; ++c) acc[c] = (f32x8)(0.f);
   for (int row = blockIdx.x * kWaves + wid; row < T; row += nw) {
     const size_t base = (size_t)row * D;
     const float rs = rstd[row];
-    f32x8 g[MAXC], xh[MAXC];
+    bf16x8 gr[MAXC], hr[MAXC], rr[DRES ? MAXC : 1];
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int ch = lane + c * 64;
+      if (ch < nch) {
+        gr[c] = *reinterpret_cast<const bf16x8*>(dy + base + ch * 8);
+        hr[c] = *reinterpret_cast<const bf16x8*>(hin + base + ch * 8);
+        if constexpr (DRES) rr[c] = *reinterpret_cast<const bf16x8*>(dres + base + ch * 8);
+      }
+    }
     float dot = 0.f;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
       const int ch = lane + c * 64;
       if (ch < nch) {
-        g[c] = load8f(dy + base + ch * 8);
-        xh[c] = load8f(hin + base + ch * 8) * rs;
-        acc[c] += g[c] * xh[c];
-        g[c] *= wv[c];
+        const f32x8 g = __builtin_convertvector(gr[c], f32x8);
+        const f32x8 xh = __builtin_convertvector(hr[c], f32x8) * rs;
+        acc[c] += g * xh;
+        const f32x8 gw = g * load8f(w + ch * 8);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) dot += g[c][j] * xh[c][j];
+        for (int j = 0; j < 8; ++j) dot += gw[j] * xh[j];
       }
     }
     dot = wave_sum(dot) / (float)D;
@@ -104,8 +112,10 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(
     for (int c = 0; c < MAXC; ++c) {
       const int ch = lane + c * 64;
       if (ch < nch) {
-        f32x8 o = (g[c] - xh[c] * dot) * rs;
-        if constexpr (DRES) o += load8f(dres + base + ch * 8);
+        const f32x8 gw = __builtin_convertvector(gr[c], f32x8) * load8f(w + ch * 8);
+        const f32x8 xh = __builtin_convertvector(hr[c], f32x8) * rs;
+        f32x8 o = (gw - xh * dot) * rs;
+        if constexpr (DRES) o += __builtin_convertvector(rr[c], f32x8);
         store8f(dx + base + ch * 8, o);
       }
     }
@@ -131,6 +141,69 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(
   }
 }
 
+// Backward for wide rows (D a multiple of 2048: Llama-3 8B/70B, Mixtral): one ROW per block
+// iteration, thread t of the 256 owns the 8-element chunks t, t+256, ... (CPL of them). Each
+// thread keeps its own dw columns for every row the block visits, so the block's dw partial needs
+// no LDS reduction, and the per-thread state is tiny (~80 VGPRs -> 5-6 waves per SIMD): the row is
+// loaded once (dy, h, dres together), reduced across the block through a 2-slot LDS array (one
+// barrier per row; slot parity keeps a fast wave from overwriting a value a slow wave still reads).
+template <int CPL, bool DRES>
+__global__ __launch_bounds__(kThreads) void rmsnorm_bwd_rowblock_kernel(
+    const bf16* __restrict__ dy, const bf16* __restrict__ hin, const bf16* __restrict__ w,
+    const float* __restrict__ rstd, const bf16* __restrict__ dres, bf16* __restrict__ dx,
+    float* __restrict__ dw_part, int T, int D) {
+  __shared__ float red[2][kWaves];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  f32x8 acc[CPL], wv[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    acc[c] = (f32x8)(0.f);
+    wv[c] = load8f(w + (tid + c * kThreads) * 8);
+  }
+  const float inv_d = 1.f / (float)D;
+  int it = 0;
+  for (int row = blockIdx.x; row < T; row += gridDim.x, ++it) {
+    const size_t base = (size_t)row * D;
+    const float rs = rstd[row];
+    bf16x8 gr[CPL], hr[CPL], rr[DRES ? CPL : 1];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const size_t off = base + (size_t)(tid + c * kThreads) * 8;
+      gr[c] = *reinterpret_cast<const bf16x8*>(dy + off);
+      hr[c] = *reinterpret_cast<const bf16x8*>(hin + off);
+      if constexpr (DRES) rr[c] = *reinterpret_cast<const bf16x8*>(dres + off);
+    }
+    float dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const f32x8 g = __builtin_convertvector(gr[c], f32x8);
+      const f32x8 xh = __builtin_convertvector(hr[c], f32x8) * rs;
+      acc[c] += g * xh;
+      const f32x8 gw = g * wv[c];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dot += gw[j] * xh[j];
+    }
+    dot = wave_sum(dot);
+    if (lane == 0) red[it & 1][wid] = dot;
+    __syncthreads();
+    dot = (red[it & 1][0] + red[it & 1][1] + red[it & 1][2] + red[it & 1][3]) * inv_d;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const f32x8 gw = __builtin_convertvector(gr[c], f32x8) * wv[c];
+      const f32x8 xh = __builtin_convertvector(hr[c], f32x8) * rs;
+      f32x8 o = (gw - xh * dot) * rs;
+      if constexpr (DRES) o += __builtin_convertvector(rr[c], f32x8);
+      store8f(dx + base + (size_t)(tid + c * kThreads) * 8, o);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    float* dst = dw_part + (size_t)blockIdx.x * D + (size_t)(tid + c * kThreads) * 8;
+    *reinterpret_cast<f32x4*>(dst) = (f32x4){acc[c][0], acc[c][1], acc[c][2], acc[c][3]};
+    *reinterpret_cast<f32x4*>(dst + 4) = (f32x4){acc[c][4], acc[c][5], acc[c][6], acc[c][7]};
+  }
+}
+
 // dw[d] = (accumulate ? dw[d] : 0) + sum_b part[b][d]; each block owns 64 columns,
 // its 4 waves split the partial rows, LDS combines them.
 template <typename OutT>
@@ -141,8 +214,10 @@ __global__ __launch_bounds__(kThreads) void column_reduce_kernel(const float* __
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + lane;
   float s = 0.f;
-  if (col < D)
+  if (col < D) {
+#pragma unroll 8
     for (int r = wid; r < R; r += kWaves) s += part[(size_t)r * D + col];
+  }
   red[wid][lane] = s;
   __syncthreads();
   if (wid == 0 && col < D) {
@@ -150,6 +225,23 @@ __global__ __launch_bounds__(kThreads) void column_reduce_kernel(const float* __
     if (accumulate) t += (float)out[col];
     out[col] = (OutT)t;
   }
+}
+
+// First pass of the dw reduction when the partial has many rows: part [R, D] -> part2 [gridDim.y, D].
+// 256 consecutive columns per block (1 KiB per row read), blockIdx.y selects a slice of rows, so a
+// [1024 x 4096] partial is read by 1024 blocks with 8 loads in flight per thread instead of 64
+// blocks walking 1024 rows each.
+__global__ __launch_bounds__(kThreads) void column_partial_kernel(const float* __restrict__ part,
+                                                                  float* __restrict__ part2, int R, int D,
+                                                                  int rows_per_slice) {
+  const int col = blockIdx.x * kThreads + threadIdx.x;
+  if (col >= D) return;
+  const int r0 = blockIdx.y * rows_per_slice;
+  const int r1 = min(R, r0 + rows_per_slice);
+  float s = 0.f;
+#pragma unroll 8
+  for (int r = r0; r < r1; ++r) s += part[(size_t)r * D + col];
+  part2[(size_t)blockIdx.y * D + col] = s;
 }
 
 int max_chunks_for(int64_t D) {
@@ -236,39 +328,77 @@ at::Tensor dlgm_rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at:
   if (has_dres) check_rows(*dres, "dres");
   auto dx = at::empty_like(dy);
   auto stream = c10::hip::getCurrentHIPStream();
-  // ~4 rows per wave at T=8192 keeps the partial buffer at 512 x D fp32
-  int64_t nblk = std::min<int64_t>((T + kWaves - 1) / kWaves, 512);
-  if (nblk < 1) nblk = 1;
-  auto part = at::empty({nblk, D}, dy.options().dtype(at::kFloat));
   auto dyp = reinterpret_cast<const bf16*>(dy.data_ptr());
   auto hp = reinterpret_cast<const bf16*>(h.data_ptr());
   auto wp = reinterpret_cast<const bf16*>(w.data_ptr());
   auto drp = has_dres ? reinterpret_cast<const bf16*>(dres->data_ptr()) : nullptr;
   auto dxp = reinterpret_cast<bf16*>(dx.data_ptr());
-#define LAUNCH_BWD(C)                                                                          \
-  if (has_dres)                                                                                \
-    rmsnorm_bwd_kernel<C, true><<<nblk, kThreads, 0, stream>>>(dyp, hp, wp, rstd.data_ptr<float>(), \
-                                                               drp, dxp, part.data_ptr<float>(), T, D); \
-  else                                                                                         \
-    rmsnorm_bwd_kernel<C, false><<<nblk, kThreads, 0, stream>>>(dyp, hp, wp, rstd.data_ptr<float>(), \
-                                                                drp, dxp, part.data_ptr<float>(), T, D);
-  switch (MAXC) {
-    case 2: LAUNCH_BWD(2); break;
-    case 4: LAUNCH_BWD(4); break;
-    case 8: LAUNCH_BWD(8); break;
-    default: LAUNCH_BWD(16); break;
-  }
+  const int cpl = (D % (8 * kThreads) == 0) ? (int)(D / (8 * kThreads)) : 0;
+  int64_t nblk;
+  at::Tensor part;
+  if (cpl == 1 || cpl == 2 || cpl == 4) {
+    // block-per-row kernel: 1024 blocks (~5 resident per CU), 8 rows each at T = 8192
+    nblk = std::max<int64_t>(1, std::min<int64_t>(T, 1024));
+    part = at::empty({nblk, D}, dy.options().dtype(at::kFloat));
+#define LAUNCH_ROWBLOCK(C)                                                                                  \
+    if (has_dres)                                                                                           \
+      rmsnorm_bwd_rowblock_kernel<C, true><<<nblk, kThreads, 0, stream>>>(dyp, hp, wp, rstd.data_ptr<float>(), \
+                                                                        drp, dxp, part.data_ptr<float>(), T, D); \
+    else                                                                                                    \
+      rmsnorm_bwd_rowblock_kernel<C, false><<<nblk, kThreads, 0, stream>>>(dyp, hp, wp, rstd.data_ptr<float>(), \
+                                                                         drp, dxp, part.data_ptr<float>(), T, D);
+    if (T > 0) {
+      switch (cpl) {
+        case 1: LAUNCH_ROWBLOCK(1); break;
+        case 2: LAUNCH_ROWBLOCK(2); break;
+        default: LAUNCH_ROWBLOCK(4); break;
+      }
+    } else {
+      part.zero_();
+    }
+#undef LAUNCH_ROWBLOCK
+  } else {
+    // wave-per-row kernel for narrow rows: 3 waves / SIMD over 256 CUs = 768 blocks of 4 waves
+    nblk = std::max<int64_t>(1, std::min<int64_t>((T + kWaves - 1) / kWaves, 768));
+    part = at::empty({nblk, D}, dy.options().dtype(at::kFloat));
+#define LAUNCH_BWD(C)                                                                                \
+    if (has_dres)                                                                                    \
+      rmsnorm_bwd_kernel<C, true><<<nblk, kThreads, 0, stream>>>(dyp, hp, wp, rstd.data_ptr<float>(),  \
+                                                                 drp, dxp, part.data_ptr<float>(), T, D); \
+    else                                                                                             \
+      rmsnorm_bwd_kernel<C, false><<<nblk, kThreads, 0, stream>>>(dyp, hp, wp, rstd.data_ptr<float>(), \
+                                                                  drp, dxp, part.data_ptr<float>(), T, D);
+    switch (MAXC) {
+      case 2: LAUNCH_BWD(2); break;
+      case 4: LAUNCH_BWD(4); break;
+      case 8: LAUNCH_BWD(8); break;
+      default: LAUNCH_BWD(16); break;
+    }
 #undef LAUNCH_BWD
+  }
   DLGM_CHECK_HIP(hipGetLastError());
+  // many partial rows: fold them 16 at a time in a wide first pass (fixed order: deterministic)
+  constexpr int kSlice = 16;
+  int64_t rows = nblk;
+  if (nblk > 4 * kSlice) {
+    const int64_t slices = (nblk + kSlice - 1) / kSlice;
+    auto part2 = at::empty({slices, D}, part.options());
+    const dim3 pgrid((D + kThreads - 1) / kThreads, slices);
+    column_partial_kernel<<<pgrid, kThreads, 0, stream>>>(part.data_ptr<float>(), part2.data_ptr<float>(), nblk,
+                                                          D, kSlice);
+    DLGM_CHECK_HIP(hipGetLastError());
+    part = part2;
+    rows = slices;
+  }
   const dim3 rgrid((D + 63) / 64);
   if (dw.scalar_type() == at::kFloat)
     column_reduce_kernel<float><<<rgrid, kThreads, 0, stream>>>(part.data_ptr<float>(),
-                                                                dw.data_ptr<float>(), nblk, D,
+                                                                dw.data_ptr<float>(), rows, D,
                                                                 accumulate_dw);
   else {
     TORCH_CHECK(dw.scalar_type() == at::kBFloat16, "rmsnorm_bwd: dw must be fp32 or bf16");
     column_reduce_kernel<bf16><<<rgrid, kThreads, 0, stream>>>(
-        part.data_ptr<float>(), reinterpret_cast<bf16*>(dw.data_ptr()), nblk, D, accumulate_dw);
+        part.data_ptr<float>(), reinterpret_cast<bf16*>(dw.data_ptr()), rows, D, accumulate_dw);
   }
   DLGM_CHECK_HIP(hipGetLastError());
   return dx;
