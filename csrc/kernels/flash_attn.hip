@@ -294,26 +294,30 @@ __global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams p) 
 // Backward
 // ----------------------------------------------------------------------------------
 
-// delta[b, hq, q] = sum_d dO[b,q,hq,d] * O[b,q,hq,d]   (one wave per row)
+// delta[b, hq, q] = sum_d dO[b,q,hq,d] * O[b,q,hq,d]. A row of D bf16 is D/8 lanes x 16 B, so a
+// wave64 covers 64 / (D/8) rows at once (4 at D = 128, 8 at D = 64): every lane loads, and the row
+// sum is a shuffle over the row's lane group only.
 template <int D>
 __global__ __launch_bounds__(256) void flash_bwd_delta_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ out,
                                                               float* __restrict__ delta, int B, int S, int Hq,
                                                               int64_t do_ss, int64_t do_sh, int64_t do_sb) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // row over (b, q, hq)
-  if (row >= (int64_t)B * S * Hq) return;
-  const int hq = row % Hq;
-  const int64_t bq = row / Hq;
+  constexpr int LPR = D / 8;             // lanes per row
+  constexpr int RPB = 256 / LPR;         // rows per block
+  const int sub = threadIdx.x % LPR;
+  const int64_t row = (int64_t)blockIdx.x * RPB + threadIdx.x / LPR;  // row over (b, q, hq)
+  const bool ok = row < (int64_t)B * S * Hq;
+  const int64_t rr = ok ? row : 0;
+  const int hq = rr % Hq;
+  const int64_t bq = rr / Hq;
   const int q = bq % S, b = bq / S;
+  const f32x8 a = load8f(dout + b * do_sb + (int64_t)q * do_ss + hq * do_sh + sub * 8);
+  const f32x8 c = load8f(out + rr * D + sub * 8);
   float acc = 0.f;
-  for (int d = lane * 8; d < D; d += 512) {
-    f32x8 a = load8f(dout + b * do_sb + (int64_t)q * do_ss + hq * do_sh + d);
-    f32x8 c = load8f(out + row * D + d);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc += a[j] * c[j];
-  }
-  acc = wave_sum(acc);
-  if (lane == 0) delta[((int64_t)b * Hq + hq) * S + q] = acc;
+  for (int j = 0; j < 8; ++j) acc += a[j] * c[j];
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (ok && sub == 0) delta[((int64_t)b * Hq + hq) * S + q] = acc;
 }
 
 struct BwdParams {
@@ -778,13 +782,13 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
   const int64_t rows = (int64_t)B * S * Hq;
   auto dop = reinterpret_cast<const bf16*>(dout.data_ptr());
   if (D == 128)
-    flash_bwd_delta_kernel<128><<<(rows + 3) / 4, 256, 0, stream>>>(dop, reinterpret_cast<const bf16*>(out.data_ptr()),
-                                                                     delta.data_ptr<float>(), B, S, Hq, dout.stride(1),
-                                                                     dout.stride(2), dout.stride(0));
+    flash_bwd_delta_kernel<128><<<(rows + 15) / 16, 256, 0, stream>>>(dop, reinterpret_cast<const bf16*>(out.data_ptr()),
+                                                                       delta.data_ptr<float>(), B, S, Hq, dout.stride(1),
+                                                                       dout.stride(2), dout.stride(0));
   else
-    flash_bwd_delta_kernel<64><<<(rows + 3) / 4, 256, 0, stream>>>(dop, reinterpret_cast<const bf16*>(out.data_ptr()),
-                                                                    delta.data_ptr<float>(), B, S, Hq, dout.stride(1),
-                                                                    dout.stride(2), dout.stride(0));
+    flash_bwd_delta_kernel<64><<<(rows + 31) / 32, 256, 0, stream>>>(dop, reinterpret_cast<const bf16*>(out.data_ptr()),
+                                                                      delta.data_ptr<float>(), B, S, Hq, dout.stride(1),
+                                                                      dout.stride(2), dout.stride(0));
   DLGM_CHECK_HIP(hipGetLastError());
   BwdParams p{reinterpret_cast<const bf16*>(q.data_ptr()), reinterpret_cast<const bf16*>(k.data_ptr()),
               reinterpret_cast<const bf16*>(v.data_ptr()), dop, lse.data_ptr<float>(), delta.data_ptr<float>(),
