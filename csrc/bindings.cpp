@@ -48,6 +48,10 @@ std::tuple<at::Tensor, at::Tensor> dlgm_moe_combine_bwd(const at::Tensor& dout, 
                                                         const at::Tensor& pos, const at::Tensor& gates);
 // transpose.hip
 at::Tensor dlgm_transpose(const at::Tensor& x, const c10::optional<at::Tensor>& out);
+// embedding.hip
+at::Tensor dlgm_embedding_fwd(const at::Tensor& table, const at::Tensor& ids);
+void dlgm_embedding_bwd_(at::Tensor grad, const at::Tensor& dy, const at::Tensor& sorted_ids, const at::Tensor& order);
+std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_router_topk(const at::Tensor& logits, int64_t k);
 
 TORCH_LIBRARY(dlgm, m) {
   m.def("rmsnorm_fwd(Tensor x, Tensor? residual, Tensor w, float eps) -> (Tensor, Tensor, Tensor)");
@@ -65,6 +69,9 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("moe_combine_bwd(Tensor dout, Tensor y, Tensor pos, Tensor gates) -> (Tensor, Tensor)");
   m.def("transpose(Tensor x, Tensor(a!)? out=None) -> Tensor");
   m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, float softmax_scale, bool causal, Tensor? dqkv=None) -> (Tensor, Tensor, Tensor)");
+  m.def("embedding_fwd(Tensor table, Tensor ids) -> Tensor");
+  m.def("embedding_bwd_(Tensor(a!) grad, Tensor dy, Tensor sorted_ids, Tensor order) -> ()");
+  m.def("router_topk(Tensor logits, int k) -> (Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(dlgm, CUDA, m) {
@@ -83,4 +90,7 @@ TORCH_LIBRARY_IMPL(dlgm, CUDA, m) {
   m.impl("moe_combine_fwd", &dlgm_moe_combine_fwd);
   m.impl("moe_combine_bwd", &dlgm_moe_combine_bwd);
   m.impl("transpose", &dlgm_transpose);
+  m.impl("embedding_fwd", &dlgm_embedding_fwd);
+  m.impl("embedding_bwd_", &dlgm_embedding_bwd_);
+  m.impl("router_topk", &dlgm_router_topk);
 }

@@ -53,8 +53,8 @@ class GPT2Embed(Unit):
         ids, pos = saved
         # second backward visit of the tied group: the head already wrote (or added) d(wte) and d(ln_f);
         # ctx.grad_acc is True here, so every write below accumulates
-        g["wpe"].index_put_((pos,), dy.to(g["wpe"].dtype), accumulate=True)
-        g["wte"].index_put_((ids,), dy.to(g["wte"].dtype), accumulate=True)
+        ops.embedding_bwd_(g["wpe"], dy, pos)
+        ops.embedding_bwd_(g["wte"], dy, ids)
         return None
 
 

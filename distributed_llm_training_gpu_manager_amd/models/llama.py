@@ -26,7 +26,6 @@ from __future__ import annotations
 from typing import Any, List, Optional, Tuple
 
 import torch
-import torch.nn.functional as F
 
 from .. import ops
 from ..ops.gemm import dx_mm, grad_mm
@@ -52,14 +51,14 @@ class LlamaEmbedding(Unit):
 
     def forward(self, p: Params, x, ctx: StepContext):
         ids = ctx.input_ids.reshape(-1)
-        return (F.embedding(ids, p["tok_embeddings"]), None), ids
+        return (ops.embedding_fwd(p["tok_embeddings"], ids), None), ids
 
     def backward(self, p: Params, g: Params, saved, dy, ctx: StepContext):
         ids = saved
         gt = g["tok_embeddings"]
         if not ctx.grad_acc:
             gt.zero_()
-        gt.index_put_((ids,), dy.reshape(-1, gt.shape[1]).to(gt.dtype), accumulate=True)
+        ops.embedding_bwd_(gt, dy, ids)  # sorted-run reduce: no atomics, deterministic [K10]
         return None
 
 

@@ -64,10 +64,7 @@ class MixtralBlock(LlamaBlock):
     def moe_forward(self, p: Params, hn2: torch.Tensor, ctx: StepContext):
         c = self.cfg
         T, E, K = hn2.shape[0], c.n_experts, c.top_k
-        logits = torch.mm(hn2, p["router"].t()).float()
-        probs = torch.softmax(logits, dim=-1)
-        topv, topi = logits.topk(K, dim=-1)
-        gates = torch.softmax(topv, dim=-1).contiguous()
+        probs, topi, gates = ops.router_topk(torch.mm(hn2, p["router"].t()), K)  # [K9]
         flat = topi.reshape(-1)
         order = torch.argsort(flat, stable=True)
         counts = torch.bincount(flat, minlength=E)

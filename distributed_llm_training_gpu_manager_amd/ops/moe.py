@@ -1,4 +1,5 @@
-"""MoE combine ops (kernel: csrc/kernels/moe.hip): gather-based, deterministic, no atomics."""
+"""MoE ops: router top-k (csrc/kernels/embedding.hip) and the gather-based, deterministic,
+atomic-free combine (csrc/kernels/moe.hip)."""
 from __future__ import annotations
 
 from typing import Optional, Tuple
@@ -6,6 +7,17 @@ from typing import Optional, Tuple
 import torch
 
 from .._native import hip_ops, use_native
+
+
+def router_topk(logits: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """fp32 router logits [T, E] -> (softmax probs [T, E], top-k expert ids [T, k] int64,
+    gates [T, k] = softmax over the selected logits) -- Mixtral routing in one pass."""
+    logits = logits.float().contiguous()
+    if use_native(logits):
+        return hip_ops().router_topk(logits, k)
+    probs = torch.softmax(logits, dim=-1)
+    topv, topi = logits.topk(k, dim=-1)
+    return probs, topi, torch.softmax(topv, dim=-1).contiguous()
 
 
 def moe_combine(y: torch.Tensor, pos: torch.Tensor, gates: Optional[torch.Tensor]) -> torch.Tensor:

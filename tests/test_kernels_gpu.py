@@ -268,3 +268,38 @@ def test_grad_mm_layouts(N, K, out_dtype):
                 assert rel_err(out, 2 * ref) < 1e-5 * 100, plan
         finally:
             gemm._plan = orig
+
+
+@pytest.mark.parametrize("D", [64, 4096])
+def test_embedding_fwd_bwd(D):
+    """Row gather + sorted-run scatter-add (repeated ids, fp32 and bf16 gradient tables) vs torch."""
+    torch.manual_seed(0)
+    V, T = 1000, 777
+    table = torch.randn(V, D, dtype=torch.bfloat16)
+    ids = torch.randint(0, 50, (T,))  # many repeats
+    ids[::7] = torch.randint(0, V, (len(ids[::7]),))
+    out = ops.embedding_fwd(table.to(DEV), ids.to(DEV))
+    assert torch.equal(out.cpu(), table[ids])
+    dy = torch.randn(T, D, dtype=torch.bfloat16)
+    ref = torch.full((V, D), 0.5).index_put_((ids,), dy.float(), accumulate=True)
+    for dt in (torch.float32, torch.bfloat16):
+        g = torch.full((V, D), 0.5, dtype=dt, device=DEV)
+        ops.embedding_bwd_(g, dy.to(DEV), ids.to(DEV))
+        assert rel_err(g, ref) < (1e-5 if dt == torch.float32 else 1e-2), dt
+    # deterministic: a second run gives the same bits
+    g1 = torch.zeros(V, D, device=DEV)
+    g2 = torch.zeros(V, D, device=DEV)
+    ops.embedding_bwd_(g1, dy.to(DEV), ids.to(DEV))
+    ops.embedding_bwd_(g2, dy.to(DEV), ids.to(DEV))
+    assert torch.equal(g1, g2)
+
+
+@pytest.mark.parametrize("E,K", [(8, 2), (8, 1), (16, 4)])
+def test_router_topk(E, K):
+    torch.manual_seed(0)
+    logits = torch.randn(1031, E) * 3
+    p_ref, i_ref, g_ref = ops.router_topk(logits, K)
+    p, i, g = ops.router_topk(logits.to(DEV), K)
+    assert rel_err(p, p_ref) < 1e-5
+    assert torch.equal(i.cpu(), i_ref)
+    assert rel_err(g, g_ref) < 1e-5
