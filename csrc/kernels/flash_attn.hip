@@ -86,6 +86,56 @@ __device__ __forceinline__ bf16x8 cat(bf16x4 a, bf16x4 b) {
   return (bf16x8){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
+typedef __attribute__((address_space(1))) const void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+// One LDS-DMA piece: 64 lanes x 16 B = 1 KiB landing lane-linearly at `lds` (wave-uniform).
+__device__ __forceinline__ void glds16(const void* src, void* lds) {
+  __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)lds, 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const void* src, void* lds) {
+  __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)lds, 4, 0, 0);
+}
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// One LDS-DMA piece through a buffer descriptor (buffer_load_dwordx4 ... lds): `base` and `nbytes`
+// are wave-uniform (the descriptor lives in SGPRs, reads at or past nbytes return zero), `voff`
+// is the per-lane byte offset, `soff` a wave-uniform byte offset (the tile advance).
+__device__ __forceinline__ void dma16(const void* base, int nbytes, uint32_t voff, uint32_t soff, void* lds) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, nbytes,
+                                                                             0x00020000),
+                                           (lptr_t)lds, 16, voff, soff, 0, 0);
+}
+
+// Loop-invariant LDS-DMA plan for a tile of ROWS x D bf16 rows that is re-staged every iteration
+// (the forward's recipe): the per-lane byte offsets of this wave's pieces are computed once, a
+// tile is then PPW buffer_load...lds per wave with a scalar row advance and no VALU. Rows at or
+// past the descriptor's end (row S) read as zeros. SWZ: 0 = row image, 1 = dual image, 2 = tr image.
+// A wave's pieces sit NW*PR rows apart (16 at D = 128, 32 at D = 64), a multiple of every swizzle's
+// row period, so they share ONE per-lane offset (1 VGPR) and differ only by a scalar soffset step.
+template <int D, int ROWS, int SWZ, int NW = 4>
+struct TileDma {
+  static constexpr int CH = D / 8, PR = 64 / CH, NP = ROWS / PR, PPW = NP / NW;
+  static_assert(NP % NW == 0, "pieces must split evenly over the waves");
+  static_assert((NW * PR) % 16 == 0, "piece row step must be a multiple of the swizzle period");
+  uint32_t off0;
+  int wave, nbytes;
+  int64_t stride;
+  const bf16* base;
+  __device__ __forceinline__ TileDma(const bf16* base_, int64_t row_stride, int nrows, int wave_, int lane)
+      : wave(wave_), nbytes((int)(((int64_t)(nrows - 1) * row_stride + D) * 2)), stride(row_stride), base(base_) {
+    const int rin = lane / CH, phys = lane % CH;
+    const int row = wave * PR + rin;
+    const int logical = SWZ == 2 ? swz_tr<D>(row, phys) : SWZ == 1 ? swz_dual<D>(row, phys) : swz_row<D>(row, phys);
+    off0 = (uint32_t)((row * row_stride + logical * 8) * 2);
+  }
+  __device__ __forceinline__ void issue(bf16* img, int row0) const {
+    const uint32_t soff = (uint32_t)(row0 * stride * 2), step = (uint32_t)(NW * PR * stride * 2);
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) dma16(base, nbytes, off0, soff + j * step, img + (wave + NW * j) * 512);
+  }
+};
+
 // bijective remap of the block id so that consecutive work items land on one XCD
 __device__ __forceinline__ int xcd_remap(int id, int total) {
   if (total % 8 != 0) return id;
@@ -116,7 +166,6 @@ __global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams p) 
   constexpr int KK = D / 16;  // MFMA k-steps over the head dim
   constexpr int DT = D / 32;  // 32-wide output tiles over the head dim
   constexpr int TILE = kFwdBKV * D;
-  constexpr int LOADS = kFwdBKV * CH / kFwdThreads;  // 16B chunks per thread per tensor
   __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -153,30 +202,15 @@ __global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams p) 
   const int kv_end = p.causal ? min(p.S, q0 + kFwdBQ) : p.S;
   const int nt = (kv_end + kFwdBKV - 1) / kFwdBKV;
 
-  uint4 kreg[LOADS], vreg[LOADS];
-  auto gload = [&](int t) {
-#pragma unroll
-    for (int i = 0; i < LOADS; ++i) {
-      const int c = threadIdx.x + i * kFwdThreads;
-      const int row = c / CH, ch = c % CH;
-      const int kv = t * kFwdBKV + row;
-      if (kv < p.S) {
-        kreg[i] = *reinterpret_cast<const uint4*>(kb + (int64_t)kv * p.k_ss + ch * 8);
-        vreg[i] = *reinterpret_cast<const uint4*>(vb + (int64_t)kv * p.v_ss + ch * 8);
-      } else {
-        kreg[i] = make_uint4(0, 0, 0, 0);
-        vreg[i] = make_uint4(0, 0, 0, 0);
-      }
-    }
-  };
-  auto lstore = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < LOADS; ++i) {
-      const int c = threadIdx.x + i * kFwdThreads;
-      const int row = c / CH, ch = c % CH;
-      *reinterpret_cast<uint4*>(smem + buf * TILE + row * D + swz_row<D>(row, ch) * 8) = kreg[i];
-      *reinterpret_cast<uint4*>(smem + (2 + buf) * TILE + row * D + swz_tr<D>(row, ch) * 8) = vreg[i];
-    }
+  // K/V tiles arrive by LDS-DMA (buffer_load ... lds, TileDma): 16 B per lane landing
+  // lane-linearly, the XOR swizzle applied to the SOURCE offset, the tile advance a scalar soffset
+  // -- staging costs no VALU and no VGPR round trip; rows past S read as zero.
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const TileDma<D, kFwdBKV, 0> kdma(kb, p.k_ss, p.S, wu, lane);
+  const TileDma<D, kFwdBKV, 2> vdma(vb, p.v_ss, p.S, wu, lane);
+  auto stage = [&](int buf, int t) {
+    kdma.issue(smem + buf * TILE, t * kFwdBKV);
+    vdma.issue(smem + (2 + buf) * TILE, t * kFwdBKV);
   };
 
   f32x16 o[DT];
@@ -185,12 +219,12 @@ __global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams p) 
   float m_run = -INFINITY, l_run = 0.f;
   const int qcol = q0w + r;
 
-  gload(0);
+  stage(0, 0);
   for (int t = 0; t < nt; ++t) {
     const int buf = t & 1;
-    lstore(buf);
-    __syncthreads();
-    if (t + 1 < nt) gload(t + 1);
+    vm_drain();  // this tile's DMA has landed (this wave's pieces) ...
+    __syncthreads();  // ... and every wave's; the other buffer's readers are done
+    if (t + 1 < nt) stage(buf ^ 1, t + 1);
     const int kv0 = t * kFwdBKV;
     if (p.causal && kv0 > q0w + 31) continue;  // whole tile above this wave's diagonal
     const bf16* kt = smem + buf * TILE;
@@ -345,17 +379,7 @@ struct BwdParams {
   bool causal;
 };
 
-typedef __attribute__((address_space(1))) const void* gptr_t;
-typedef __attribute__((address_space(3))) void* lptr_t;
 
-// One LDS-DMA piece: 64 lanes x 16 B = 1 KiB landing lane-linearly at `lds` (wave-uniform).
-__device__ __forceinline__ void glds16(const void* src, void* lds) {
-  __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)lds, 16, 0, 0);
-}
-__device__ __forceinline__ void glds4(const void* src, void* lds) {
-  __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)lds, 4, 0, 0);
-}
-__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Stage ROWS x D bf16 rows (row r at base + r*row_stride, r clamped to < nrows_valid) into an
 // LDS image swizzled by SWZ, using LDS-DMA pieces issued by `wave` of `nwaves`. The image is

@@ -18,7 +18,8 @@ from pathlib import Path
 import torch
 
 _PKG_DIR = Path(__file__).resolve().parent
-HIP_LIB = _PKG_DIR / "_dlgm_hip.so"
+# DLGM_HIP_LIB: A/B a different build of the kernels in the same process/device (tools/ab_kernels.sh)
+HIP_LIB = Path(os.environ.get("DLGM_HIP_LIB", _PKG_DIR / "_dlgm_hip.so"))
 HOST_LIB = _PKG_DIR / "_dlgm_host.so"
 
 _lock = threading.Lock()
