@@ -29,6 +29,7 @@
 //    atomics shaped as 128-byte row segments.
 #include <torch/all.h>
 #include <c10/hip/HIPStream.h>
+#include <type_traits>
 #include "dlgm_common.h"
 
 using namespace dlgm;
@@ -219,14 +220,16 @@ __global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams p) 
   float m_run = -INFINITY, l_run = 0.f;
   const int qcol = q0w + r;
 
-  stage(0, 0);
-  for (int t = 0; t < nt; ++t) {
-    const int buf = t & 1;
+  // One KV tile. The loop below is unrolled by two so that the LDS buffer is a compile-time
+  // constant in each copy: every ds_read then addresses (per-lane offset VGPR + immediate), with no
+  // per-read address add in the loop.
+  auto tile = [&](auto bufc, int t) {
+    constexpr int buf = decltype(bufc)::value;
     vm_drain();  // this tile's DMA has landed (this wave's pieces) ...
     __syncthreads();  // ... and every wave's; the other buffer's readers are done
     if (t + 1 < nt) stage(buf ^ 1, t + 1);
     const int kv0 = t * kFwdBKV;
-    if (p.causal && kv0 > q0w + 31) continue;  // whole tile above this wave's diagonal
+    if (p.causal && kv0 > q0w + 31) return;  // whole tile above this wave's diagonal
     const bf16* kt = smem + buf * TILE;
     const bf16* vt = smem + (2 + buf) * TILE;
 
@@ -304,6 +307,11 @@ __global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams p) 
           o[dt] = mfma32(cat(a1, a2), pf[u][s2], o[dt]);
         }
     }
+  };
+  stage(0, 0);
+  for (int t = 0; t < nt; t += 2) {
+    tile(std::integral_constant<int, 0>{}, t);
+    if (t + 1 < nt) tile(std::integral_constant<int, 1>{}, t + 1);
   }
 
   // ---- epilogue: normalise, store O [b, q, hq, d] and LSE [b, hq, q]
