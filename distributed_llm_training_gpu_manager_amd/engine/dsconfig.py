@@ -67,6 +67,12 @@ def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, **overri
         max_reuse_distance=zo.get("stage3_max_reuse_distance", 1e9),
         prefetch_bucket_size=float(zo.get("stage3_prefetch_bucket_size", 5e8)),
     )
+    # engine knobs without a DeepSpeed key travel in the "mi355x" block (launcher.config.MI355XOptions)
+    mi = ds.get("mi355x") or {}
+    cfg.expert_parallel_size = int(mi.get("expert_parallel_size", cfg.expert_parallel_size))
+    cfg.sequence_parallel_size = int(mi.get("sequence_parallel_size", cfg.sequence_parallel_size))
+    if mi.get("comm_dtype"):
+        cfg.comm_dtype = {"fp32": torch.float32, "float32": torch.float32}.get(mi["comm_dtype"], torch.bfloat16)
     for k, v in overrides.items():
         setattr(cfg, k, v)
     return cfg, notes

@@ -37,17 +37,23 @@ from .dsconfig import engine_config_from_ds
 class SyntheticData:
     """Deterministic random token batches: (seed, rank, step, micro) -> the same tokens after a restart."""
 
-    def __init__(self, vocab: int, mbs: int, seq: int, ga: int, seed: int, rank: int, device: torch.device):
+    def __init__(self, vocab: int, mbs: int, seq: int, ga: int, seed: int, rank: int, device: torch.device,
+                 sp_rank: int = 0, sp_size: int = 1):
+        """`rank` is the data-parallel rank; under sequence parallelism every rank of an SP group draws
+        the same full sequences and keeps its own contiguous chunk of seq / sp_size tokens."""
         self.vocab, self.mbs, self.seq, self.ga = vocab, mbs, seq, ga
         self.seed, self.rank, self.device = seed, rank, device
+        self.sp_rank, self.sp_size = sp_rank, sp_size
         self.gen = torch.Generator(device=device)
 
     def batches(self, step: int) -> List[Tuple[torch.Tensor, torch.Tensor]]:
         out = []
+        n = self.seq // self.sp_size
+        sl = slice(self.sp_rank * n, (self.sp_rank + 1) * n)
         for mi in range(self.ga):
             self.gen.manual_seed(((self.seed * 1_000_003 + self.rank) * 1_000_003 + step) * 131 + mi)
             toks = torch.randint(0, self.vocab, (self.mbs, self.seq + 1), device=self.device, generator=self.gen)
-            out.append((toks[:, :-1].contiguous(), toks[:, 1:].contiguous()))
+            out.append((toks[:, :-1][:, sl].contiguous(), toks[:, 1:][:, sl].contiguous()))
         return out
 
 
@@ -94,6 +100,14 @@ class Trainer:
                                                  seed=args.seed), []
         if args.lr_scale != 1.0:
             self.ecfg.lr *= args.lr_scale
+        if getattr(args, "expert_parallel", 0):
+            self.ecfg.expert_parallel_size = args.expert_parallel
+        if getattr(args, "sequence_parallel", 0):
+            # --seq-len is the FULL sequence; each rank of the SP group holds one contiguous chunk
+            assert args.seq_len % args.sequence_parallel == 0, "--seq-len must divide by --sequence-parallel"
+            self.ecfg.sequence_parallel_size = args.sequence_parallel
+        self.sp = max(1, self.ecfg.sequence_parallel_size)
+        self.ecfg.seq_len = args.seq_len // self.sp
         if getattr(args, "wall_clock_breakdown", False):
             self.ecfg.wall_clock_breakdown = True
         self.engine = ZeroEngine(self.mcfg, self.ecfg, self.env.device, self.comm)
@@ -102,7 +116,8 @@ class Trainer:
         save_dir = args.save_dir or os.environ.get("DLGM_SAVE_DIR")
         self.ckpt = AsyncCheckpointer(self.engine, save_dir, mode=args.ckpt_mode) if save_dir else None
         self.data = SyntheticData(self.mcfg.vocab_size, self.ecfg.micro_batch_size, args.seq_len,
-                                  self.ecfg.grad_accum, args.seed, self.env.rank, self.env.device)
+                                  self.ecfg.grad_accum, args.seed, self.env.rank // self.sp, self.env.device,
+                                  sp_rank=self.env.rank % self.sp, sp_size=self.sp)
         self.pusher = MetricsPusher(args.metrics_url if self.env.rank == 0 else None,
                                     os.environ.get("DLGM_JOB_ID", args.job_id))
         self.preempt = False
@@ -138,7 +153,7 @@ class Trainer:
                 self.monitor.reset()
         for n in self.notes:
             self._say(f"note: {n}")
-        tokens_step = self.ecfg.micro_batch_size * a.seq_len * self.ecfg.grad_accum * self.env.world
+        tokens_step = self.ecfg.micro_batch_size * self.ecfg.seq_len * self.ecfg.grad_accum * self.env.world
         t_last = time.time()
         rc = 0
         for step in range(start + 1, a.steps + 1):
@@ -232,6 +247,9 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--log-json", default=None)
     ap.add_argument("--n-layers", type=int, default=0, help="override the preset's depth (drills only)")
     ap.add_argument("--wall-clock-breakdown", action="store_true", help="per-phase HIP-event timers in the log")
+    ap.add_argument("--expert-parallel", type=int, default=0, help="expert-parallel size (Mixtral)")
+    ap.add_argument("--sequence-parallel", type=int, default=0,
+                    help="Ulysses sequence-parallel size: ranks of a group split each sequence")
     a, unknown = ap.parse_known_args(argv)
     return a
 

@@ -54,6 +54,7 @@ class MI355XOptions(BaseModel):
     max_restarts: int = Field(default=3, ge=0)
     comm_dtype: Optional[str] = None
     expert_parallel_size: int = Field(default=1, ge=1)
+    sequence_parallel_size: int = Field(default=1, ge=1, description="Ulysses sequence parallelism (long context)")
 
 
 class DeepSpeedConfig(BaseModel):

@@ -55,6 +55,7 @@ class StepContext:
     grad_scale: float  # d(loss_total)/d(loss_row)
     rope: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
     ep_group: Any = None
+    sp_group: Any = None  # sequence-parallel Comm (parallel/sp.py): seq_len is then the LOCAL chunk
     aux: Dict[str, Any] = field(default_factory=dict)
     grad_acc: bool = False  # backward ADDS into the gradient views (later micro-batch / tied second visit)
 

@@ -29,6 +29,7 @@ import torch
 
 from .. import ops
 from ..ops.gemm import dx_mm, grad_mm
+from ..parallel.sp import sp_attention_bwd, sp_attention_fwd
 from .common import ParamSpec, Params, StepContext, Unit
 from .config import ModelConfig
 
@@ -89,9 +90,14 @@ class LlamaBlock(Unit):
         hn1, x, rstd1 = ops.rmsnorm_fwd(xa, p["attn_norm"], c.norm_eps, residual=xb)
         qkv = torch.mm(hn1, p["wqkv"].t())
         cos, sin = ctx.rope
-        ops.rope_(qkv, cos, sin, c.n_heads + c.n_kv_heads, c.head_dim, S)
-        q, k, v = self._split(qkv, B, S)
-        attn, lse = ops.flash_attn_fwd(q, k, v, causal=True)
+        ops.rope_(qkv, cos, sin, c.n_heads + c.n_kv_heads, c.head_dim, S)  # SP: tables start at this chunk
+        if ctx.sp_group is not None:
+            # sequence parallel: all-to-all to (full sequence, head slice), attention, all-to-all back;
+            # the `lse` slot carries what the backward needs
+            attn, lse = sp_attention_fwd(qkv, B, S, c.n_heads, c.n_kv_heads, c.head_dim, ctx.sp_group)
+        else:
+            q, k, v = self._split(qkv, B, S)
+            attn, lse = ops.flash_attn_fwd(q, k, v, causal=True)
         attn2d = attn.view(T, c.n_heads * c.head_dim)
         o = torch.mm(attn2d, p["wo"].t())
         return (x, rstd1, hn1, qkv, attn, lse), o
@@ -116,9 +122,12 @@ class LlamaBlock(Unit):
         acc = ctx.grad_acc
         grad_mm(g["wo"], dh.t(), attn2d, acc)
         dattn = dx_mm(dh, p, "wo").view_as(attn)
-        q, k, v = self._split(qkv, B, S)
         dqkv = torch.empty_like(qkv).view(T, -1)
-        ops.flash_attn_bwd(dattn, q, k, v, attn, lse, causal=True, dqkv=dqkv)
+        if ctx.sp_group is not None:
+            sp_attention_bwd(dattn, lse, B, S, c.n_heads, c.n_kv_heads, c.head_dim, ctx.sp_group, dqkv)
+        else:
+            q, k, v = self._split(qkv, B, S)
+            ops.flash_attn_bwd(dattn, q, k, v, attn, lse, causal=True, dqkv=dqkv)
         cos, sin = ctx.rope
         ops.rope_(dqkv, cos, sin, c.n_heads + c.n_kv_heads, c.head_dim, S, inverse=True)
         grad_mm(g["wqkv"], dqkv.t(), hn1, acc)

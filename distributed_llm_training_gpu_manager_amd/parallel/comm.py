@@ -146,19 +146,24 @@ class Comm:
         if not self.is_gloo:
             return Handle(dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group,
                                                  async_op=async_op))
-        # gloo has no all_to_all: emulate with per-peer send/recv pairs (CPU tests only)
+        # gloo has no all_to_all: emulate with per-peer send/recv pairs (tests only; gloo's point-to-point
+        # ops take host tensors, so device tensors are staged through host memory)
         ins = list(inp.split(in_splits if in_splits else [inp.shape[0] // self.world] * self.world))
         outs = list(out.split(out_splits if out_splits else [out.shape[0] // self.world] * self.world))
+        host = [o.cpu() if o.is_cuda else o for o in outs]
         ops = []
         for peer in range(self.world):
             if peer == self.rank:
                 outs[peer].copy_(ins[peer])
                 continue
-            ops.append(dist.P2POp(dist.isend, ins[peer].contiguous(), peer, group=self.group))
-            ops.append(dist.P2POp(dist.irecv, outs[peer], peer, group=self.group))
+            ops.append(dist.P2POp(dist.isend, ins[peer].contiguous().cpu(), peer, group=self.group))
+            ops.append(dist.P2POp(dist.irecv, host[peer], peer, group=self.group))
         if ops:
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
+        for peer in range(self.world):
+            if peer != self.rank and host[peer] is not outs[peer]:
+                outs[peer].copy_(host[peer])
         return DONE
 
     def broadcast(self, t: torch.Tensor, src: int = 0) -> None:

@@ -87,6 +87,9 @@ class EngineConfig:
     live_hbm_fraction: float = 0.12
     seed: int = 1234
     expert_parallel_size: int = 1
+    # Ulysses sequence parallelism (parallel/sp.py): seq_len is then the LOCAL chunk per rank and a
+    # group of sequence_parallel_size consecutive ranks holds one sequence of seq_len * size tokens
+    sequence_parallel_size: int = 1
     offload_optimizer: str = "none"  # none | cpu | nvme (ZeRO-Offload parity path: parallel/offload.py)
     nvme_path: Optional[str] = None
     wall_clock_breakdown: bool = False  # per-phase HIP-event timers (utils/timers.py)
@@ -202,6 +205,12 @@ class ZeroEngine:
             self.ep_comm, self.edp_comm = None, self.comm
         ep_comm = ep_comm or self.ep_comm
         self.ep_comm = ep_comm
+        self.sp_size, self.sp_comm = max(1, cfg.sequence_parallel_size), None
+        if self.sp_size > 1 and self.W > 1:
+            from .sp import build_sp_comm
+            self.sp_comm = build_sp_comm(self.sp_size)
+        else:
+            self.sp_size = 1
         ep_rank = self.ep_comm.rank if self.ep_comm is not None else 0
         self.gather_comm = self.comm
         if cfg.separate_gather_comm and self.W > 1 and self.stage > 0:
@@ -252,8 +261,11 @@ class ZeroEngine:
         self.loss_acc = torch.zeros((), dtype=torch.float32, device=device)
         from ..ops.rope import rope_tables
         if model_cfg.arch in ("llama", "mixtral"):
-            self.rope = rope_tables(model_cfg.head_dim, max(cfg.seq_len, 1), model_cfg.rope_theta, device,
-                                    model_cfg.rope_scaling)
+            S = max(cfg.seq_len, 1)
+            cos, sin = rope_tables(model_cfg.head_dim, S * self.sp_size, model_cfg.rope_theta, device,
+                                   model_cfg.rope_scaling)
+            off = (self.sp_comm.rank if self.sp_comm is not None else 0) * S  # this rank's chunk: global positions
+            self.rope = (cos[off:off + S].contiguous(), sin[off:off + S].contiguous())
         else:
             self.rope = None
         # group visit bookkeeping (tied weights appear twice)
@@ -483,7 +495,7 @@ class ZeroEngine:
         if self.scaler is not None:
             gs *= self.scaler.scale
         return StepContext(batch=B, seq_len=S, input_ids=ids, labels=labels, grad_scale=gs, rope=self.rope,
-                           ep_group=self.ep_comm)
+                           ep_group=self.ep_comm, sp_group=self.sp_comm)
 
     def micro_step(self, ids: torch.Tensor, labels: torch.Tensor, first: bool, last: bool) -> torch.Tensor:
         ctx = self._context(ids, labels)
