@@ -646,16 +646,18 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams p
 
   const int kv_end = p.causal ? min(p.S, q0 + kDqBQ) : p.S;
   const int nt = (kv_end + kDqBKV - 1) / kDqBKV;
+  const TileDma<D, kDqBKV, 1> kdma(kb, p.k_ss, p.S, w, lane);
+  const TileDma<D, kDqBKV, 0> vdma(vb, p.v_ss, p.S, w, lane);
   auto stage = [&](int buf, int t) {
     bf16* img = smem + buf * 2 * TILE;
-    stage_rows<D, kDqBKV, 1>(img, kb, p.k_ss, t * kDqBKV, p.S, w, lane);
-    stage_rows<D, kDqBKV, 0>(img + TILE, vb, p.v_ss, t * kDqBKV, p.S, w, lane);
+    kdma.issue(img, t * kDqBKV);
+    vdma.issue(img + TILE, t * kDqBKV);
   };
-  stage(0, 0);
-  vm_drain();
-  __syncthreads();
-  for (int t = 0; t < nt; ++t) {
-    const int buf = t & 1;
+  // unrolled by two: the LDS buffer is a compile-time constant in each copy (immediate ds_read offsets)
+  auto tile = [&](auto bufc, int t) {
+    constexpr int buf = decltype(bufc)::value;
+    vm_drain();
+    __syncthreads();
     if (t + 1 < nt) stage(buf ^ 1, t + 1);
     const int kv0 = t * kDqBKV;
     if (!(p.causal && kv0 > q0w + 31)) {
@@ -709,8 +711,11 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams p
           }
       }
     }
-    vm_drain();
-    __syncthreads();
+  };
+  stage(0, 0);
+  for (int t = 0; t < nt; t += 2) {
+    tile(std::integral_constant<int, 0>{}, t);
+    if (t + 1 < nt) tile(std::integral_constant<int, 1>{}, t + 1);
   }
   if (qcol < p.S) {
     bf16* orow = p.dq + ((int64_t)b * p.S + qcol) * p.dq_ss + hq * D;
