@@ -460,11 +460,12 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
   const int nqt = (p.S + kKvBQ - 1) / kKvBQ;
   const int t0 = p.causal ? k0 / kKvBQ : 0;
 
+  const TileDma<D, kKvBQ, 1> qdma(qb, p.q_ss, p.S, w, lane), dodma(dob, p.do_ss, p.S, w, lane);
   auto stage = [&](int buf, int t) {
     const int q0 = t * kKvBQ;
     bf16* img = smem + buf * 2 * QT;
-    stage_rows<D, kKvBQ, 1>(img, qb, p.q_ss, q0, p.S, w, lane);
-    stage_rows<D, kKvBQ, 1>(img + QT, dob, p.do_ss, q0, p.S, w, lane);
+    qdma.issue(img, q0);
+    dodma.issue(img + QT, q0);
     if (w == 0) {
       int q = q0 + (lane & 31);
       q = q < p.S ? q : p.S - 1;
@@ -472,11 +473,11 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
     }
   };
 
-  if (t0 < nqt) stage(0, t0);
-  vm_drain();
-  __syncthreads();
-  for (int t = t0; t < nqt; ++t) {
-    const int buf = (t - t0) & 1;
+  // unrolled by two: the LDS buffer is a compile-time constant in each copy (immediate ds_read offsets)
+  auto tile = [&](auto bufc, int t) {
+    constexpr int buf = decltype(bufc)::value;
+    vm_drain();  // this tile's LDS-DMA has landed ...
+    __syncthreads();  // ... for every wave, and the other buffer's readers are done
     if (t + 1 < nqt) stage(buf ^ 1, t + 1);
     const int q0 = t * kKvBQ;
     const bool active = uniform(!(p.causal && q0 + kKvBQ - 1 < kw0));
@@ -541,8 +542,11 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
         }
       }
     }
-    vm_drain();  // the next tile's LDS-DMA has landed
-    __syncthreads();
+  };
+  if (t0 < nqt) stage(0, t0);
+  for (int t = t0; t < nqt; t += 2) {
+    tile(std::integral_constant<int, 0>{}, t);
+    if (t + 1 < nqt) tile(std::integral_constant<int, 1>{}, t + 1);
   }
   if (key >= p.S) return;
 #pragma unroll
