@@ -1,0 +1,59 @@
+"""bench.py driver contract, exercised on CPU/gloo with a tiny model.
+
+The round driver runs ``python -m torch.distributed.run --nnodes=1 --nproc-per-node N
+--master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W`` and reads ONE JSON
+line from rank 0 with a fixed set of fields; the N > 1 path (process group, max over ranks, whole-job
+tokens/s) is checked here with two gloo ranks.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIELDS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+          "vs_baseline", "dtype", "data", "config"}
+
+
+def _port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(cmd):
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    res = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout
+    return json.loads(lines[0])
+
+
+def _check(out, n, steps, warmup):
+    assert FIELDS <= set(out), FIELDS - set(out)
+    assert out["n_gpus"] == n and out["steps"] == steps and out["warmup"] == warmup
+    assert out["value"] > 0 and out["ms_per_step"] > 0 and out["higher_is_better"] is True
+    assert out["scaling"] == "weak" and out["dtype"] == "bf16"
+    cfg = out["config"]
+    assert cfg["parallelism"] == f"zero3-dp{n}" and cfg["seq_len"] == 64
+    # whole-job tokens/s: N ranks x mbs x seq x GA tokens per step
+    tokens = n * cfg["micro_batch_per_gpu"] * cfg["seq_len"] * cfg["grad_accum"] * steps
+    assert abs(out["value"] - tokens / (out["ms_per_step"] * steps / 1000)) / out["value"] < 0.02
+
+
+def test_bench_single_process():
+    out = _run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--model", "llama-tiny", "--seq", "64",
+                "--ga", "2"])
+    _check(out, 1, 2, 1)
+
+
+def test_bench_torchrun_two_ranks():
+    out = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--steps", "2",
+                "--warmup", "1", "--model", "llama-tiny", "--seq", "64", "--ga", "2"])
+    _check(out, 2, 2, 1)
+    assert out["extra"]["zero3_allgathers_per_step"] > 0  # partitioned: the residency plan gathers once per unit
