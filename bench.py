@@ -46,7 +46,9 @@ def main() -> int:
     ap.add_argument("--live-params", default="hbm",
                     help="ZeRO-3 stage3_max_live_parameters: a number, or 'hbm' = sized to the GPU's memory")
     ap.add_argument("--reuse-distance", default="hbm", help="ZeRO-3 stage3_max_reuse_distance (number or 'hbm')")
-    ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--profile-steps", type=int, default=0,
+                    help="after the timed steps, trace this many extra steps with torch.profiler")
+    ap.add_argument("--profile-dir", default="gpurun_out/torch_trace")
     args = ap.parse_args()
 
     from distributed_llm_training_gpu_manager_amd.models import get_config
@@ -94,6 +96,12 @@ def main() -> int:
     t = torch.tensor([elapsed], dtype=torch.float64, device=env.device)
     comm.all_reduce_max(t)
     elapsed = float(t.item())
+
+    if args.profile_steps > 0:  # outside the timed region: never part of the reported number
+        from distributed_llm_training_gpu_manager_amd.utils.profiling import trace_window
+        with trace_window(args.profile_dir, env.rank):
+            for _ in range(args.profile_steps):
+                eng.train_step(batches)
 
     tokens_per_step_gpu = args.mbs * args.seq * args.ga
     total_tokens = tokens_per_step_gpu * env.world * args.steps

@@ -31,6 +31,7 @@ from ..launcher.supervisor import EXIT_NAN_HALT, EXIT_PREEMPTED, write_status
 from ..models import get_config
 from ..parallel.comm import Comm, init_distributed
 from ..parallel.zero import EngineConfig, ZeroEngine
+from ..utils.profiling import trace_window
 from .dsconfig import engine_config_from_ds
 
 
@@ -159,7 +160,11 @@ class Trainer:
         for step in range(start + 1, a.steps + 1):
             if a.inject_nan_step == step:
                 self.engine.fault_inject_nan = True
-            m = self.engine.train_step(self.data.batches(step))
+            prof = getattr(a, "profile_steps", 0) and step - start == 2  # trace window after one warm step
+            with trace_window(a.profile_dir if prof else None, self.env.rank):
+                m = self.engine.train_step(self.data.batches(step))
+                for _ in range(a.profile_steps - 1 if prof else 0):  # extra traced steps reuse this step's data
+                    self.engine.train_step(self.data.batches(step))
             self.trap.record(step, self.engine.stats)
             # deterministic halt decision: every rank reads the (all-reduced) stats of THIS step
             bad = float(self.engine.stats[1].item())
@@ -248,6 +253,8 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--n-layers", type=int, default=0, help="override the preset's depth (drills only)")
     ap.add_argument("--wall-clock-breakdown", action="store_true", help="per-phase HIP-event timers in the log")
     ap.add_argument("--expert-parallel", type=int, default=0, help="expert-parallel size (Mixtral)")
+    ap.add_argument("--profile-steps", type=int, default=0, help="torch.profiler trace of N steps (from step 2)")
+    ap.add_argument("--profile-dir", default="torch_trace")
     ap.add_argument("--sequence-parallel", type=int, default=0,
                     help="Ulysses sequence-parallel size: ranks of a group split each sequence")
     a, unknown = ap.parse_known_args(argv)
