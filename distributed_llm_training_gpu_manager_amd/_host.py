@@ -35,6 +35,22 @@ def lib():
                                      ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)]
         L.dlgm_close_file.restype = ctypes.c_int
         L.dlgm_close_file.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.dlgm_aio_create.restype = ctypes.c_void_p
+        L.dlgm_aio_create.argtypes = [ctypes.c_int, ctypes.c_size_t]
+        L.dlgm_aio_destroy.restype = None
+        L.dlgm_aio_destroy.argtypes = [ctypes.c_void_p]
+        L.dlgm_aio_open.restype = ctypes.c_int
+        L.dlgm_aio_open.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_size_t]
+        L.dlgm_aio_is_direct.restype = ctypes.c_int
+        L.dlgm_aio_is_direct.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.dlgm_aio_close.restype = ctypes.c_int
+        L.dlgm_aio_close.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        L.dlgm_aio_submit.restype = ctypes.c_int64
+        L.dlgm_aio_submit.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                      ctypes.c_int]
+        for fn in (L.dlgm_aio_wait, L.dlgm_aio_poll):
+            fn.restype = ctypes.c_int
+            fn.argtypes = [ctypes.c_void_p, ctypes.c_int64]
         L.dlgm_cpu_adamw.restype = None
         L.dlgm_cpu_adamw.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_size_t] + [ctypes.c_float] * 8
         _lib = L
@@ -149,3 +165,72 @@ class StreamWriter:
                 os.fsync(self.f.fileno())
             self.f.close()
         return self.crcs
+
+
+def aligned_empty(numel: int, dtype: torch.dtype = torch.float32, align: int = 4096) -> torch.Tensor:
+    """A CPU tensor whose storage starts on an `align`-byte boundary (O_DIRECT staging)."""
+    esz = torch.empty((), dtype=dtype).element_size()
+    raw = torch.empty(numel * esz + align, dtype=torch.uint8)
+    skip = (-raw.data_ptr()) % align
+    return raw[skip:skip + numel * esz].view(dtype)
+
+
+class Aio:
+    """Asynchronous pread/pwrite engine (csrc/host/aio.cpp): a persistent I/O thread pool, requests split
+    into `block_size` pieces, non-blocking submit returning a ticket. DeepSpeed ``aio`` block parity:
+    ``thread_count`` x ``queue_depth`` pieces in flight."""
+
+    def __init__(self, threads: int = 8, block_size: int = 8 << 20):
+        L = lib()
+        if L is None:
+            raise RuntimeError("host runtime _dlgm_host.so not built")
+        self._L = L
+        self._e = ctypes.c_void_p(L.dlgm_aio_create(int(threads), int(block_size)))
+
+    def open(self, path: str, size: int = 0, direct: bool = False) -> int:
+        h = self._L.dlgm_aio_open(self._e, path.encode(), int(direct), int(size))
+        if h < 0:
+            raise OSError(-h, os.strerror(-h), path)
+        return h
+
+    def is_direct(self, h: int) -> bool:
+        return bool(self._L.dlgm_aio_is_direct(self._e, h))
+
+    def _submit(self, h: int, t: torch.Tensor, offset: int, write: int) -> int:
+        assert t.device.type == "cpu" and t.is_contiguous()
+        tk = self._L.dlgm_aio_submit(self._e, h, ctypes.c_void_p(t.data_ptr()), t.numel() * t.element_size(),
+                                     int(offset), write)
+        if tk < 0:
+            raise OSError(-tk, os.strerror(-tk))
+        return tk
+
+    def read(self, h: int, t: torch.Tensor, offset: int) -> int:
+        """Start filling `t` from byte `offset` of file `h`; returns a ticket (keep `t` alive until waited)."""
+        return self._submit(h, t, offset, 0)
+
+    def write(self, h: int, t: torch.Tensor, offset: int) -> int:
+        return self._submit(h, t, offset, 1)
+
+    def wait(self, ticket: int) -> None:
+        rc = self._L.dlgm_aio_wait(self._e, ticket)
+        if rc != 0:
+            raise OSError(-rc, os.strerror(-rc))
+
+    def done(self, ticket: int) -> bool:
+        return self._L.dlgm_aio_poll(self._e, ticket) == 1
+
+    def close(self, h: int, fsync: bool = False) -> None:
+        rc = self._L.dlgm_aio_close(self._e, h, int(fsync))
+        if rc != 0:
+            raise OSError(-rc, os.strerror(-rc))
+
+    def shutdown(self) -> None:
+        if self._e:
+            self._L.dlgm_aio_destroy(self._e)  # drains queued pieces, joins the threads, closes files
+            self._e = ctypes.c_void_p(None)
+
+    def __del__(self):
+        try:
+            self.shutdown()
+        except Exception:
+            pass

@@ -61,6 +61,9 @@ def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, **overri
         min_loss_scale=float(ds.get("fp16", {}).get("min_loss_scale", 1.0)),
         offload_optimizer=off_o,
         nvme_path=zo.get("offload_optimizer", {}).get("nvme_path"),
+        offload_buffer_count=int(zo.get("offload_optimizer", {}).get("buffer_count", 4)),
+        aio_threads=max(1, int(ds.get("aio", {}).get("thread_count", 1)) * int(ds.get("aio", {}).get("queue_depth", 8))),
+        aio_block_size=int(ds.get("aio", {}).get("block_size", 8 << 20)),
         wall_clock_breakdown=bool(ds.get("wall_clock_breakdown", False)),
         # ZeRO-3 residency (parallel/residency.py); a number, or "hbm" to size the budget to the GPU
         max_live_parameters=zo.get("stage3_max_live_parameters", 1e9),

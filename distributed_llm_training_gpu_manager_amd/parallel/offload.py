@@ -16,10 +16,19 @@ Step (one HIP side stream, two pinned staging slots per direction)
     CPU  AdamW chunk i       (csrc/host/ckpt_io.cpp dlgm_cpu_adamw: AVX2/FMA, OpenMP)
     H2D  bf16 params chunk i-1
 so PCIe traffic in both directions overlaps the host update.
+
+NVMe ("nvme"): the three state files are swapped through ``buffer_count`` (reference default 4,
+``deepspeed_launcher.py:201``) host staging slots by the C++ AIO engine (csrc/host/aio.cpp, the
+DeepSpeed ``aio`` op's role): reads of chunk i+buffer_count-2 and the write-back of chunk i-1 are
+in flight while chunk i is updated, so host RAM holds only the ring, not the optimizer state. The
+files are also mapped (``master`` / ``exp_avg`` / ``exp_avg_sq`` tensors) for the cold paths --
+initialisation, checkpoint capture / restore, consolidation -- which share the page cache with
+the engine's buffered I/O and therefore always see the swapped state.
 """
 from __future__ import annotations
 
 import os
+import time
 from typing import List, Optional
 
 import torch
@@ -31,7 +40,8 @@ CHUNK_ELEMS = 32 << 20  # 128 MiB of fp32 gradient per staging slot
 
 class HostOffloadOptimizer:
     def __init__(self, numel: int, device: torch.device, kind: str = "cpu", nvme_path: Optional[str] = None,
-                 rank: int = 0, chunk_elems: int = CHUNK_ELEMS):
+                 rank: int = 0, chunk_elems: int = CHUNK_ELEMS, buffer_count: int = 4, aio_threads: int = 8,
+                 aio_block_size: int = 8 << 20):
         assert kind in ("cpu", "nvme"), kind
         if _host.lib() is None:
             raise RuntimeError("optimizer offload needs the host runtime (_dlgm_host.so); run build()")
@@ -39,11 +49,17 @@ class HostOffloadOptimizer:
         self.cuda = device.type == "cuda"
         self.chunk = max(1, min(chunk_elems, numel))
         self.files: List[str] = []
+        self.aio: Optional[_host.Aio] = None
         if kind == "nvme":
             root = nvme_path or os.environ.get("DLGM_NVME_PATH", "/tmp/dlgm_nvme")
             os.makedirs(root, exist_ok=True)
             self.master, self.exp_avg, self.exp_avg_sq = (self._mmap(root, rank, nm) for nm in
                                                           ("master", "exp_avg", "exp_avg_sq"))
+            self.aio = _host.Aio(aio_threads, aio_block_size)
+            self.fh = [self.aio.open(p, self.n * 4) for p in self.files]
+            self.nbuf = max(3, int(buffer_count))
+            self.sslot = [_host.aligned_empty(3 * self.chunk).view(3, self.chunk) for _ in range(self.nbuf)]
+            self.swap_stats = {"read_GiB": 0.0, "write_GiB": 0.0, "io_wait_s": 0.0}
         else:
             mk = lambda: torch.zeros(numel, dtype=torch.float32, pin_memory=self.cuda)  # noqa: E731
             self.master, self.exp_avg, self.exp_avg_sq = mk(), mk(), mk()
@@ -75,12 +91,14 @@ class HostOffloadOptimizer:
         bc1 = 1.0 - beta1 ** step
         bc2 = 1.0 - beta2 ** step
         hyper = (lr, beta1, beta2, eps, weight_decay, bc1, bc2, gscale)
-        if not self.cuda:
+        if not self.cuda and self.kind != "nvme":
             _host.cpu_adamw_(self.master, self.exp_avg, self.exp_avg_sq, grad_shard,
                              p16_shard if p16_shard.dtype == torch.bfloat16 else None, *hyper)
             if p16_shard.dtype != torch.bfloat16:
                 p16_shard.copy_(self.master)
             return
+        if self.kind == "nvme":
+            return self._step_swapped(grad_shard, p16_shard, hyper)
         chunks = [(off, min(self.chunk, self.n - off)) for off in range(0, self.n, self.chunk)]
         cur = torch.cuda.current_stream(self.device)
         s = self.stream
@@ -113,7 +131,90 @@ class HostOffloadOptimizer:
             h2d[slot] = ev
         cur.wait_stream(s)  # compute resumes on the updated bf16 params
 
+    def _step_swapped(self, grad_shard: torch.Tensor, p16_shard: torch.Tensor, hyper) -> None:
+        """NVMe: state chunks stream file -> ring slot -> AdamW -> file, reads running buffer_count-2
+        chunks ahead and writes draining behind; gradients / bf16 params move as in the host path."""
+        chunks = [(off, min(self.chunk, self.n - off)) for off in range(0, self.n, self.chunk)]
+        nb, ahead = self.nbuf, self.nbuf - 2
+        aio = self.aio
+        reads: dict = {}
+        writes: dict = {}
+        waited = 0.0
+
+        def wait_all(tickets) -> None:
+            nonlocal waited
+            t0 = time.perf_counter()
+            for tk in tickets:
+                aio.wait(tk)
+            waited += time.perf_counter() - t0
+
+        def issue_read(i: int) -> None:
+            if i - nb in writes:  # the slot's previous chunk must be on its way to the file first
+                wait_all(writes.pop(i - nb))
+            off, ln = chunks[i]
+            st = self.sslot[i % nb]
+            reads[i] = [aio.read(h, st[k, :ln], off * 4) for k, h in enumerate(self.fh)]
+
+        cuda = self.cuda
+        if cuda:
+            cur = torch.cuda.current_stream(self.device)
+            s = self.stream
+            s.wait_stream(cur)  # gradients final
+            d2h: List[Optional[torch.cuda.Event]] = [None] * len(chunks)
+            h2d: List[Optional[torch.cuda.Event]] = [None, None]
+
+            def issue_d2h(i: int) -> None:
+                off, ln = chunks[i]
+                with torch.cuda.stream(s):
+                    self.gslot[i % 2][:ln].copy_(grad_shard.narrow(0, off, ln), non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(s)
+                d2h[i] = ev
+
+            issue_d2h(0)
+        for i in range(min(ahead, len(chunks))):
+            issue_read(i)
+        for i, (off, ln) in enumerate(chunks):
+            if i + ahead < len(chunks):
+                issue_read(i + ahead)
+            if cuda and i + 1 < len(chunks):
+                issue_d2h(i + 1)
+            wait_all(reads.pop(i))
+            st = self.sslot[i % nb]
+            if cuda:
+                d2h[i].synchronize()
+                slot = i % 2
+                if h2d[slot] is not None:
+                    h2d[slot].synchronize()
+                g, p16 = self.gslot[slot][:ln], self.pslot[slot][:ln]
+            else:
+                g = grad_shard.narrow(0, off, ln)
+                p16 = p16_shard.narrow(0, off, ln) if p16_shard.dtype == torch.bfloat16 else None
+            _host.cpu_adamw_(st[0, :ln], st[1, :ln], st[2, :ln], g, p16, *hyper)
+            writes[i] = [aio.write(h, st[k, :ln], off * 4) for k, h in enumerate(self.fh)]
+            if cuda:
+                with torch.cuda.stream(s):
+                    p16_shard.narrow(0, off, ln).copy_(p16, non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(s)
+                h2d[slot] = ev
+            elif p16 is None:
+                p16_shard.narrow(0, off, ln).copy_(st[0, :ln])
+        for i in sorted(writes):
+            wait_all(writes.pop(i))  # the mapped views (checkpoint capture) read the page cache from here on
+        if cuda:
+            cur.wait_stream(s)
+        nbytes = self.n * 4 * 3 / 2 ** 30
+        self.swap_stats["read_GiB"] += nbytes
+        self.swap_stats["write_GiB"] += nbytes
+        self.swap_stats["io_wait_s"] += waited
+
     def close(self) -> None:
+        if self.aio is not None:
+            for h in self.fh:
+                self.aio.close(h)
+            self.aio.shutdown()
+            self.aio = None
         for p in self.files:
             try:
                 os.remove(p)

@@ -92,6 +92,9 @@ class EngineConfig:
     sequence_parallel_size: int = 1
     offload_optimizer: str = "none"  # none | cpu | nvme (ZeRO-Offload parity path: parallel/offload.py)
     nvme_path: Optional[str] = None
+    offload_buffer_count: int = 4  # NVMe swap ring slots (offload_optimizer.buffer_count)
+    aio_threads: int = 8  # C++ AIO engine: I/O threads (DeepSpeed aio thread_count x queue_depth)
+    aio_block_size: int = 8 << 20  # bytes per I/O piece (DeepSpeed aio block_size)
     wall_clock_breakdown: bool = False  # per-phase HIP-event timers (utils/timers.py)
     # parameter all-gathers on their own communicator (own RCCL stream), so a prefetch gather of the
     # next block and the reduce-scatter of the previous block's gradients run concurrently on xGMI
@@ -290,7 +293,10 @@ class ZeroEngine:
         self.offload = None
         if self.cfg.offload_optimizer in ("cpu", "nvme"):
             from .offload import HostOffloadOptimizer
-            self.offload = HostOffloadOptimizer(n, dev, self.cfg.offload_optimizer, self.cfg.nvme_path, self.rank)
+            self.offload = HostOffloadOptimizer(n, dev, self.cfg.offload_optimizer, self.cfg.nvme_path, self.rank,
+                                                buffer_count=self.cfg.offload_buffer_count,
+                                                aio_threads=self.cfg.aio_threads,
+                                                aio_block_size=self.cfg.aio_block_size)
             self.master, self.exp_avg, self.exp_avg_sq = (self.offload.master, self.offload.exp_avg,
                                                           self.offload.exp_avg_sq)
         else:

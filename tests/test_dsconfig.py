@@ -1,0 +1,42 @@
+"""DeepSpeed-schema JSON -> EngineConfig (engine/dsconfig.py): every key the reference's generator emits
+(``ai_engine/deepspeed_launcher.py:124-238``) lands on the engine knob that implements it."""
+import torch
+
+from distributed_llm_training_gpu_manager_amd.engine.dsconfig import engine_config_from_ds
+from distributed_llm_training_gpu_manager_amd.launcher.config import generate_config, presets
+
+
+def test_presets_map_onto_engine():
+    for name, pc in presets().items():
+        ds = generate_config(pc)
+        cfg, notes = engine_config_from_ds(ds, seq_len=4096)
+        zo = ds["zero_optimization"]
+        assert cfg.zero_stage == zo["stage"], name
+        assert cfg.micro_batch_size == ds["train_micro_batch_size_per_gpu"]
+        assert cfg.grad_accum == ds["gradient_accumulation_steps"]
+        assert cfg.grad_clip == ds["gradient_clipping"]
+        if zo["stage"] < 3:
+            continue
+        assert cfg.max_live_parameters == zo["stage3_max_live_parameters"]
+        assert cfg.max_reuse_distance == zo["stage3_max_reuse_distance"]
+        assert cfg.prefetch_bucket_size == zo["stage3_prefetch_bucket_size"]
+        off = zo.get("offload_optimizer", {})
+        assert cfg.offload_optimizer == off.get("device", "none")
+        if "buffer_count" in off:
+            assert cfg.offload_buffer_count == off["buffer_count"]
+        if zo.get("offload_param", {}).get("device", "none") != "none":
+            assert any("offload_param" in n for n in notes)
+
+
+def test_aio_and_mi355x_blocks():
+    ds = {"zero_optimization": {"stage": 2, "offload_optimizer": {"device": "nvme", "nvme_path": "/nvme",
+                                                                  "buffer_count": 6}},
+          "aio": {"block_size": 1 << 20, "queue_depth": 4, "thread_count": 2},
+          "communication_data_type": "fp16",
+          "mi355x": {"expert_parallel_size": 2, "sequence_parallel_size": 4, "comm_dtype": "fp32"}}
+    cfg, notes = engine_config_from_ds(ds, seq_len=1024)
+    assert (cfg.offload_optimizer, cfg.nvme_path, cfg.offload_buffer_count) == ("nvme", "/nvme", 6)
+    assert (cfg.aio_threads, cfg.aio_block_size) == (8, 1 << 20)
+    assert (cfg.expert_parallel_size, cfg.sequence_parallel_size) == (2, 4)
+    assert cfg.comm_dtype == torch.float32
+    assert any("A20" in n for n in notes)

@@ -29,3 +29,21 @@ def test_host_runtime_asan_ubsan(tmp_path):
     r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
     assert "self-test OK" in r.stdout
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no host C++ compiler")
+@pytest.mark.parametrize("san", ["address,undefined", "thread"])
+def test_aio_engine_sanitizers(tmp_path, san):
+    """The NVMe AIO engine (csrc/host/aio.cpp) under ASan+UBSan and under ThreadSanitizer (race detection
+    on the submit / worker / wait / destroy paths)."""
+    exe = str(tmp_path / "aio_selftest")
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", f"-fsanitize={san}",
+           "-fno-sanitize-recover=all", os.path.join(ROOT, "tests", "native", "aio_test.cpp"),
+           os.path.join(ROOT, "csrc", "host", "aio.cpp"), "-o", exe, "-lpthread"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    env = {**os.environ, "ASAN_OPTIONS": "detect_leaks=1:halt_on_error=1:verify_asan_link_order=0",
+           "UBSAN_OPTIONS": "print_stacktrace=1:halt_on_error=1", "TSAN_OPTIONS": "halt_on_error=1"}
+    r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    assert "aio self-test OK" in r.stdout
