@@ -46,6 +46,9 @@ def main() -> int:
     ap.add_argument("--live-params", default="hbm",
                     help="ZeRO-3 stage3_max_live_parameters: a number, or 'hbm' = sized to the GPU's memory")
     ap.add_argument("--reuse-distance", default="hbm", help="ZeRO-3 stage3_max_reuse_distance (number or 'hbm')")
+    ap.add_argument("--local-grads", default="hbm",
+                    help="ZeRO-2/3 gradient accumulation: 'hbm' (local fp32 + one reduce-scatter per step when the "
+                         "full gradient fits in 15%% of HBM), 'on', or 'off' (reduce-scatter every micro-batch)")
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="after the timed steps, trace this many extra steps with torch.profiler")
     ap.add_argument("--profile-dir", default="gpurun_out/torch_trace")
@@ -66,7 +69,8 @@ def main() -> int:
     ecfg = EngineConfig(zero_stage=args.zero, micro_batch_size=args.mbs, seq_len=args.seq, grad_accum=args.ga,
                         lr=3e-5, warmup_steps=100, total_steps=10000, grad_clip=1.0,
                         activation_checkpointing=args.ckpt, max_live_parameters=_knob(args.live_params),
-                        max_reuse_distance=_knob(args.reuse_distance))
+                        max_reuse_distance=_knob(args.reuse_distance),
+                        local_grad_accum={"on": True, "off": False}.get(args.local_grads, args.local_grads))
     t0 = time.time()
     eng = ZeroEngine(mcfg, ecfg, env.device, comm)
     if env.device.type == "cuda":
@@ -133,6 +137,7 @@ def main() -> int:
                 "activation_checkpointing": args.ckpt,
                 "stage3_max_live_parameters": args.live_params,
                 "stage3_max_reuse_distance": args.reuse_distance,
+                "grad_reduce_scatter": "per_step" if eng.local_grads else "per_micro_batch",
             },
             "extra": {
                 "tokens_per_sec_per_gpu": round(tps / env.world, 2),

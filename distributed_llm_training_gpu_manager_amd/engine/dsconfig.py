@@ -74,6 +74,8 @@ def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, **overri
     mi = ds.get("mi355x") or {}
     cfg.expert_parallel_size = int(mi.get("expert_parallel_size", cfg.expert_parallel_size))
     cfg.sequence_parallel_size = int(mi.get("sequence_parallel_size", cfg.sequence_parallel_size))
+    if "local_grad_accum" in mi:
+        cfg.local_grad_accum = mi["local_grad_accum"]
     if mi.get("comm_dtype"):
         cfg.comm_dtype = {"fp32": torch.float32, "float32": torch.float32}.get(mi["comm_dtype"], torch.bfloat16)
     for k, v in overrides.items():

@@ -20,7 +20,7 @@ from __future__ import annotations
 
 from datetime import datetime, timezone
 from enum import Enum
-from typing import Any, Dict, Optional
+from typing import Any, Dict, Optional, Union
 
 from pydantic import BaseModel, Field
 
@@ -55,6 +55,8 @@ class MI355XOptions(BaseModel):
     comm_dtype: Optional[str] = None
     expert_parallel_size: int = Field(default=1, ge=1)
     sequence_parallel_size: int = Field(default=1, ge=1, description="Ulysses sequence parallelism (long context)")
+    local_grad_accum: Union[bool, str] = Field(
+        default="hbm", description="ZeRO-2/3: fp32 grads accumulate locally, one reduce-scatter per step ('hbm': if they fit)")
 
 
 class DeepSpeedConfig(BaseModel):

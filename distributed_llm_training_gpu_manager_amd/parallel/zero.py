@@ -11,7 +11,8 @@ Storage (per rank; P = partition world = W for stages 1-3, 1 for stage 0)
     master, exp_avg, exp_avg_sq, grad_shard  fp32 [same]  -- ONE buffer each, so
                 the optimizer is one fused HIP launch with no host sync
     p16_full    bf16 [sum_g N_g]       stages 1-2 (persistent gathered params)
-    grad_full   fp32 [sum_g N_g]       stage 1 (local accumulation until the boundary)
+    grad_full   fp32 [sum_g N_g]       stage 1, and stages 2-3 with local_grad_accum (local
+                                       accumulation until the boundary)
 
 Buckets = units: every transformer block is one flat segment (Llama-3-8B:
 218 M params, 436 MB bf16; 70B: 856 M, 1.7 GB). That is the MI355X bucket policy
@@ -26,7 +27,14 @@ Schedule (one micro-batch)
               gradient partition (P == 1, ZeRO-0/1: "direct", GEMM beta = 1) or
               writes bf16 grads into a flat scratch segment that is async
               reduce-scattered(avg) (ZeRO-2/3, P > 1) with the fp32 accumulation
-              deferred by one unit so RCCL overlaps the next unit's backward
+              deferred by one unit so RCCL overlaps the next unit's backward.
+              With ``local_grad_accum`` (ZeRO-2/3, grad_accum > 1, default "hbm": when
+              a full fp32 gradient fits in 15 % of HBM -- Llama-3-8B: 32 GB of 288)
+              every micro-batch accumulates fp32 grads directly (like ZeRO-1) and
+              each unit is reduce-scattered ONCE per optimizer step, in comm_dtype,
+              overlapped with the last micro-batch's backward: 1/GA of DeepSpeed's
+              per-micro-batch gradient traffic (FSDP ``no_sync`` pattern); params
+              and optimizer state stay partitioned
     step    : grad_stats (sum g^2, #non-finite) -> all_reduce(2 floats) ->
               fused AdamW reading clip coef / overflow flag on device ->
               (stage 1/2) all-gather updated bf16 params
@@ -92,6 +100,11 @@ class EngineConfig:
     sequence_parallel_size: int = 1
     offload_optimizer: str = "none"  # none | cpu | nvme (ZeRO-Offload parity path: parallel/offload.py)
     nvme_path: Optional[str] = None
+    # ZeRO-2/3 gradients: True = accumulate fp32 locally and reduce-scatter once per optimizer step;
+    # False = reduce-scatter every micro-batch (DeepSpeed); "hbm" = True when GA > 1 and the full fp32
+    # gradient fits in local_grad_hbm_fraction of the device
+    local_grad_accum: Any = "hbm"
+    local_grad_hbm_fraction: float = 0.15
     offload_buffer_count: int = 4  # NVMe swap ring slots (offload_optimizer.buffer_count)
     aio_threads: int = 8  # C++ AIO engine: I/O threads (DeepSpeed aio thread_count x queue_depth)
     aio_block_size: int = 8 << 20  # bytes per I/O piece (DeepSpeed aio block_size)
@@ -311,8 +324,23 @@ class ZeroEngine:
             self.p16_full = self.p16_shard  # P == 1: shard == full
         elif self.stage in (1, 2):
             self.p16_full = torch.zeros(self.full_total, dtype=self.dtype, device=dev)
-        if self.stage == 1:
+        self.local_grads = self._want_local_grads()
+        if self.stage == 1 or self.local_grads:
             self.grad_full = torch.zeros(self.full_total, **f32)
+
+    def _want_local_grads(self) -> bool:
+        """ZeRO-2/3: accumulate fp32 gradients locally across micro-batches (one reduce-scatter per step)?"""
+        v = self.cfg.local_grad_accum
+        if self.stage not in (2, 3) or not any(g.P > 1 for g in self.groups):
+            return False
+        if isinstance(v, str):
+            if v not in ("hbm", "auto"):
+                raise ValueError(f"local_grad_accum must be a bool or 'hbm', got {v!r}")
+            if self.cfg.grad_accum <= 1 or not self.is_cuda:
+                return False
+            hbm = torch.cuda.get_device_properties(self.device).total_memory
+            return self.full_total * 4 <= self.cfg.local_grad_hbm_fraction * hbm
+        return bool(v)
 
     def _init_params(self) -> None:
         init_dev = self.cfg.init_device
@@ -441,7 +469,7 @@ class ZeroEngine:
         """
         if g.P == 1:
             return self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
-        if self.stage == 1:
+        if self.stage == 1 or self.local_grads:
             return self.grad_full.narrow(0, g.full_off, g.numel)
         return None
 
@@ -451,7 +479,15 @@ class ZeroEngine:
             # an expert sees the tokens of every EP rank, each scaled by 1/(its own tokens): divide by the
             # EP size so expert grads are the global mean like the dense grads (which are AVG-reduced)
             tgt.mul_(1.0 / self.ep_size)
-        if g.P > 1:  # ZeRO-1: reduce-scatter the local accumulator into this rank's shard
+        if g.P > 1 and self.local_grads and self.cfg.comm_dtype != tgt.dtype:
+            # ZeRO-2/3 local accumulation: one reduce-scatter per step in comm_dtype (half the bytes of
+            # fp32), then the shard is written (beta = 0) from the reduced chunk
+            src = tgt.to(self.cfg.comm_dtype)
+            out = torch.empty(g.shard_numel, dtype=src.dtype, device=self.device)
+            shard_tgt = self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
+            pending.append((g.comm.reduce_scatter(out, src, avg=True, async_op=True),
+                            (shard_tgt, out, 0.0, None, 1.0, src)))
+        elif g.P > 1:  # ZeRO-1 (or fp32 comm): reduce-scatter the local accumulator into this rank's shard
             out = self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
             pending.append((g.comm.reduce_scatter(out, tgt, avg=True, async_op=True), tgt))
         elif g.comm.world > 1:  # ZeRO-0: plain data parallel
@@ -489,7 +525,7 @@ class ZeroEngine:
             h, payload = pending.pop(0)
             h.wait()
             if isinstance(payload, tuple):
-                shard_tgt, out, beta, src, alpha = payload
+                shard_tgt, out, beta, src, alpha = payload[:5]  # payload[5]: input kept alive until here
                 ops.accumulate_(shard_tgt, out, alpha, beta)
                 if src is not None and src.dtype == self.dtype:
                     self._release_gbuf(src)

@@ -196,3 +196,40 @@ def test_comm_bench_gloo_world2(tmp_path):
         rows = json.load(f)
     assert {r["op"] for r in rows} == {"all_gather", "reduce_scatter", "all_reduce", "all_to_all"}
     assert all(r["busbw_GBps"] > 0 and r["world"] == 2 for r in rows)
+
+
+def _local_worker(rank, world, port, stage, local, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = _cfg(stage, 2, torch.bfloat16)
+    cfg.local_grad_accum = local
+    eng = ZeroEngine(get_config("llama-tiny"), cfg, torch.device("cpu"), Comm())
+    assert eng.local_grads == local and (eng.grad_full is not None) == local
+    losses, grads0 = [], None
+    for mbs in _data("llama-tiny", 2, 2 * world):
+        m = eng.train_step([(t[:, :-1], t[:, 1:]) for t in mbs[2 * rank:2 * rank + 2]])
+        losses.append(float(m["loss"]))
+        if grads0 is None:
+            grads0 = eng.full_grads()
+    params = eng.full_params()
+    if rank == 0:
+        torch.save({"params": params, "losses": losses, "grads0": grads0}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("stage", [2, 3])
+def test_local_grad_accum_world2_matches_single(tmp_path, stage):
+    """ZeRO-2/3 with local fp32 accumulation across GA micro-batches and ONE bf16 reduce-scatter per step
+    (local_grad_accum) == single-process GA=4 training, like the per-micro-batch reduce-scatter path."""
+    ref_eng = ZeroEngine(get_config("llama-tiny"), _cfg(stage, 4), torch.device("cpu"))
+    ref_grads0 = None
+    for mbs in _data("llama-tiny", 2, 4):
+        ref_eng.train_step([(t[:, :-1], t[:, 1:]) for t in mbs])
+        if ref_grads0 is None:
+            ref_grads0 = ref_eng.full_grads()
+    ref_params = ref_eng.full_params()
+    for local in (True, False):
+        out = str(tmp_path / f"l{int(local)}.pt")
+        mp.spawn(_local_worker, args=(2, _free_port(), stage, local, out), nprocs=2, join=True)
+        _compare(torch.load(out, weights_only=True), ref_params, ref_grads0, 2)

@@ -31,9 +31,9 @@ def _free_port() -> int:
     return port
 
 
-def _data(mc, steps):
+def _data(mc, steps, n=2):
     g = torch.Generator().manual_seed(23)
-    return [[torch.randint(0, mc.vocab_size, (2, 129), generator=g) for _ in range(2)] for _ in range(steps)]
+    return [[torch.randint(0, mc.vocab_size, (2, 129), generator=g) for _ in range(n)] for _ in range(steps)]
 
 
 def _cfg(stage, ga, live):
@@ -42,17 +42,19 @@ def _cfg(stage, ga, live):
                         max_reuse_distance=live)
 
 
-def _worker(rank, world, port, stage, live, out_path):
+def _worker(rank, world, port, stage, live, out_path, ga=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     mc = get_config("llama-tiny")
-    eng = ZeroEngine(mc, _cfg(stage, 1, live), dev, Comm())
+    eng = ZeroEngine(mc, _cfg(stage, ga, live), dev, Comm())
+    # ga > 1 on the GPU: the default local_grad_accum="hbm" turns on (one reduce-scatter per step)
+    assert eng.local_grads == (ga > 1 and stage in (2, 3))
     grads0 = None
-    for step in _data(mc, 3):
-        t = step[rank].to(dev)
-        eng.train_step([(t[:, :-1].contiguous(), t[:, 1:].contiguous())])
+    for step in _data(mc, 3, world * ga):
+        ts = [t.to(dev) for t in step[rank * ga:(rank + 1) * ga]]
+        eng.train_step([(t[:, :-1].contiguous(), t[:, 1:].contiguous()) for t in ts])
         if grads0 is None:
             grads0 = {k: v.float().cpu() for k, v in eng.full_grads().items()}
     torch.cuda.synchronize()
@@ -63,16 +65,17 @@ def _worker(rank, world, port, stage, live, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("stage,live", [(1, 1e9), (2, 1e9), (3, 0), (3, "hbm")])
-def test_two_ranks_on_one_gpu_match_single_process(tmp_path, stage, live):
+@pytest.mark.parametrize("stage,live,ga", [(1, 1e9, 1), (2, 1e9, 1), (3, 0, 1), (3, "hbm", 1), (2, 1e9, 2),
+                                           (3, "hbm", 2)])
+def test_two_ranks_on_one_gpu_match_single_process(tmp_path, stage, live, ga):
     out = str(tmp_path / "w2.pt")
-    mp.spawn(_worker, args=(2, _free_port(), stage, live, out), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), stage, live, out, ga), nprocs=2, join=True)
     got = torch.load(out, weights_only=True)
     dev = torch.device("cuda", 0)
     mc = get_config("llama-tiny")
-    eng = ZeroEngine(mc, _cfg(stage, 2, live), dev)
+    eng = ZeroEngine(mc, _cfg(stage, 2 * ga, live), dev)
     grads0 = None
-    for step in _data(mc, 3):
+    for step in _data(mc, 3, 2 * ga):
         eng.train_step([(t[:, :-1].contiguous().to(dev), t[:, 1:].contiguous().to(dev)) for t in step])
         if grads0 is None:
             grads0 = {k: v.float().cpu() for k, v in eng.full_grads().items()}

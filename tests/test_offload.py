@@ -60,9 +60,10 @@ def test_offload_nan_step_is_skipped():
 
 
 @pytest.mark.gpu
-def test_offload_matches_device_optimizer_gpu():
+@pytest.mark.parametrize("offload", ["cpu", "nvme"])
+def test_offload_matches_device_optimizer_gpu(tmp_path, offload):
     ref_l, ref_p, _ = _run("cuda", "none")
-    got_l, got_p, _ = _run("cuda", "cpu")
+    got_l, got_p, _ = _run("cuda", offload, tmp_path)
     for a, b in zip(ref_l, got_l):
         assert abs(a - b) < 2e-3 * max(1.0, abs(a)), (ref_l, got_l)
     for k, v in ref_p.items():
