@@ -52,6 +52,11 @@ at::Tensor dlgm_transpose(const at::Tensor& x, const c10::optional<at::Tensor>& 
 at::Tensor dlgm_embedding_fwd(const at::Tensor& table, const at::Tensor& ids);
 void dlgm_embedding_bwd_(at::Tensor grad, const at::Tensor& dy, const at::Tensor& sorted_ids, const at::Tensor& order);
 std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_router_topk(const at::Tensor& logits, int64_t k);
+// gemm_lt.hip
+int64_t dlgm_gemm_lt(at::Tensor out, const at::Tensor& a, const at::Tensor& b, double beta, int64_t algo_index);
+at::Tensor dlgm_gemm_lt_tune(const at::Tensor& out, const at::Tensor& a, const at::Tensor& b, double beta,
+                             int64_t n_heuristic, bool all_algos, int64_t reps);
+int64_t dlgm_gemm_lt_version();
 
 TORCH_LIBRARY(dlgm, m) {
   m.def("rmsnorm_fwd(Tensor x, Tensor? residual, Tensor w, float eps) -> (Tensor, Tensor, Tensor)");
@@ -72,6 +77,9 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("embedding_fwd(Tensor table, Tensor ids) -> Tensor");
   m.def("embedding_bwd_(Tensor(a!) grad, Tensor dy, Tensor sorted_ids, Tensor order) -> ()");
   m.def("router_topk(Tensor logits, int k) -> (Tensor, Tensor, Tensor)");
+  m.def("gemm_lt(Tensor(a!) out, Tensor a, Tensor b, float beta, int algo) -> int");
+  m.def("gemm_lt_tune(Tensor out, Tensor a, Tensor b, float beta, int n_heuristic, bool all_algos, int reps) -> Tensor");
+  m.def("gemm_lt_version() -> int", &dlgm_gemm_lt_version);
 }
 
 TORCH_LIBRARY_IMPL(dlgm, CUDA, m) {
@@ -93,4 +101,6 @@ TORCH_LIBRARY_IMPL(dlgm, CUDA, m) {
   m.impl("embedding_fwd", &dlgm_embedding_fwd);
   m.impl("embedding_bwd_", &dlgm_embedding_bwd_);
   m.impl("router_topk", &dlgm_router_topk);
+  m.impl("gemm_lt", &dlgm_gemm_lt);
+  m.impl("gemm_lt_tune", &dlgm_gemm_lt_tune);
 }

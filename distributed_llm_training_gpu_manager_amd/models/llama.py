@@ -28,7 +28,7 @@ from typing import Any, List, Optional, Tuple
 import torch
 
 from .. import ops
-from ..ops.gemm import dx_mm, grad_mm
+from ..ops.gemm import dx_mm, grad_mm, mm
 from ..parallel.sp import sp_attention_bwd, sp_attention_fwd
 from .common import ParamSpec, Params, StepContext, Unit
 from .config import ModelConfig
@@ -88,7 +88,7 @@ class LlamaBlock(Unit):
         T = B * S
         xa, xb = _as_pair(x_pair)
         hn1, x, rstd1 = ops.rmsnorm_fwd(xa, p["attn_norm"], c.norm_eps, residual=xb)
-        qkv = torch.mm(hn1, p["wqkv"].t())
+        qkv = mm(hn1, p["wqkv"].t())
         cos, sin = ctx.rope
         ops.rope_(qkv, cos, sin, c.n_heads + c.n_kv_heads, c.head_dim, S)  # SP: tables start at this chunk
         if ctx.sp_group is not None:
@@ -99,7 +99,7 @@ class LlamaBlock(Unit):
             q, k, v = self._split(qkv, B, S)
             attn, lse = ops.flash_attn_fwd(q, k, v, causal=True)
         attn2d = attn.view(T, c.n_heads * c.head_dim)
-        o = torch.mm(attn2d, p["wo"].t())
+        o = mm(attn2d, p["wo"].t())
         return (x, rstd1, hn1, qkv, attn, lse), o
 
     def _split(self, qkv: torch.Tensor, B: int, S: int):
@@ -140,9 +140,9 @@ class LlamaBlock(Unit):
         saved_attn, o = self.attn_forward(p, x_pair, ctx)
         x = saved_attn[0]
         hn2, h, rstd2 = ops.rmsnorm_fwd(x, p["mlp_norm"], c.norm_eps, residual=o)
-        gu = torch.mm(hn2, p["w_gate_up"].t())
+        gu = mm(hn2, p["w_gate_up"].t())
         a = ops.swiglu_fwd(gu)
-        d = torch.mm(a, p["w_down"].t())
+        d = mm(a, p["w_down"].t())
         return (h, d), (saved_attn, h, rstd2, hn2, gu, a)
 
     def backward(self, p: Params, g: Params, saved, dy: torch.Tensor, ctx: StepContext):
@@ -184,7 +184,7 @@ class LlamaHead(Unit):
         c = self.cfg
         xa, xb = _as_pair(x_pair)
         hn, x, rstd = ops.rmsnorm_fwd(xa, p["norm"], c.norm_eps, residual=xb)
-        logits = torch.mm(hn, p["lm_head"].t())
+        logits = mm(hn, p["lm_head"].t())
         labels = ctx.labels.reshape(-1)
         loss_rows, _ = ops.cross_entropy_fwd_bwd_(logits, labels, ctx.grad_scale)
         # logits now hold d(loss)/d(logits); keep them for backward

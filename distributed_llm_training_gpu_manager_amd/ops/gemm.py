@@ -7,6 +7,9 @@ instead of being rounded to bf16 and added by a separate pass.
 """
 from __future__ import annotations
 
+import json
+import os
+from pathlib import Path
 from typing import Optional
 
 import torch
@@ -17,6 +20,8 @@ from .._native import hip_ops, use_native
 # hipBLASLt on gfx950, bf16 x bf16 -> fp32 (measured, tools/probe_dw_layout2.py): both operands with
 # the reduction (token) dim strided ("NN", what dW = dy^T x is) ~1.0 PF; one operand K-contiguous
 # ~1.27 PF; both ~1.35 PF. The HIP transpose streams at ~4.5 TB/s.
+TUNED_DIR = Path(__file__).resolve().parent.parent / "tuned"
+
 _PF = {"NN": 1.0e15, "A": 1.27e15, "B": 1.27e15, "TN": 1.35e15}
 _TR_BW, _TR_LAT = 4.5e12, 8e-6
 
@@ -35,19 +40,32 @@ def _plan(a: torch.Tensor, b: torch.Tensor) -> str:
     return min(cost, key=cost.get)
 
 
+def _plannable(a: torch.Tensor, b: torch.Tensor) -> bool:
+    return (a.is_cuda and a.dtype == torch.bfloat16 and a.dim() == 2 and a.stride(0) == 1 and a.stride(1) != 1
+            and b.stride(-1) == 1 and a.shape[0] % 8 == 0 and a.shape[1] % 8 == 0 and b.shape[1] % 8 == 0)
+
+
+def apply_plan(a: torch.Tensor, b: torch.Tensor, plan: str):
+    """Make the operands the plan names K-contiguous (HIP transpose)."""
+    if plan in ("A", "TN"):
+        a = transpose(a.t())  # [N, T] contiguous
+    if plan in ("B", "TN"):
+        b = transpose(b).t()  # [T, K] view of a contiguous [K, T]
+    return a, b
+
+
 def grad_mm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, acc: bool) -> torch.Tensor:
     """out (+)= a @ b. `out` may be bf16 (scratch, acc must be False) or fp32 (direct accumulation).
 
     For the weight-gradient shape (a = dy.t() with dy [T, N] row-major, b = x [T, K] row-major) the
     operands whose transpose pays for itself are first made K-contiguous with the HIP transpose.
+    fp32 outputs on the GPU then go through hipBLASLt directly with a per-shape tuned solution
+    (:func:`lt_mm`).
     """
-    if out.is_cuda and a.dtype == torch.bfloat16 and a.dim() == 2 and a.stride(0) == 1 and a.stride(1) != 1 \
-            and b.stride(-1) == 1 and a.shape[0] % 8 == 0 and a.shape[1] % 8 == 0 and b.shape[1] % 8 == 0:
-        plan = _plan(a, b)
-        if plan in ("A", "TN"):
-            a = transpose(a.t())  # [N, T] contiguous
-        if plan in ("B", "TN"):
-            b = transpose(b).t()  # [T, K] view of a contiguous [K, T]
+    if out.is_cuda and _plannable(a, b):
+        a, b = apply_plan(a, b, _plan(a, b))
+    if out.is_cuda and lt_enabled() and lt_mm(out, a, b, acc):
+        return out
     if out.dtype == a.dtype:
         if acc:
             return torch.addmm(out, a, b, beta=1.0, out=out)
@@ -60,6 +78,55 @@ def grad_mm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, acc: bool) -> t
     if acc:
         return out.add_(r)
     return out.copy_(r)
+
+
+# ---------------------------------------------------------------------------------------------
+# hipBLASLt with per-shape solution choice (csrc/kernels/gemm_lt.hip) for the fp32-output dW GEMMs
+_LT: dict = {"table": None, "version": None, "timings": {}}
+
+
+def lt_enabled() -> bool:
+    return os.environ.get("DLGM_GEMM_LT", "1") != "0"
+
+
+def _lt_key(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, beta: float) -> str:
+    def lay(t):
+        return f"N{t.stride(0)}" if t.stride(1) == 1 else f"T{t.stride(1)}"
+    return (f"{a.shape[0]}x{b.shape[1]}x{a.shape[1]}:{lay(a)}:{lay(b)}:{str(out.dtype)[6:]}{out.stride(0)}"
+            f":beta{int(beta != 0)}")
+
+
+def _lt_table() -> dict:
+    """Tuned solution indices for this hipBLASLt build (tools/tune_gemm_lt.py), keyed by problem."""
+    if _LT["table"] is None:
+        ver = int(hip_ops().gemm_lt_version())
+        _LT["version"] = ver
+        _LT["table"] = {}
+        path = TUNED_DIR / f"gemm_lt_v{ver}.json"
+        if path.exists():
+            with open(path) as f:
+                _LT["table"].update(json.load(f).get("solutions", {}))
+    return _LT["table"]
+
+
+def lt_mm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, acc: bool) -> bool:
+    """out (+)= a @ b through hipBLASLt with the solution tuned for this exact problem, if the table
+    (tools/bench_gemm_lt.py --write) has one; False = not tuned, the caller takes the aten path."""
+    beta = 1.0 if acc else 0.0
+    idx = _lt_table().get(_lt_key(out, a, b, beta))
+    if idx is None or idx < 0:
+        return False
+    hip_ops().gemm_lt(out, a, b, beta, idx)
+    return True
+
+
+def mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a @ b for the forward / input-gradient GEMMs: tuned hipBLASLt solution when one is recorded."""
+    if a.is_cuda and a.dtype == torch.bfloat16 and lt_enabled():
+        out = torch.empty(a.shape[0], b.shape[1], dtype=a.dtype, device=a.device)
+        if lt_mm(out, a, b, False):
+            return out
+    return torch.mm(a, b)
 
 
 def grad_copy(out: torch.Tensor, src: torch.Tensor, acc: bool) -> None:
@@ -87,5 +154,5 @@ def dx_mm(dy: torch.Tensor, p: dict, name: str) -> torch.Tensor:
     dy @ (W^T)^T -- both operands K-contiguous, hipBLASLt's fastest layout on gfx950."""
     wt = p.get(name + ".T")
     if wt is not None:
-        return torch.mm(dy, wt.t())
-    return torch.mm(dy, p[name])
+        return mm(dy, wt.t())
+    return mm(dy, p[name])

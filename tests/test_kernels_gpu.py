@@ -270,6 +270,36 @@ def test_grad_mm_layouts(N, K, out_dtype):
             gemm._plan = orig
 
 
+@pytest.mark.parametrize("la,lb", [("N", "N"), ("N", "T"), ("T", "N"), ("T", "T")])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+def test_gemm_lt_layouts_and_tuning(la, lb, out_dtype):
+    """hipBLASLt direct GEMM (csrc/kernels/gemm_lt.hip): row-major / transposed-view operands with padded
+    leading dims, beta 0 and 1, heuristic default and every tuned candidate == fp32 reference."""
+    ops_ = _native.hip_ops()
+    torch.manual_seed(1)
+    M, N, K = 384, 640, 512
+
+    def make(r, c, lay):  # [r, c] logical, row-major with a padded stride, or a transposed view
+        if lay == "N":
+            return torch.randn(r, c + 8, dtype=torch.bfloat16, device=DEV)[:, :c]
+        return torch.randn(c, r + 8, dtype=torch.bfloat16, device=DEV)[:, :r].t()
+
+    a, b = make(M, K, la), make(K, N, lb)
+    ref = a.float() @ b.float()
+    out = torch.zeros(M, N, dtype=out_dtype, device=DEV)
+    idx = int(ops_.gemm_lt(out, a, b, 0.0, -1))
+    assert idx >= 0 and rel_err(out, ref) < 1e-2
+    if out_dtype == torch.float32:
+        ops_.gemm_lt(out, a, b, 1.0, -1)
+        assert rel_err(out, 2 * ref) < 1e-5 * 100
+    cands = ops_.gemm_lt_tune(out, a, b, 0.0, 8, False, 1)
+    assert cands.shape[0] >= 1 and bool((cands[1:, 1] >= cands[:-1, 1]).all())
+    for i in cands[:, 0].tolist():
+        o2 = torch.full_like(out, float("nan"))
+        assert int(ops_.gemm_lt(o2, a, b, 0.0, int(i))) == int(i)
+        assert rel_err(o2, ref) < 1e-2, i
+
+
 @pytest.mark.parametrize("D", [64, 4096])
 def test_embedding_fwd_bwd(D):
     """Row gather + sorted-run scatter-add (repeated ids, fp32 and bf16 gradient tables) vs torch."""

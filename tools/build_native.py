@@ -122,7 +122,7 @@ def build(jobs: int | None = None, verbose: bool = False, force: bool = False) -
     torch_flags = [*common, *(f"-I{p}" for p in tinc), f"-I{sysconfig.get_paths()['include']}",
                    f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM=1", "-DTORCH_API_INCLUDE_EXTENSION_H"]
     kern_src = sorted((CSRC / "kernels").glob("*.hip")) + [CSRC / "bindings.cpp"]
-    kern_ld = [f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", "-ltorch",
+    kern_ld = [f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", "-ltorch", "-lhipblaslt",
                f"-Wl,-rpath,{tlib}"]
     outs = [_build_lib("_dlgm_hip.so", kern_src, torch_flags, kern_ld, jobs, verbose, force)]
     host_src = sorted((CSRC / "host").glob("*.cpp"))
