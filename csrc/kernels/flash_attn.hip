@@ -79,6 +79,12 @@ __device__ __forceinline__ bf16x8 lds_read_b128(const bf16* base) {
   return *reinterpret_cast<const bf16x8*>(base);
 }
 
+// x of lane i ^ 32 (the other half-wave): one v_permlane32_swap instead of an LDS bpermute round trip
+__device__ __forceinline__ float swap_halves(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(__lane_id() < 32 ? r[1] : r[0]);
+}
+
 __device__ __forceinline__ bf16x4 lds_read_tr(const bf16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(p));
 }
@@ -263,7 +269,7 @@ __global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams p) 
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[u][i]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * p.scale_log2;
+    mx = fmaxf(mx, swap_halves(mx)) * p.scale_log2;
     // raise the reference max only when some row of the wave outgrew it by > 2^kRescaleLog2
     // (wave-uniform branch: the common case skips the O / l rescale entirely)
     if (__any(mx > m_run + kRescaleLog2)) {
@@ -315,21 +321,27 @@ __global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams p) 
   }
 
   // ---- epilogue: normalise, store O [b, q, hq, d] and LSE [b, hq, q]
-  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float l_tot = l_run + swap_halves(l_run);
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-  if (qcol < p.S) {
-    bf16* orow = p.o + (((int64_t)b * p.S + qcol) * p.Hq + hq) * D;
+  // Lane (r, h) holds columns 8k + 4h .. +3 of row r for each 8-column group k. One half-exchange
+  // (v_permlane32_swap) per dword of a group pair (k, k+1) leaves lanes h = 0 with columns
+  // 8k .. 8k+7 and lanes h = 1 with 8k+8 .. 8k+15: one 16-byte store per pair instead of two
+  // 8-byte stores (the tail is store-issue bound). Both lanes of a pair share the row, so the swap
+  // runs on all lanes and only the store is guarded.
+  bf16* orow = p.o + (((int64_t)b * p.S + qcol) * p.Hq + hq) * D;
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d = dt * 32 + 8 * g4 + 4 * h;
-        bf16x4 v = {(bf16)(o[dt][4 * g4 + 0] * inv), (bf16)(o[dt][4 * g4 + 1] * inv),
-                    (bf16)(o[dt][4 * g4 + 2] * inv), (bf16)(o[dt][4 * g4 + 3] * inv)};
-        *reinterpret_cast<bf16x4*>(orow + d) = v;
-      }
-    if (h == 0) p.lse[((int64_t)b * p.Hq + hq) * p.S + qcol] = (m_run + log2f(l_tot)) * kLn2;
+  for (int k = 0; k < 4 * DT; k += 2) {
+    const f32x16& oa = o[k >> 2];
+    const f32x16& ob = o[(k + 1) >> 2];
+    const int ja = 4 * (k & 3), jb = 4 * ((k + 1) & 3);
+    bf16x4 va = {(bf16)(oa[ja] * inv), (bf16)(oa[ja + 1] * inv), (bf16)(oa[ja + 2] * inv), (bf16)(oa[ja + 3] * inv)};
+    bf16x4 vb = {(bf16)(ob[jb] * inv), (bf16)(ob[jb + 1] * inv), (bf16)(ob[jb + 2] * inv), (bf16)(ob[jb + 3] * inv)};
+    uint2 a = __builtin_bit_cast(uint2, va), c = __builtin_bit_cast(uint2, vb);
+    const auto sx = __builtin_amdgcn_permlane32_swap(a.x, c.x, false, false);
+    const auto sy = __builtin_amdgcn_permlane32_swap(a.y, c.y, false, false);
+    if (qcol < p.S) *reinterpret_cast<uint4*>(orow + 8 * k + 8 * h) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
   }
+  if (qcol < p.S && h == 0) p.lse[((int64_t)b * p.Hq + hq) * p.S + qcol] = (m_run + log2f(l_tot)) * kLn2;
 }
 
 // ----------------------------------------------------------------------------------
