@@ -233,3 +233,58 @@ def test_local_grad_accum_world2_matches_single(tmp_path, stage):
         out = str(tmp_path / f"l{int(local)}.pt")
         mp.spawn(_local_worker, args=(2, _free_port(), stage, local, out), nprocs=2, join=True)
         _compare(torch.load(out, weights_only=True), ref_params, ref_grads0, 2)
+
+
+def _ckpt_worker(rank, world, port, save_dir, out_path):
+    from distributed_llm_training_gpu_manager_amd.ckpt.checkpoint import AsyncCheckpointer
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = ZeroEngine(get_config("llama-tiny"), _cfg(3, 1), torch.device("cpu"), Comm())
+    t = _data("llama-tiny", 1, world)[0][rank]
+    eng.train_step([(t[:, :-1], t[:, 1:])])
+    ck = AsyncCheckpointer(eng, save_dir)
+    ck.save(1, {"step": 1}, blocking=True)
+    ck.close()
+    full = eng.full_params()
+    if rank == 0:
+        torch.save(full, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_zero3_world2_checkpoint_offline_consolidation(tmp_path):
+    """Shards written by two ZeRO-3 ranks -> ckpt/zero_to_fp32 (no process group) == gathered parameters."""
+    from distributed_llm_training_gpu_manager_amd.ckpt import zero_to_fp32
+
+    out = str(tmp_path / "full.pt")
+    mp.spawn(_ckpt_worker, args=(2, _free_port(), str(tmp_path / "ck"), out), nprocs=2, join=True)
+    ref = torch.load(out, weights_only=True)
+    got = zero_to_fp32.consolidate(str(tmp_path / "ck"))
+    assert set(got) == set(ref)
+    for k, v in ref.items():
+        assert torch.equal(got[k], v.float()), k
+
+
+def _detail_worker(rank, world, port, stage, local):
+    # TORCH_DISTRIBUTED_DEBUG=DETAIL wraps the process group: every collective first cross-checks its
+    # op / shapes / dtypes across ranks, so an engine that issues collectives in a rank-dependent order
+    # or with mismatched buffers fails here instead of hanging on RCCL (SURVEY.md §5.2)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      TORCH_DISTRIBUTED_DEBUG="DETAIL")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    assert dist.get_debug_level() == dist.DebugLevel.DETAIL
+    cfg = _cfg(stage, 2, torch.bfloat16)
+    cfg.local_grad_accum = local
+    cfg.max_live_parameters, cfg.max_reuse_distance = 0, 0  # re-gather every visit: the most collectives
+    eng = ZeroEngine(get_config("llama-tiny"), cfg, torch.device("cpu"), Comm())
+    for mbs in _data("llama-tiny", 2, 2 * world):
+        eng.train_step([(t[:, :-1], t[:, 1:]) for t in mbs[2 * rank:2 * rank + 2]])
+    eng.full_params()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("stage,local", [(1, False), (2, True), (3, False), (3, True)])
+def test_collective_consistency_under_distributed_debug(stage, local):
+    mp.spawn(_detail_worker, args=(2, _free_port(), stage, local), nprocs=2, join=True)

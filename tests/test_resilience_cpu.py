@@ -160,3 +160,27 @@ def test_wall_clock_breakdown_timers():
     assert s["forward"]["count"] == 2 and s["backward+reduce"]["count"] == 2 and s["optimizer_step"]["count"] == 1
     assert all(v["total_ms"] > 0 for v in s.values())
     assert eng.timers.summary() == {}
+
+
+def test_zero_to_fp32_offline_consolidation(tmp_path):
+    """ckpt/zero_to_fp32.py rebuilds the full fp32 parameters from the shard files alone (no engine)."""
+    from distributed_llm_training_gpu_manager_amd.ckpt import zero_to_fp32
+
+    mc = get_config("llama-tiny")
+    eng = ZeroEngine(mc, EngineConfig(zero_stage=3, seq_len=32, init_device="cpu"), torch.device("cpu"))
+    eng.master.normal_()
+    eng.exp_avg.uniform_()
+    ck = AsyncCheckpointer(eng, str(tmp_path))
+    ck.save(5, {"step": 5}, blocking=True)
+    full = eng.full_params()
+    got = zero_to_fp32.consolidate(str(tmp_path))
+    assert set(got) == set(full)
+    for k, v in full.items():
+        assert torch.equal(got[k], v.float()), k
+    m1 = zero_to_fp32.consolidate(str(tmp_path), "global_step5", state="exp_avg")
+    assert all(torch.equal(m1[k], v) for k, v in eng._gather_flat(eng.exp_avg).items())
+    out = tmp_path / "w.safetensors"
+    assert zero_to_fp32.main([str(tmp_path), str(out), "--dtype", "bf16"]) == 0
+    from safetensors.torch import load_file
+    sd = load_file(str(out))
+    assert all(torch.equal(sd[k], v.to(torch.bfloat16)) for k, v in full.items())
