@@ -272,6 +272,7 @@ def _detail_worker(rank, world, port, stage, local):
     # or with mismatched buffers fails here instead of hanging on RCCL
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       TORCH_DISTRIBUTED_DEBUG="DETAIL")
+    dist.set_debug_level_from_env()  # the level is read at import; this process imported torch before the env
     dist.init_process_group("gloo", rank=rank, world_size=world)
     assert dist.get_debug_level() == dist.DebugLevel.DETAIL
     cfg = _cfg(stage, 2, torch.bfloat16)
