@@ -85,6 +85,29 @@ __device__ __forceinline__ float swap_halves(float x) {
   return __uint_as_float(__lane_id() < 32 ? r[1] : r[0]);
 }
 
+// Store one 32-row x D accumulator row block (lane (r, h) holds columns 8k + 4h .. +3 of row r for
+// each 8-column group k) as bf16, scaled. One half-exchange (v_permlane32_swap) per dword of a group
+// pair (k, k+1) leaves lanes h = 0 with columns 8k .. 8k+7 and lanes h = 1 with 8k+8 .. 8k+15: one
+// 16-byte store per pair instead of two 8-byte stores (the tail is store-issue bound). Both lanes of
+// a pair share the row, so the swap runs on all lanes and only the store is guarded by `valid`.
+template <int DT>
+__device__ __forceinline__ void store_rows_bf16(bf16* row, const f32x16 (&acc)[DT], float scale, int h, bool valid) {
+#pragma unroll
+  for (int k = 0; k < 4 * DT; k += 2) {
+    const f32x16& oa = acc[k >> 2];
+    const f32x16& ob = acc[(k + 1) >> 2];
+    const int ja = 4 * (k & 3), jb = 4 * ((k + 1) & 3);
+    bf16x4 va = {(bf16)(oa[ja] * scale), (bf16)(oa[ja + 1] * scale), (bf16)(oa[ja + 2] * scale),
+                 (bf16)(oa[ja + 3] * scale)};
+    bf16x4 vb = {(bf16)(ob[jb] * scale), (bf16)(ob[jb + 1] * scale), (bf16)(ob[jb + 2] * scale),
+                 (bf16)(ob[jb + 3] * scale)};
+    uint2 a = __builtin_bit_cast(uint2, va), c = __builtin_bit_cast(uint2, vb);
+    const auto sx = __builtin_amdgcn_permlane32_swap(a.x, c.x, false, false);
+    const auto sy = __builtin_amdgcn_permlane32_swap(a.y, c.y, false, false);
+    if (valid) *reinterpret_cast<uint4*>(row + 8 * k + 8 * h) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+  }
+}
+
 __device__ __forceinline__ bf16x4 lds_read_tr(const bf16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(p));
 }
@@ -323,24 +346,7 @@ __global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams p) 
   // ---- epilogue: normalise, store O [b, q, hq, d] and LSE [b, hq, q]
   const float l_tot = l_run + swap_halves(l_run);
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-  // Lane (r, h) holds columns 8k + 4h .. +3 of row r for each 8-column group k. One half-exchange
-  // (v_permlane32_swap) per dword of a group pair (k, k+1) leaves lanes h = 0 with columns
-  // 8k .. 8k+7 and lanes h = 1 with 8k+8 .. 8k+15: one 16-byte store per pair instead of two
-  // 8-byte stores (the tail is store-issue bound). Both lanes of a pair share the row, so the swap
-  // runs on all lanes and only the store is guarded.
-  bf16* orow = p.o + (((int64_t)b * p.S + qcol) * p.Hq + hq) * D;
-#pragma unroll
-  for (int k = 0; k < 4 * DT; k += 2) {
-    const f32x16& oa = o[k >> 2];
-    const f32x16& ob = o[(k + 1) >> 2];
-    const int ja = 4 * (k & 3), jb = 4 * ((k + 1) & 3);
-    bf16x4 va = {(bf16)(oa[ja] * inv), (bf16)(oa[ja + 1] * inv), (bf16)(oa[ja + 2] * inv), (bf16)(oa[ja + 3] * inv)};
-    bf16x4 vb = {(bf16)(ob[jb] * inv), (bf16)(ob[jb + 1] * inv), (bf16)(ob[jb + 2] * inv), (bf16)(ob[jb + 3] * inv)};
-    uint2 a = __builtin_bit_cast(uint2, va), c = __builtin_bit_cast(uint2, vb);
-    const auto sx = __builtin_amdgcn_permlane32_swap(a.x, c.x, false, false);
-    const auto sy = __builtin_amdgcn_permlane32_swap(a.y, c.y, false, false);
-    if (qcol < p.S) *reinterpret_cast<uint4*>(orow + 8 * k + 8 * h) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
-  }
+  store_rows_bf16<DT>(p.o + (((int64_t)b * p.S + qcol) * p.Hq + hq) * D, o, inv, h, qcol < p.S);
   if (qcol < p.S && h == 0) p.lse[((int64_t)b * p.Hq + hq) * p.S + qcol] = (m_run + log2f(l_tot)) * kLn2;
 }
 
@@ -560,23 +566,15 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
     tile(std::integral_constant<int, 0>{}, t);
     if (t + 1 < nqt) tile(std::integral_constant<int, 1>{}, t + 1);
   }
+  if (group == 1) {  // the lane-pair swaps of the widened store need every lane, in or out of range
+    store_rows_bf16<DT>(p.dk + ((int64_t)b * p.S + key) * p.dkv_ss + hk * D, dkt, p.scale, h, key < p.S);
+    store_rows_bf16<DT>(p.dv + ((int64_t)b * p.S + key) * p.dkv_ss + hk * D, dvt, 1.f, h, key < p.S);
+    return;
+  }
   if (key >= p.S) return;
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) dkt[dt] *= p.scale;
-  if (group == 1) {
-    bf16* dkr = p.dk + ((int64_t)b * p.S + key) * p.dkv_ss + hk * D;
-    bf16* dvr = p.dv + ((int64_t)b * p.S + key) * p.dkv_ss + hk * D;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d = dt * 32 + 8 * g4 + 4 * h;
-        *reinterpret_cast<bf16x4*>(dkr + d) = (bf16x4){(bf16)dkt[dt][4 * g4 + 0], (bf16)dkt[dt][4 * g4 + 1],
-                                                       (bf16)dkt[dt][4 * g4 + 2], (bf16)dkt[dt][4 * g4 + 3]};
-        *reinterpret_cast<bf16x4*>(dvr + d) = (bf16x4){(bf16)dvt[dt][4 * g4 + 0], (bf16)dvt[dt][4 * g4 + 1],
-                                                       (bf16)dvt[dt][4 * g4 + 2], (bf16)dvt[dt][4 * g4 + 3]};
-      }
-  } else {
+  {
     const int64_t off = ((((int64_t)hh * p.B + b) * p.S + key) * p.Hkv + hk) * D;
     float* dkr = p.dk_part + off;
     float* dvr = p.dv_part + off;
@@ -733,19 +731,7 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams p
     tile(std::integral_constant<int, 0>{}, t);
     if (t + 1 < nt) tile(std::integral_constant<int, 1>{}, t + 1);
   }
-  if (qcol < p.S) {
-    bf16* orow = p.dq + ((int64_t)b * p.S + qcol) * p.dq_ss + hq * D;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) dqt[dt] *= p.scale;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d = dt * 32 + 8 * g4 + 4 * h;
-        *reinterpret_cast<bf16x4*>(orow + d) = (bf16x4){(bf16)dqt[dt][4 * g4 + 0], (bf16)dqt[dt][4 * g4 + 1],
-                                                        (bf16)dqt[dt][4 * g4 + 2], (bf16)dqt[dt][4 * g4 + 3]};
-      }
-  }
+  store_rows_bf16<DT>(p.dq + ((int64_t)b * p.S + qcol) * p.dq_ss + hq * D, dqt, p.scale, h, qcol < p.S);
 }
 
 void check_qkv(const at::Tensor& t, const char* name) {
