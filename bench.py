@@ -49,6 +49,8 @@ def main() -> int:
     ap.add_argument("--local-grads", default="hbm",
                     help="ZeRO-2/3 gradient accumulation: 'hbm' (local fp32 + one reduce-scatter per step when the "
                          "full gradient fits in 15%% of HBM), 'on', or 'off' (reduce-scatter every micro-batch)")
+    ap.add_argument("--hip-graphs", action="store_true",
+                    help="replay the micro-batch loop as one captured HIP graph (1 GPU, dense models)")
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="after the timed steps, trace this many extra steps with torch.profiler")
     ap.add_argument("--profile-dir", default="gpurun_out/torch_trace")
@@ -70,7 +72,8 @@ def main() -> int:
                         lr=3e-5, warmup_steps=100, total_steps=10000, grad_clip=1.0,
                         activation_checkpointing=args.ckpt, max_live_parameters=_knob(args.live_params),
                         max_reuse_distance=_knob(args.reuse_distance),
-                        local_grad_accum={"on": True, "off": False}.get(args.local_grads, args.local_grads))
+                        local_grad_accum={"on": True, "off": False}.get(args.local_grads, args.local_grads),
+                        hip_graphs=args.hip_graphs)
     t0 = time.time()
     eng = ZeroEngine(mcfg, ecfg, env.device, comm)
     if env.device.type == "cuda":
@@ -138,6 +141,7 @@ def main() -> int:
                 "stage3_max_live_parameters": args.live_params,
                 "stage3_max_reuse_distance": args.reuse_distance,
                 "grad_reduce_scatter": "per_step" if eng.local_grads else "per_micro_batch",
+                "hip_graphs": eng._graph is not None,
             },
             "extra": {
                 "tokens_per_sec_per_gpu": round(tps / env.world, 2),

@@ -76,6 +76,8 @@ def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, **overri
     cfg.sequence_parallel_size = int(mi.get("sequence_parallel_size", cfg.sequence_parallel_size))
     if "local_grad_accum" in mi:
         cfg.local_grad_accum = mi["local_grad_accum"]
+    if "hip_graphs" in mi:
+        cfg.hip_graphs = bool(mi["hip_graphs"])
     if mi.get("comm_dtype"):
         cfg.comm_dtype = {"fp32": torch.float32, "float32": torch.float32}.get(mi["comm_dtype"], torch.bfloat16)
     for k, v in overrides.items():

@@ -111,6 +111,8 @@ class Trainer:
         self.ecfg.seq_len = args.seq_len // self.sp
         if getattr(args, "wall_clock_breakdown", False):
             self.ecfg.wall_clock_breakdown = True
+        if getattr(args, "hip_graphs", False):
+            self.ecfg.hip_graphs = True
         self.engine = ZeroEngine(self.mcfg, self.ecfg, self.env.device, self.comm)
         self.monitor = LossSpikeMonitor(MonitorConfig())
         self.trap = NanTrap(self.env.device, self.monitor)
@@ -257,6 +259,8 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--profile-dir", default="torch_trace")
     ap.add_argument("--sequence-parallel", type=int, default=0,
                     help="Ulysses sequence-parallel size: ranks of a group split each sequence")
+    ap.add_argument("--hip-graphs", action="store_true",
+                    help="replay each step's micro-batch loop as one captured HIP graph (single rank, dense)")
     a, unknown = ap.parse_known_args(argv)
     return a
 

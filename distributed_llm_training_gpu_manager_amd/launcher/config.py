@@ -57,6 +57,8 @@ class MI355XOptions(BaseModel):
     sequence_parallel_size: int = Field(default=1, ge=1, description="Ulysses sequence parallelism (long context)")
     local_grad_accum: Union[bool, str] = Field(
         default="hbm", description="ZeRO-2/3: fp32 grads accumulate locally, one reduce-scatter per step ('hbm': if they fit)")
+    hip_graphs: bool = Field(default=False, description="replay the micro-batch loop as one captured HIP graph "
+                             "(single rank, dense models)")
 
 
 class DeepSpeedConfig(BaseModel):

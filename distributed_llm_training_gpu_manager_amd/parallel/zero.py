@@ -117,6 +117,11 @@ class EngineConfig:
     # input-gradient GEMMs then run with both operands K-contiguous (refreshed once per optimizer step)
     transposed_weight_cache: bool = True
     init_device: str = "auto"  # "cpu" gives bit-identical init on any device (tests); auto: cpu below 1e9 params
+    # replay the GA micro-batches of a step (forward + backward + gradient accumulation) as ONE captured
+    # HIP graph: one launch instead of ~30 kernel launches per layer per micro-batch, for models whose
+    # step is launch-bound (GPT-2-small, small Llama). Needs a step with no collective and no host sync
+    # inside the micro-batch loop (single rank, dense model, no offload, bf16); otherwise eager.
+    hip_graphs: bool = False
     fp16: bool = False  # dynamic loss scaling path (reference fp16 block)
     loss_scale: float = 0.0  # 0 = dynamic
     initial_scale_power: int = 16
@@ -294,6 +299,8 @@ class ZeroEngine:
         self._gbuf_pool: Dict[int, List[torch.Tensor]] = {}
         self._act_offload = None
         self.fault_inject_nan = False  # fault injection: poison one gradient element on the next micro-step
+        self._graph: Optional[Dict[str, Any]] = None  # captured micro-batch loop (cfg.hip_graphs)
+        self._graph_state = "cold"  # cold -> warm (one eager step done) | failed (capture refused)
         from ..utils.timers import PhaseTimers
         self.timers = PhaseTimers(device, enabled=cfg.wall_clock_breakdown)
         self.hooks: List[Any] = []  # callables(engine, metrics) after each step (NaN trap, monitors)
@@ -718,10 +725,10 @@ class ZeroEngine:
         ``grad_norm``) -- nothing here synchronises with the host.
         """
         assert len(micro_batches) == self.cfg.grad_accum
-        self.loss_acc.zero_()
-        for i, (ids, labels) in enumerate(micro_batches):
-            loss = self.micro_step(ids, labels, first=(i == 0), last=(i == len(micro_batches) - 1))
-            self.loss_acc += loss.float()
+        if self.graph_capturable() and not self.fault_inject_nan:
+            self._graphed_micro_loop(micro_batches)
+        else:
+            self._micro_loop(micro_batches)
         out = self.optimizer_step()
         tokens = sum(int(ids.numel()) for ids, _ in micro_batches)
         metrics = {"loss": self.loss_acc / tokens, "grad_norm": self.stats[0].sqrt()
@@ -730,6 +737,68 @@ class ZeroEngine:
         for hk in self.hooks:
             hk(self, metrics)
         return metrics
+
+    def _micro_loop(self, micro_batches: Sequence[Tuple[torch.Tensor, torch.Tensor]]) -> None:
+        self.loss_acc.zero_()
+        for i, (ids, labels) in enumerate(micro_batches):
+            loss = self.micro_step(ids, labels, first=(i == 0), last=(i == len(micro_batches) - 1))
+            self.loss_acc += loss.float()
+
+    # ------------------------------------------------------------------ HIP graphs
+    def graph_capturable(self) -> bool:
+        """Is the micro-batch loop free of collectives and host synchronisation (so it can be captured)?
+
+        Single rank (every group P == 1: gradients land directly in the fp32 shard, no gather), dense
+        model (MoE dispatch sizes are read on the host), no optimizer / activation offload (host
+        copies), no fp16 loss scaler (its scale is a host float baked into the gradient scale), no
+        per-phase timers (host-side event bookkeeping)."""
+        c = self.cfg
+        return (c.hip_graphs and self.is_cuda and self.W == 1 and not self.has_experts and self.offload is None
+                and self.scaler is None and not c.cpu_checkpointing and not self.timers.enabled
+                and self.sp_size == 1 and self._graph_state != "failed")
+
+    def _graphed_micro_loop(self, micro_batches: Sequence[Tuple[torch.Tensor, torch.Tensor]]) -> None:
+        """Capture the micro-batch loop once per batch shape (after one eager warm-up step that creates
+        the library handles, hipBLASLt solutions and transposed-weight buffers), then replay it with the
+        new token ids copied into the captured input buffers.
+
+        The captured work writes only storage that outlives the graph (fp32 gradient shard, loss
+        accumulator, the transposed-weight cache -- refreshed inside the graph at every replay, since
+        its version is invalidated before the capture); activations live in the graph's private pool."""
+        key = tuple((tuple(i.shape), tuple(l.shape)) for i, l in micro_batches)
+        g = self._graph
+        if g is None or g["key"] != key:
+            if self._graph_state != "warm":  # first step of this shape: eager, creates lazy state
+                self._graph_state = "warm"
+                self._graph = None
+                self._micro_loop(micro_batches)
+                return
+            static = [(i.clone(), l.clone()) for i, l in micro_batches]
+            for gi in list(self._tcache):  # recompute the transposes inside the graph (stale each step)
+                self._tcache[gi] = (-1, self._tcache[gi][1])
+            self._graph = None
+            torch.cuda.synchronize(self.device)
+            torch.cuda.empty_cache()  # hand the eager step's cached activation blocks to the graph pool
+            graph = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(graph):
+                    self._micro_loop(static)
+            except Exception as e:  # an op that cannot be captured: stay eager for the rest of the run
+                self._graph_state = "failed"
+                self._tcache.clear()
+                import warnings
+                warnings.warn(f"HIP graph capture failed ({type(e).__name__}: {e}); running eagerly")
+                torch.cuda.synchronize(self.device)
+                self._micro_loop(micro_batches)
+                return
+            self._graph = {"key": key, "graph": graph, "static": static}
+            g = self._graph
+        for (si, sl), (ids, labels) in zip(g["static"], micro_batches):
+            if si.data_ptr() != ids.data_ptr():
+                si.copy_(ids, non_blocking=True)
+                sl.copy_(labels, non_blocking=True)
+        g["graph"].replay()
+        self._tcache = {gi: (self._pver, c) for gi, (_, c) in self._tcache.items()}
 
     # ------------------------------------------------------------------ helpers
     def full_params(self) -> Dict[str, torch.Tensor]:

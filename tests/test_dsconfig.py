@@ -39,5 +39,7 @@ def test_aio_and_mi355x_blocks():
     assert (cfg.aio_threads, cfg.aio_block_size) == (8, 1 << 20)
     assert (cfg.expert_parallel_size, cfg.sequence_parallel_size) == (2, 4)
     assert engine_config_from_ds({"mi355x": {"local_grad_accum": False}}, 64)[0].local_grad_accum is False
+    assert engine_config_from_ds({"mi355x": {"hip_graphs": True}}, 64)[0].hip_graphs is True
+    assert cfg.hip_graphs is False
     assert cfg.comm_dtype == torch.float32
     assert any("A20" in n for n in notes)
