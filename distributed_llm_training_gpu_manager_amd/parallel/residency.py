@@ -76,6 +76,12 @@ class ResidencyPlan:
         self.resident_groups = sorted(resident)
         self.resident_params = used
 
+    def held_through_step(self, gi: int) -> bool:
+        """Every visit of gathered group gi is kept: one all-gather per step, the copy stays put until the
+        optimizer step (what lets ZeRO-3 give it a transposed-weight cache, ZeroEngine._add_resident_tcache)."""
+        vs = [v for v, gis in enumerate(self.visits) if gi in gis]
+        return bool(vs) and all(self._keep.get((v, gi), False) for v in vs)
+
     def keep(self, v: int, gi: int, last_micro: bool) -> bool:
         """After the last micro-batch nothing survives a wrap: the optimizer step changes the parameters."""
         if not self._keep.get((v, gi), False):

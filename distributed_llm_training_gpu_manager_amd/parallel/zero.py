@@ -116,6 +116,9 @@ class EngineConfig:
     # keep W^T of the big 2-D weights while the compute copy is stationary (P == 1, ZeRO-0/1/2): the
     # input-gradient GEMMs then run with both operands K-contiguous (refreshed once per optimizer step)
     transposed_weight_cache: bool = True
+    # ZeRO-3 (P > 1): groups the residency plan holds gathered for the whole step get the W^T cache too,
+    # while the caches fit in this fraction of HBM (Llama-3-8B: 14 GiB)
+    tcache_hbm_fraction: float = 0.08
     init_device: str = "auto"  # "cpu" gives bit-identical init on any device (tests); auto: cpu below 1e9 params
     # replay the GA micro-batches of a step (forward + backward + gradient accumulation) as ONE captured
     # HIP graph: one launch instead of ~30 kernel launches per layer per micro-batch, for models whose
@@ -296,6 +299,8 @@ class ZeroEngine:
                 self._bwd_last_visit[gi] = min(si, self._bwd_last_visit.get(gi, si))
         self._live: Dict[int, Tuple[torch.Tensor, Handle]] = {}
         self._build_live_plan()
+        if cfg.transposed_weight_cache and self.stage == 3:
+            self._add_resident_tcache()
         self._gbuf_pool: Dict[int, List[torch.Tensor]] = {}
         self._act_offload = None
         self.fault_inject_nan = False  # fault injection: poison one gradient element on the next micro-step
@@ -441,6 +446,23 @@ class ZeroEngine:
         max_reuse = resolve_limit(self.cfg.max_reuse_distance, hbm, unbounded_for_hbm=True)
         gathered = [self.stage == 3 and g.P > 1 for g in self.groups]
         self.live_plan = ResidencyPlan(visits, [g.numel for g in self.groups], gathered, max_live, max_reuse)
+
+    def _add_resident_tcache(self) -> None:
+        """ZeRO-3, P > 1: a gathered group the residency plan holds through the whole step is as stationary
+        between optimizer steps as a ZeRO-1/2 weight, so its dX GEMMs get the cached W^T as well (built on
+        the first fetch after the step's all-gather, reused by every micro-batch). Without this a ZeRO-3
+        run on N > 1 GPUs would lose the K-contiguous dX layout the single-GPU run has."""
+        budget = (self.cfg.tcache_hbm_fraction * torch.cuda.get_device_properties(self.device).total_memory
+                  if self.is_cuda else math.inf)
+        used = 0
+        for g in self.groups:
+            if g.P == 1 or g.idx in self._tnames or not self.live_plan.held_through_step(g.idx):
+                continue
+            names = [(sp.name, tuple(sp.shape)) for sp in g.specs if sp.tcache and len(sp.shape) == 2]
+            nbytes = sum(shp[0] * shp[1] for _, shp in names) * self.p16_shard.element_size()
+            if names and used + nbytes <= budget:
+                self._tnames[g.idx] = names
+                used += nbytes
 
     def _after_visit(self, v: int, gis, last_micro: bool) -> None:
         """Drop the gathered copies the residency plan does not keep past visit v (ZeRO-3)."""

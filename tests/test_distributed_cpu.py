@@ -289,3 +289,43 @@ def _detail_worker(rank, world, port, stage, local):
 @pytest.mark.parametrize("stage,local", [(1, False), (2, True), (3, False), (3, True)])
 def test_collective_consistency_under_distributed_debug(stage, local):
     mp.spawn(_detail_worker, args=(2, _free_port(), stage, local), nprocs=2, join=True)
+
+
+def _tcache_worker(rank, world, port, on, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = _cfg(3, 2, torch.bfloat16)
+    cfg.transposed_weight_cache = on
+    eng = ZeroEngine(get_config("llama-tiny"), cfg, torch.device("cpu"), Comm())
+    # every gathered group is held through the step ('hbm' residency is unbounded on CPU), so every
+    # group with a 2-D compute weight gets the W^T cache under ZeRO-3 as well
+    assert bool(eng._tnames) == on
+    assert all(eng.live_plan.held_through_step(gi) for gi in eng._tnames)
+    losses = []
+    for mbs in _data("llama-tiny", 3, 2 * world):
+        m = eng.train_step([(t[:, :-1], t[:, 1:]) for t in mbs[2 * rank:2 * rank + 2]])
+        losses.append(float(m["loss"]))
+    if on:
+        assert eng.memory_report()["weight_T_cache_GiB"] > 0
+    params = eng.full_params()
+    if rank == 0:
+        torch.save({"params": params, "losses": losses}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_zero3_world2_resident_transposed_cache_is_transparent(tmp_path):
+    """ZeRO-3 on 2 ranks: dX through the W^T cache of the step-resident gathered weights (rebuilt after
+    every optimizer step's all-gather) trains like dX through the gathered W."""
+    res = {}
+    for on in (False, True):
+        out = str(tmp_path / f"t{int(on)}.pt")
+        mp.spawn(_tcache_worker, args=(2, _free_port(), on, out), nprocs=2, join=True)
+        res[on] = torch.load(out, weights_only=True)
+    assert res[False]["losses"][0] == res[True]["losses"][0]
+    for a, b in zip(res[False]["losses"], res[True]["losses"]):
+        assert abs(a - b) < 1e-3 * max(1.0, abs(a))
+    for k, v in res[False]["params"].items():
+        d = (res[True]["params"][k] - v).abs()
+        assert float(d.max()) <= 2 * 1e-2 * 3 + 1e-3, k
+        assert float((d > 1e-3).float().mean()) < 0.02, k
