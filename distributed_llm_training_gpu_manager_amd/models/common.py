@@ -133,7 +133,7 @@ class AutogradUnit(Unit):
                 if not ctx.grad_acc:
                     g[k].zero_()
             elif ctx.grad_acc:
-                g[k].add_(leaf.grad.to(g[k].dtype))
+                g[k].add_(leaf.grad)  # mixed-dtype in-place add: no separate bf16 -> fp32 copy kernel
             else:
                 g[k].copy_(leaf.grad)
         if isinstance(xin, torch.Tensor) and xin.requires_grad:

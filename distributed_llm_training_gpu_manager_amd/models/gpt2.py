@@ -17,6 +17,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import ops
+from ..ops.gemm import grad_copy, grad_mm, mm
 from .common import AutogradUnit, ParamSpec, Params, StepContext, Unit
 from .config import ModelConfig
 
@@ -93,27 +94,53 @@ class GPT2Block(AutogradUnit):
         return 3.0 * (2 * T * c.d_model * (4 * c.d_model + 2 * c.ffn_dim) + 2 * T * S * c.d_model)
 
 
-class GPT2Head(AutogradUnit):
+class GPT2Head(Unit):
+    """Final LayerNorm + (tied) LM head + the fused HIP cross-entropy (loss and dlogits in one pass,
+    like :class:`~.llama.LlamaHead`): no fp32 logits, no separate softmax forward/backward sweeps."""
+
     name = "head"
 
     def __init__(self, cfg: ModelConfig):
         self.cfg = cfg
 
-    def fwd(self, p: Params, x: torch.Tensor, ctx: StepContext) -> torch.Tensor:
-        c = self.cfg
-        h = F.layer_norm(x, (c.d_model,), p["ln_f_w"], p["ln_f_b"], c.norm_eps)
-        w = p["wte"] if c.tie_embeddings else p["lm_head"]
-        logits = F.linear(h, w).float()
-        return F.cross_entropy(logits, ctx.labels.reshape(-1), reduction="sum") * ctx.grad_scale
+    def _w(self, p: Params) -> torch.Tensor:
+        return p["wte"] if self.cfg.tie_embeddings else p["lm_head"]
 
     def forward(self, p: Params, x, ctx: StepContext):
-        with torch.no_grad():
-            y = self.fwd(p, x, ctx)
-        return y / ctx.grad_scale, x
+        c = self.cfg
+        h = F.layer_norm(x, (c.d_model,), p["ln_f_w"], p["ln_f_b"], c.norm_eps).reshape(-1, c.d_model)
+        w = self._w(p)
+        V = w.shape[0]
+        if V % 8:  # the CE kernel wants a 16-byte row stride: logits live in a padded buffer
+            logits = torch.empty(h.shape[0], V + (-V) % 8, dtype=h.dtype, device=h.device)[:, :V]
+            torch.mm(h, w.t(), out=logits)
+        else:
+            logits = mm(h, w.t())
+        loss_rows, _ = ops.cross_entropy_fwd_bwd_(logits, ctx.labels.reshape(-1), ctx.grad_scale)
+        # logits now hold d(loss)/d(logits) (scaled by grad_scale); keep them for backward
+        return loss_rows.sum(), (x, logits)
 
     def backward(self, p: Params, g: Params, saved, dy, ctx: StepContext):
-        # first backward visit of the tied group: overwrite wte/ln_f grads (embed adds later)
-        return super().backward(p, g, saved, None, ctx)
+        # first backward visit of the tied group: write (or, under accumulation, add) d(wte) / d(ln_f);
+        # the embedding's visit adds later
+        c = self.cfg
+        x, dlogits = saved
+        lw = p["ln_f_w"].detach().requires_grad_(True)
+        lb = p["ln_f_b"].detach().requires_grad_(True)
+        xin = x.detach().requires_grad_(True)
+        with torch.enable_grad():
+            h = F.layer_norm(xin, (c.d_model,), lw, lb, c.norm_eps)
+        wname = "wte" if c.tie_embeddings else "lm_head"
+        grad_mm(g[wname], dlogits.t(), h.detach().reshape(-1, c.d_model), ctx.grad_acc)
+        dh = torch.mm(dlogits, self._w(p))
+        h.backward(dh.view_as(h))
+        for k, leaf in (("ln_f_w", lw), ("ln_f_b", lb)):
+            grad_copy(g[k], leaf.grad, ctx.grad_acc)
+        if not ctx.grad_acc:
+            g["wpe"].zero_()  # the embedding's visit accumulates into it
+            if not c.tie_embeddings:
+                g["wte"].zero_()
+        return xin.grad
 
     def flops(self, ctx: StepContext) -> float:
         return 3.0 * 2 * ctx.tokens * self.cfg.d_model * self.cfg.vocab_size

@@ -83,3 +83,25 @@ def llama_loss(params: Dict[str, torch.Tensor], cfg: ModelConfig, ids: torch.Ten
     hn = _rms(x, params["head.norm"], cfg.norm_eps)
     logits = hn @ params["head.lm_head"].t()
     return F.cross_entropy(logits.float(), labels.reshape(-1))
+
+
+def gpt2_loss(params: Dict[str, torch.Tensor], cfg: ModelConfig, ids: torch.Tensor,
+              labels: torch.Tensor) -> torch.Tensor:
+    """Plain fp32 GPT-2 (pre-LN, GELU-tanh, tied or untied LM head) for the engine's numerics tests."""
+    B, S = ids.shape
+    H, D = cfg.n_heads, cfg.d_model
+    hd = D // H
+    pos = torch.arange(S).repeat(B)
+    x = params["ends.wte"][ids.reshape(-1)] + params["ends.wpe"][pos]
+    for i in range(cfg.n_layers):
+        pre = f"layer{i}."
+        h = F.layer_norm(x, (D,), params[pre + "ln1_w"], params[pre + "ln1_b"], cfg.norm_eps)
+        qkv = (h @ params[pre + "attn_w"].t() + params[pre + "attn_b"]).view(B, S, 3, H, hd)
+        a = _attn(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]).reshape(B * S, D)
+        x = x + a @ params[pre + "proj_w"].t() + params[pre + "proj_b"]
+        h = F.layer_norm(x, (D,), params[pre + "ln2_w"], params[pre + "ln2_b"], cfg.norm_eps)
+        h = F.gelu(h @ params[pre + "fc_w"].t() + params[pre + "fc_b"], approximate="tanh")
+        x = x + h @ params[pre + "out_w"].t() + params[pre + "out_b"]
+    h = F.layer_norm(x, (D,), params["ends.ln_f_w"], params["ends.ln_f_b"], cfg.norm_eps)
+    w = params["ends.wte"] if cfg.tie_embeddings else params["ends.lm_head"]
+    return F.cross_entropy((h @ w.t()).float(), labels.reshape(-1))

@@ -3,7 +3,7 @@ import pytest
 import torch
 
 from distributed_llm_training_gpu_manager_amd.models import get_config
-from distributed_llm_training_gpu_manager_amd.models.reference import llama_loss
+from distributed_llm_training_gpu_manager_amd.models.reference import gpt2_loss, llama_loss
 from distributed_llm_training_gpu_manager_amd.parallel.zero import EngineConfig, ZeroEngine
 
 
@@ -32,8 +32,11 @@ def _check(device: str, model: str = "llama-tiny", tol: float = 5e-2):
     g = torch.Generator().manual_seed(3)
     toks = [torch.randint(0, mc.vocab_size, (2, 65), generator=g) for _ in range(2)]
     mbs = [(t[:, :-1].to(device), t[:, 1:].to(device)) for t in toks]
-    cos, sin = (t.cpu() for t in eng.rope)
-    ref_loss = sum(llama_loss(params, mc, t[:, :-1], t[:, 1:], cos, sin) for t in toks) / 2
+    if mc.arch == "gpt2":
+        ref_loss = sum(gpt2_loss(params, mc, t[:, :-1], t[:, 1:]) for t in toks) / 2
+    else:
+        cos, sin = (t.cpu() for t in eng.rope)
+        ref_loss = sum(llama_loss(params, mc, t[:, :-1], t[:, 1:], cos, sin) for t in toks) / 2
     ref_loss.backward()
     loss_acc = torch.zeros((), device=device)
     for i, (ids, lab) in enumerate(mbs):
@@ -50,6 +53,12 @@ def _check(device: str, model: str = "llama-tiny", tol: float = 5e-2):
 
 def test_llama_manual_backward_matches_autograd_cpu():
     _check("cpu")
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_gpt2_engine_backward_matches_autograd(device):
+    # tied wte: LM-head dW (fused HIP cross-entropy dlogits) + embedding scatter-add into one segment
+    _check(device, "gpt2-tiny")
 
 
 def test_mixtral_manual_backward_matches_autograd_cpu():
