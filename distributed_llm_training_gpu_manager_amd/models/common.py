@@ -108,26 +108,51 @@ def init_param(spec: ParamSpec, out: torch.Tensor, gen: torch.Generator, seed: i
 
 
 class AutogradUnit(Unit):
-    """Unit whose backward is derived by autograd (recomputes its forward in backward)."""
+    """Unit whose backward is derived by autograd.
+
+    ``keep_graph = False``: the forward runs without a graph and the backward recomputes it (minimum
+    activation memory). ``keep_graph = True``: the forward records the autograd graph, so its saved
+    activations (and the gathered parameter views it references) live until the backward, which then
+    only runs the backward kernels -- no second forward. The engine's activation checkpointing still
+    applies on top: a checkpointed unit is re-run by the engine right before its backward.
+    """
+
+    keep_graph = False
 
     def fwd(self, p: Params, x: Any, ctx: StepContext) -> Any:
         raise NotImplementedError
 
+    @staticmethod
+    def _leaves(p: Params, x: Any):
+        leaves = {k: v.detach().requires_grad_(True) for k, v in p.items()}
+        xin = x.detach().requires_grad_(x.is_floating_point()) if isinstance(x, torch.Tensor) else x
+        return leaves, xin
+
     def forward(self, p: Params, x: Any, ctx: StepContext):
+        if self.keep_graph and torch.is_tensor(x):
+            leaves, xin = self._leaves(p, x)
+            with torch.enable_grad():
+                y = self.fwd(leaves, xin, ctx)
+            return y.detach(), ("graph", leaves, xin, y)
         with torch.no_grad():
             y = self.fwd(p, x, ctx)
         return y, x
 
     def backward(self, p: Params, g: Params, saved: Any, dy: Any, ctx: StepContext):
-        x = saved
-        leaves = {k: v.detach().requires_grad_(True) for k, v in p.items()}
-        xin = x.detach().requires_grad_(x.is_floating_point()) if isinstance(x, torch.Tensor) else x
-        with torch.enable_grad():
-            y = self.fwd(leaves, xin, ctx)
+        if isinstance(saved, tuple) and len(saved) == 4 and saved[0] == "graph":
+            _, leaves, xin, y = saved
             if dy is None:  # loss unit
                 y.backward()
             else:
                 y.backward(dy)
+        else:
+            leaves, xin = self._leaves(p, saved)
+            with torch.enable_grad():
+                y = self.fwd(leaves, xin, ctx)
+                if dy is None:  # loss unit
+                    y.backward()
+                else:
+                    y.backward(dy)
         for k, leaf in leaves.items():
             if leaf.grad is None:
                 if not ctx.grad_acc:

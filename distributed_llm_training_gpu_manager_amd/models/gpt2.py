@@ -1,7 +1,7 @@
 """GPT-2 family (BASELINE config 1: GPT-2-small ZeRO-1 plumbing run, CPU/gloo).
 
-Blocks are :class:`AutogradUnit` s (LayerNorm / GELU are not on the MI355X
-headline path); attention still goes through :mod:`ops.attention`, i.e. the HIP
+Blocks are :class:`AutogradUnit` s that keep their autograd graph from the forward
+(LayerNorm / GELU are not on the MI355X headline path); attention still goes through :mod:`ops.attention`, i.e. the HIP
 flash kernel on the GPU (head_dim 64 instance) and the fp32 reference on CPU.
 
 Tied input/output embeddings: the embedding table is ONE parameter group that
@@ -60,6 +60,8 @@ class GPT2Embed(Unit):
 
 
 class GPT2Block(AutogradUnit):
+    keep_graph = True  # GPT-2-small activations are small: save them instead of re-running the forward
+
     def __init__(self, cfg: ModelConfig, layer: int):
         self.cfg = cfg
         self.name = f"layer{layer}"

@@ -196,3 +196,24 @@ def test_hip_graph_replay_matches_eager_gpu(model, stage):
         assert abs(a - b) <= 1e-4 * max(1.0, abs(b)), (lg, le)
     err = float((eg.master - ee.master).abs().max() / ee.master.abs().max())
     assert err < 1e-4, err
+
+
+def test_gpt2_kept_graph_matches_activation_checkpointing_cpu():
+    """GPT-2 blocks keep their forward autograd graph; with activation checkpointing the engine re-runs
+    the block right before its backward instead. Both must train identically."""
+    mc = get_config("gpt2-tiny")
+    res = {}
+    for ck in (False, True):
+        ec = EngineConfig(zero_stage=3, micro_batch_size=2, seq_len=64, grad_accum=2, lr=1e-2, scheduler="constant",
+                          init_device="cpu", activation_checkpointing=ck)
+        eng = ZeroEngine(mc, ec, torch.device("cpu"))
+        g = torch.Generator().manual_seed(1)
+        losses = []
+        for _ in range(3):
+            mbs = []
+            for _ in range(2):
+                t = torch.randint(0, mc.vocab_size, (2, 65), generator=g)
+                mbs.append((t[:, :-1], t[:, 1:]))
+            losses.append(float(eng.train_step(mbs)["loss"]))
+        res[ck] = losses
+    assert res[False] == res[True], res
