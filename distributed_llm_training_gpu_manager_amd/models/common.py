@@ -107,6 +107,19 @@ def init_param(spec: ParamSpec, out: torch.Tensor, gen: torch.Generator, seed: i
         out.normal_(0.0, spec.std, generator=gen)
 
 
+def _store_grad(dst: torch.Tensor, src: torch.Tensor, acc: bool) -> None:
+    """dst (+)= src. fp32 targets on the GPU take the HIP accumulate kernel (one pass, bf16 or fp32 source:
+    torch's mixed-dtype add runs ~3x slower and the cast-then-add pair costs two passes)."""
+    if (dst.is_cuda and dst.dtype == torch.float32 and src.dtype in (torch.bfloat16, torch.float32)
+            and dst.is_contiguous() and src.is_contiguous() and dst.data_ptr() % 16 == 0 and src.data_ptr() % 16 == 0):
+        from ..ops.optim import accumulate_
+        accumulate_(dst, src.reshape(dst.shape), 1.0, 1.0 if acc else 0.0)
+    elif acc:
+        dst.add_(src.to(dst.dtype))
+    else:
+        dst.copy_(src)
+
+
 class AutogradUnit(Unit):
     """Unit whose backward is derived by autograd.
 
@@ -157,10 +170,8 @@ class AutogradUnit(Unit):
             if leaf.grad is None:
                 if not ctx.grad_acc:
                     g[k].zero_()
-            elif ctx.grad_acc:
-                g[k].add_(leaf.grad)  # mixed-dtype in-place add: no separate bf16 -> fp32 copy kernel
             else:
-                g[k].copy_(leaf.grad)
+                _store_grad(g[k], leaf.grad, ctx.grad_acc)
         if isinstance(xin, torch.Tensor) and xin.requires_grad:
             return xin.grad
         return None

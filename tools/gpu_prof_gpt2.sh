@@ -2,8 +2,8 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out/prof_gpt2
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_gpt2 -o run -- \
-    python -u bench.py --model gpt2-small --seq 1024 --mbs 8 --ga 4 --zero 1 --steps 5 --warmup 2 \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_gpt2 -o run -- \
+    python -u bench.py --model gpt2-small --seq 1024 --mbs 8 --ga 4 --zero 1 --steps 5 --warmup 2 ${GPT2_ARGS:-} \
     > gpurun_out/prof_gpt2/bench.log 2>&1
 rc=$?
 f=$(find gpurun_out/prof_gpt2 -name '*kernel_stats.csv' | head -1)
