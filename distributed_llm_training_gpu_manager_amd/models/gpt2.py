@@ -83,8 +83,8 @@ class GPT2Block(AutogradUnit):
         c = self.cfg
         B, S, H, hd = ctx.batch, ctx.seq_len, c.n_heads, c.head_dim
         h = F.layer_norm(x, (c.d_model,), p["ln1_w"], p["ln1_b"], c.norm_eps)
-        qkv = F.linear(h, p["attn_w"], p["attn_b"]).view(B, S, 3, H, hd)
-        a = ops.flash_attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal=True)
+        qkv = F.linear(h, p["attn_w"], p["attn_b"])  # [B*S, 3*D]: q | k | v per token
+        a = ops.flash_attention_qkv(qkv, B, S, H, H, hd, causal=True)  # one packed dqkv in backward
         x = x + F.linear(a.reshape(B * S, c.d_model), p["proj_w"], p["proj_b"])
         h = F.layer_norm(x, (c.d_model,), p["ln2_w"], p["ln2_b"], c.norm_eps)
         h = F.gelu(F.linear(h, p["fc_w"], p["fc_b"]), approximate="tanh")

@@ -119,3 +119,39 @@ class FlashAttentionFunction(torch.autograd.Function):
 
 def flash_attention(q, k, v, causal: bool = True, softmax_scale: Optional[float] = None):
     return FlashAttentionFunction.apply(q, k, v, causal, softmax_scale)
+
+
+def _split_qkv(qkv: torch.Tensor, B: int, S: int, hq: int, hkv: int, d: int):
+    f = qkv.view(B, S, -1)
+    return (f[..., :hq * d].unflatten(2, (hq, d)), f[..., hq * d:(hq + hkv) * d].unflatten(2, (hkv, d)),
+            f[..., (hq + hkv) * d:].unflatten(2, (hkv, d)))
+
+
+class FlashAttentionQKVFunction(torch.autograd.Function):
+    """Attention over a packed QKV projection output [B*S, (Hq+2Hkv)*D]. The backward writes dq/dk/dv
+    straight into ONE packed gradient (the layout the QKV GEMM's backward reads), so autograd does
+    not build three zero-filled slice gradients and add them up."""
+
+    @staticmethod
+    def forward(ctx, qkv, B, S, hq, hkv, d, causal, scale):
+        q, k, v = _split_qkv(qkv, B, S, hq, hkv, d)
+        out, lse = flash_attn_fwd(q, k, v, scale, causal)
+        ctx.save_for_backward(qkv, out, lse)
+        ctx.meta = (B, S, hq, hkv, d, causal, scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse = ctx.saved_tensors
+        B, S, hq, hkv, d, causal, scale = ctx.meta
+        q, k, v = _split_qkv(qkv, B, S, hq, hkv, d)
+        dqkv = torch.empty(qkv.shape, dtype=qkv.dtype, device=qkv.device)
+        flash_attn_bwd(dout.contiguous(), q, k, v, out, lse, scale, causal, dqkv=dqkv)
+        return dqkv, None, None, None, None, None, None, None
+
+
+def flash_attention_qkv(qkv: torch.Tensor, batch: int, seq: int, n_heads: int, n_kv_heads: int, head_dim: int,
+                        causal: bool = True, softmax_scale: Optional[float] = None) -> torch.Tensor:
+    """out [B, S, Hq, D] = attention(q, k, v) with q|k|v packed per token in a contiguous [B*S, (Hq+2Hkv)*D]."""
+    assert qkv.is_contiguous() and qkv.shape == (batch * seq, (n_heads + 2 * n_kv_heads) * head_dim), qkv.shape
+    return FlashAttentionQKVFunction.apply(qkv, batch, seq, n_heads, n_kv_heads, head_dim, causal, softmax_scale)

@@ -217,3 +217,27 @@ def test_gpt2_kept_graph_matches_activation_checkpointing_cpu():
             losses.append(float(eng.train_step(mbs)["loss"]))
         res[ck] = losses
     assert res[False] == res[True], res
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("hq,hkv,d", [(4, 4, 64), (8, 2, 128)])
+def test_packed_qkv_attention_matches_fp32_reference(device, hq, hkv, d):
+    """flash_attention_qkv (one packed dqkv from the HIP backward) == fp32 autograd attention."""
+    from distributed_llm_training_gpu_manager_amd.models.reference import _attn
+    from distributed_llm_training_gpu_manager_amd.ops import flash_attention_qkv
+
+    B, S = 2, 256
+    g = torch.Generator().manual_seed(4)
+    qkv32 = torch.randn(B * S, (hq + 2 * hkv) * d, generator=g)
+    dout = torch.randn(B, S, hq, d, generator=g)
+    x = qkv32.to(device=device, dtype=torch.bfloat16).requires_grad_(True)
+    out = flash_attention_qkv(x, B, S, hq, hkv, d)
+    out.backward(dout.to(device=device, dtype=torch.bfloat16))
+    r = qkv32.clone().requires_grad_(True)
+    f = r.view(B, S, -1)
+    ref = _attn(f[..., :hq * d].unflatten(2, (hq, d)), f[..., hq * d:(hq + hkv) * d].unflatten(2, (hkv, d)),
+                f[..., (hq + hkv) * d:].unflatten(2, (hkv, d)))
+    ref.backward(dout)
+    assert float((out.float().cpu() - ref).abs().max()) < 3e-2
+    err = float((x.grad.float().cpu() - r.grad).abs().max() / r.grad.abs().max())
+    assert err < 3e-2, err
