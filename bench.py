@@ -54,6 +54,9 @@ def main() -> int:
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="after the timed steps, trace this many extra steps with torch.profiler")
     ap.add_argument("--profile-dir", default="gpurun_out/torch_trace")
+    ap.add_argument("--n-layers", type=int, default=0,
+                    help="override the preset's layer count (kernel profiling of big models on one GPU only; "
+                         "the headline always runs the full preset)")
     args = ap.parse_args()
 
     from distributed_llm_training_gpu_manager_amd.models import get_config
@@ -67,7 +70,7 @@ def main() -> int:
     if env.device.type == "cuda":
         _native.hip_ops()  # fail loudly if the HIP kernels are not built
     comm = Comm()
-    mcfg = get_config(args.model)
+    mcfg = get_config(args.model, **({"n_layers": args.n_layers} if args.n_layers else {}))
     ecfg = EngineConfig(zero_stage=args.zero, micro_batch_size=args.mbs, seq_len=args.seq, grad_accum=args.ga,
                         lr=3e-5, warmup_steps=100, total_steps=10000, grad_clip=1.0,
                         activation_checkpointing=args.ckpt, max_live_parameters=_knob(args.live_params),
@@ -131,7 +134,7 @@ def main() -> int:
             "dtype": "bf16",
             "data": "synthetic (uniform random token ids; random-init weights)",
             "config": {
-                "model": mcfg.name,
+                "model": mcfg.name if not args.n_layers else f"{mcfg.name} ({mcfg.n_layers} layers)",
                 "global_batch": args.mbs * args.ga * env.world,
                 "micro_batch_per_gpu": args.mbs,
                 "grad_accum": args.ga,
