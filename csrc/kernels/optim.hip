@@ -49,7 +49,23 @@ __global__ __launch_bounds__(kThreads) void grad_stats_partial_kernel(const T* _
   __shared__ float red[kThreads / 64];
   float ss = 0.f, bad = 0.f;
   const int64_t nv = n >> 2;
-  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kThreads) {
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  // four independent 16-byte loads in flight per lane before any of them is consumed
+  for (; i + 3 * stride < nv; i += 4 * stride) {
+    float v[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) load4<T>(g + (i + u * stride) * 4, v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool fin = __builtin_isfinite(v[u][j]);
+        bad += fin ? 0.f : 1.f;
+        ss += fin ? v[u][j] * v[u][j] : 0.f;
+      }
+  }
+  for (; i < nv; i += stride) {
     float v[4];
     load4<T>(g + i * 4, v);
 #pragma unroll
@@ -191,7 +207,7 @@ void dlgm_grad_stats(at::TensorList grads, at::Tensor out, bool accumulate) {
   int64_t total = 0;
   for (const auto& g : grads) {
     check_flat(g, "grad");
-    const int64_t gr = std::min<int64_t>(stream_grid(g.numel() / 4), 512);
+    const int64_t gr = std::min<int64_t>(stream_grid(g.numel() / 4), 1024);
     grids.push_back(gr);
     total += gr;
   }
