@@ -87,15 +87,16 @@ class MixtralBlock(LlamaBlock):
         F = c.ffn_dim
         M = x.shape[0]
         gu_all = x.new_empty((M, 2 * F))
-        a_all = x.new_empty((M, F))
         y = x.new_empty((M, c.d_model))
         off = 0
         for e, n in enumerate(counts):
             if n:
-                xe = x.narrow(0, off, n)
-                gu = gu_all.narrow(0, off, n)
-                torch.mm(xe, p["w_gate_up"][e].t(), out=gu)
-                a_all.narrow(0, off, n).copy_(ops.swiglu_fwd(gu))
+                torch.mm(x.narrow(0, off, n), p["w_gate_up"][e].t(), out=gu_all.narrow(0, off, n))
+            off += n
+        a_all = ops.swiglu_fwd(gu_all)  # the expert segments are contiguous: one launch, no per-expert copy
+        off = 0
+        for e, n in enumerate(counts):
+            if n:
                 torch.mm(a_all.narrow(0, off, n), p["w_down"][e].t(), out=y.narrow(0, off, n))
             off += n
         return y, (gu_all, a_all, counts)
@@ -103,6 +104,7 @@ class MixtralBlock(LlamaBlock):
     def _experts_bwd(self, p: Params, g: Params, x: torch.Tensor, dy: torch.Tensor, saved, acc: bool):
         gu_all, a_all, counts = saved
         dx = torch.empty_like(x)
+        da_all = torch.empty_like(a_all)
         off = 0
         for e, n in enumerate(counts):
             if n == 0:
@@ -112,10 +114,16 @@ class MixtralBlock(LlamaBlock):
                 continue
             dye = dy.narrow(0, off, n)
             grad_mm(g["w_down"][e], dye.t(), a_all.narrow(0, off, n), acc)
-            da = torch.mm(dye, p["w_down"][e])
-            dgu = ops.swiglu_bwd(da, gu_all.narrow(0, off, n))
-            grad_mm(g["w_gate_up"][e], dgu.t(), x.narrow(0, off, n), acc)
-            torch.mm(dgu, p["w_gate_up"][e], out=dx.narrow(0, off, n))
+            torch.mm(dye, p["w_down"][e], out=da_all.narrow(0, off, n))
+            off += n
+        dgu_all = ops.swiglu_bwd(da_all, gu_all)  # one launch over every expert's rows
+        del da_all
+        off = 0
+        for e, n in enumerate(counts):
+            if n:
+                dgu = dgu_all.narrow(0, off, n)
+                grad_mm(g["w_gate_up"][e], dgu.t(), x.narrow(0, off, n), acc)
+                torch.mm(dgu, p["w_gate_up"][e], out=dx.narrow(0, off, n))
             off += n
         return dx
 
