@@ -55,14 +55,21 @@ def test_presets_and_preset_launch():
     assert r.status_code == 400 and "Available" in r.json()["detail"]
 
 
-def test_config_generate_is_pure(tmp_path):
+def test_config_generate_is_pure(tmp_path, monkeypatch):
+    import tempfile
+
+    # every tempfile-based write lands in tmp_path; /tmp itself is shared with concurrent test workers,
+    # so only config-looking new names there count
+    monkeypatch.setattr(tempfile, "tempdir", str(tmp_path))
     before = set(os.listdir("/tmp"))
     r = client.post("/api/v1/training/config/generate", json={"training_script": "t.py", "num_gpus": 8})
     assert r.status_code == 200
     j = r.json()
     assert j["deepspeed_config"]["zero_optimization"]["stage"] == 3 and j["effective_batch_size"] == 256
     assert "--nproc-per-node=8" in j["launch_command"]
-    assert set(os.listdir("/tmp")) == before  # A24: no temp file written
+    assert os.listdir(tmp_path) == []  # A24: no temp file written
+    new = set(os.listdir("/tmp")) - before
+    assert not [n for n in new if "ds_config" in n or "deepspeed" in n], new
 
 
 def test_monitoring_flow_and_nan_safety():
