@@ -9,7 +9,7 @@ MODE=${1:-all}
 STEPS=${BENCH_STEPS:-3}
 run() { echo "== $*" ; "$@"; }
 if [ "$MODE" = "all" ] || [ "$MODE" = "test" ]; then
-  run timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+  run timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
   tail -30 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
   run timeout -k 10 300 python __graft_entry__.py smoke 2>&1 | tee gpurun_out/smoke.log || exit 1
 fi
