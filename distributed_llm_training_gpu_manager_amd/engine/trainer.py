@@ -15,6 +15,7 @@ import argparse
 import json
 import math
 import os
+import queue
 import signal
 import sys
 import threading
@@ -59,20 +60,39 @@ class SyntheticData:
 
 
 class MetricsPusher:
-    """Best-effort, non-blocking POST of TrainingMetrics to the control plane's /monitoring/ingest."""
+    """Best-effort, non-blocking POST of TrainingMetrics to the control plane's /monitoring/ingest.
+
+    One sender thread drains a queue, so batches arrive in step order (the monitor's rules and the
+    Prometheus step gauge depend on it) and the training loop never waits on HTTP."""
 
     def __init__(self, url: Optional[str], job_id: str):
         self.url, self.job_id = url, job_id
-        self._buf: List[Dict[str, Any]] = []
-        self._lock = threading.Lock()
+        self._q: "queue.Queue[Optional[Dict[str, Any]]]" = queue.Queue()
+        self._thread: Optional[threading.Thread] = None
+        if url:
+            self._thread = threading.Thread(target=self._loop, daemon=True, name="metrics-push")
+            self._thread.start()
 
     def push(self, m: Dict[str, Any]) -> None:
-        if not self.url:
-            return
-        with self._lock:
-            self._buf.append(m)
-            batch, self._buf = self._buf, []
-        threading.Thread(target=self._send, args=(batch,), daemon=True).start()
+        if self.url:
+            self._q.put(m)
+
+    def _loop(self) -> None:
+        while True:
+            m = self._q.get()
+            if m is None:
+                return
+            batch = [m]
+            while True:  # coalesce whatever queued up while the last POST was in flight
+                try:
+                    nxt = self._q.get_nowait()
+                except queue.Empty:
+                    break
+                if nxt is None:
+                    self._send(batch)
+                    return
+                batch.append(nxt)
+            self._send(batch)
 
     def _send(self, batch) -> None:
         body = json.dumps({"job_id": self.job_id, "metrics": batch}).encode()
@@ -82,6 +102,11 @@ class MetricsPusher:
             urllib.request.urlopen(req, timeout=2).read()
         except Exception:  # noqa: BLE001
             pass
+
+    def close(self, timeout_s: float = 5.0) -> None:
+        if self._thread is not None:
+            self._q.put(None)
+            self._thread.join(timeout_s)
 
 
 class Trainer:
@@ -113,6 +138,8 @@ class Trainer:
             self.ecfg.wall_clock_breakdown = True
         if getattr(args, "hip_graphs", False):
             self.ecfg.hip_graphs = True
+        if args.halt_on_nan and not self.ecfg.fp16:
+            self.ecfg.nan_latch = True  # the host runs one step ahead of the NaN decision (see NanTrap)
         self.engine = ZeroEngine(self.mcfg, self.ecfg, self.env.device, self.comm)
         self.monitor = LossSpikeMonitor(MonitorConfig())
         self.trap = NanTrap(self.env.device, self.monitor)
@@ -135,13 +162,51 @@ class Trainer:
         if self.env.rank == 0:
             print(f"[train] {msg}", flush=True)
 
-    def _sync_flag(self, flag: bool) -> bool:
-        """All ranks agree on a host-side flag (preemption signals may reach ranks at different steps)."""
-        if self.comm.world == 1:
-            return flag
-        t = torch.tensor([1.0 if flag else 0.0], device=self.env.device)
-        self.comm.all_reduce_max(t)
-        return bool(t.item() > 0)
+    def _report(self, step: int, issued: Dict[str, Any]) -> Dict[str, Any]:
+        """Read step `step`'s report (stats + loss) from the pinned ring: called for step t-1 right after
+        step t is queued, so the wait overlaps step t on the GPU. The values are all-reduced, so every
+        rank takes the same halt / preemption decision at the same loop iteration."""
+        v = self.trap.get(step)
+        if v is None:
+            v = [float(x) for x in torch.cat([self.engine.stats, issued["m"]["loss"].reshape(1).float()]).tolist()]
+        ss, bad, flag, loss = v[0], v[1], v[2], v[3]
+        now = time.time()
+        dt = now - self._t_last
+        self._t_last = now
+        rec = {"step": step, "loss": loss, "grad_norm": math.sqrt(max(ss, 0.0)) * issued["inv_scale"],
+               "lr": issued["m"]["lr"], "step_s": dt, "tokens_per_sec": self._tokens_step / max(dt, 1e-9),
+               "nonfinite": bad, "preempt": flag > 0}
+        self.log.append(rec)
+        a = self.args
+        if self.env.rank == 0:
+            write_status(step, loss=loss, nonfinite=bad)
+            alerts = self.monitor.ingest(TrainingMetrics(step=step, loss=loss, learning_rate=rec["lr"],
+                                                         gradient_norm=rec["grad_norm"],
+                                                         tokens_per_sec=rec["tokens_per_sec"]))
+            self.pusher.push({"step": step, "loss": loss if math.isfinite(loss) else 1e30,
+                              "learning_rate": rec["lr"], "gradient_norm": rec["grad_norm"]
+                              if math.isfinite(rec["grad_norm"]) else 1e30})
+            if step % a.log_interval == 0 and self.engine.timers.enabled:
+                rec["wall_clock_breakdown_ms"] = {k: v["total_ms"] for k, v in self.engine.timers.summary().items()}
+            if step % a.log_interval == 0 or alerts:
+                self._say(json.dumps(json_safe(rec)) + ("" if not alerts else f" alerts={[x.alert_type for x in alerts]}"))
+        return rec
+
+    def _decide(self, rec: Dict[str, Any], last_issued: int) -> Optional[int]:
+        """Exit code to stop with after step rec['step'] (None: go on). `last_issued` has been queued too;
+        with the NaN latch its update is skipped on the device, so a NaN halt leaves the pre-NaN state."""
+        a = self.args
+        if rec["nonfinite"] > 0 and a.halt_on_nan:
+            self._say(f"NaN/Inf gradients at step {rec['step']} ({int(rec['nonfinite'])} elements): update skipped "
+                      f"on device; halting")
+            return EXIT_NAN_HALT
+        if rec["preempt"]:
+            t0 = time.time()
+            if self.ckpt is not None:
+                self.ckpt.save(last_issued, client_state={"step": last_issued, "preempted": True}, blocking=True)
+            self._say(f"preemption: emergency checkpoint at step {last_issued} in {time.time() - t0:.2f}s; exiting")
+            return EXIT_PREEMPTED
+        return None
 
     def run(self) -> int:
         a = self.args
@@ -156,63 +221,78 @@ class Trainer:
                 self.monitor.reset()
         for n in self.notes:
             self._say(f"note: {n}")
-        tokens_step = self.ecfg.micro_batch_size * self.ecfg.seq_len * self.ecfg.grad_accum * self.env.world
-        t_last = time.time()
+        self._tokens_step = self.ecfg.micro_batch_size * self.ecfg.seq_len * self.ecfg.grad_accum * self.env.world
+        self._t_last = time.time()
+        self.engine.sync_flags = self.env.world > 1
+        first_attempt = os.environ.get("DLGM_RESTART", "0") == "0"
         rc = 0
+        prev: Optional[Tuple[int, Dict[str, Any]]] = None
+        last = start
         for step in range(start + 1, a.steps + 1):
-            if a.inject_nan_step == step:
+            if a.inject_nan_step == step and first_attempt:
                 self.engine.fault_inject_nan = True
+            self.engine.host_flag = 1.0 if self.preempt else 0.0
             prof = getattr(a, "profile_steps", 0) and step - start == 2  # trace window after one warm step
             with trace_window(a.profile_dir if prof else None, self.env.rank):
                 m = self.engine.train_step(self.data.batches(step))
                 for _ in range(a.profile_steps - 1 if prof else 0):  # extra traced steps reuse this step's data
                     self.engine.train_step(self.data.batches(step))
-            self.trap.record(step, self.engine.stats)
-            # deterministic halt decision: every rank reads the (all-reduced) stats of THIS step
-            bad = float(self.engine.stats[1].item())
-            now = time.time()
-            loss = float(m["loss"])
-            rec = {"step": step, "loss": loss, "grad_norm": float(m["grad_norm"]), "lr": m["lr"],
-                   "step_s": now - t_last, "tokens_per_sec": tokens_step / max(now - t_last, 1e-9)}
-            t_last = now
-            self.log.append(rec)
-            if self.env.rank == 0:
-                write_status(step, loss=loss, nonfinite=bad)
-                alerts = self.monitor.ingest(TrainingMetrics(step=step, loss=loss, learning_rate=m["lr"],
-                                                             gradient_norm=rec["grad_norm"],
-                                                             tokens_per_sec=rec["tokens_per_sec"]))
-                self.pusher.push({"step": step, "loss": loss if math.isfinite(loss) else 1e30,
-                                  "learning_rate": m["lr"], "gradient_norm": rec["grad_norm"]
-                                  if math.isfinite(rec["grad_norm"]) else 1e30})
-                if step % a.log_interval == 0 and self.engine.timers.enabled:
-                    rec["wall_clock_breakdown_ms"] = {k: v["total_ms"] for k, v in self.engine.timers.summary().items()}
-                if step % a.log_interval == 0 or alerts:
-                    self._say(json.dumps(rec) + ("" if not alerts else f" alerts={[x.alert_type for x in alerts]}"))
-            first_attempt = os.environ.get("DLGM_RESTART", "0") == "0"
+            inv = 1.0 / self.engine.scaler.scale if self.engine.scaler else 1.0
+            self.trap.record(step, torch.cat([self.engine.stats, m["loss"].reshape(1).float()]))
+            issued = {"m": m, "inv_scale": inv}
+            last = step
+            # step t-1's outcome, read while step t runs on the device
+            if prev is not None:
+                stop = self._decide(self._report(*prev), step)
+                prev = None
+                if stop is not None:
+                    rc = stop
+                    break
+            save_due = self.ckpt is not None and a.save_interval > 0 and step % a.save_interval == 0
+            if save_due:  # never persist a step before knowing it is clean
+                rec = self._report(step, issued)
+                stop = self._decide(rec, step)
+                if stop is not None:
+                    rc = stop
+                    break
+                self.ckpt.save(step, client_state={"step": step})
+            else:
+                prev = (step, issued)
             if a.kill_at_step == step and first_attempt and self.env.rank == 0:
                 if self.ckpt is not None:
                     self.ckpt.wait()  # the drill kills after the last interval checkpoint is durable
                 os.kill(os.getpid(), signal.SIGKILL)
             if a.preempt_at_step == step and first_attempt:
                 os.kill(os.getpid(), signal.SIGUSR1)
-            if bad > 0 and a.halt_on_nan:
-                self._say(f"NaN/Inf gradients at step {step} ({int(bad)} elements): update skipped on device; halting")
-                rc = EXIT_NAN_HALT
-                break
-            if self.ckpt is not None and a.save_interval > 0 and step % a.save_interval == 0:
-                self.ckpt.save(step, client_state={"step": step})
-            if self._sync_flag(self.preempt):
+            if self.preempt and self.env.world == 1:
+                # one rank needs no agreement: checkpoint the step just queued, now (W > 1 ranks agree through
+                # the flag slot of the next step's all-reduced stats)
+                if prev is not None:  # prev is this step (not read yet): never persist a NaN step
+                    rec = self._report(*prev)
+                    prev = None
+                    if rec["nonfinite"] > 0 and a.halt_on_nan:
+                        rc = self._decide(rec, step)
+                        break
                 t0 = time.time()
                 if self.ckpt is not None:
                     self.ckpt.save(step, client_state={"step": step, "preempted": True}, blocking=True)
                 self._say(f"preemption: emergency checkpoint at step {step} in {time.time() - t0:.2f}s; exiting")
                 rc = EXIT_PREEMPTED
                 break
+        if prev is not None and rc == 0:
+            stop = self._decide(self._report(*prev), last)
+            rc = stop or 0
+        if rc == 0 and self.preempt and self.env.world == 1:
+            # a notice that arrived after the last step was queued (one rank: no agreement needed)
+            if self.ckpt is not None:
+                self.ckpt.save(last, client_state={"step": last, "preempted": True}, blocking=True)
+            rc = EXIT_PREEMPTED
         if self.ckpt is not None:
             self.ckpt.wait()
             if rc == 0 and a.export:
                 export_consolidated(self.engine, a.export)
         self.trap.close()
+        self.pusher.close()
         if a.log_json and self.env.rank == 0:
             with open(a.log_json, "w") as f:
                 json.dump(json_safe({"log": self.log, "ckpt": self.ckpt.history if self.ckpt else [],

@@ -22,24 +22,29 @@ import torch.distributed as dist
 from .comm import Comm
 
 
-def build_ep_comms(ep_size: int) -> Tuple[Optional[Comm], Optional[Comm]]:
-    """Return (ep_comm, expert_dp_comm) for this rank; every rank must call this collectively."""
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+def build_ep_comms(ep_size: int, comm: Optional[Comm] = None) -> Tuple[Optional[Comm], Optional[Comm]]:
+    """Return (ep_comm, expert_dp_comm) for this rank; every rank must call this collectively.
+
+    The EP all-to-all always gets a communicator of its own -- also when ep_size == world -- so the
+    token exchange runs on its own RCCL stream instead of queueing behind the dense gradient
+    reduce-scatters on the world communicator."""
+    comm = comm or Comm()
+    if comm.world == 1:
         return None, None
-    world, rank = dist.get_world_size(), dist.get_rank()
+    world, rank = comm.world, comm.rank
     assert world % ep_size == 0, "world size must be a multiple of expert_parallel_size"
     ep_comm = edp_comm = None
     for b in range(world // ep_size):
         ranks = list(range(b * ep_size, (b + 1) * ep_size))
-        g = dist.new_group(ranks) if ep_size < world else dist.group.WORLD
+        g = comm.duplicate() if ep_size == world else comm.new_group(ranks)
         if rank in ranks:
-            ep_comm = Comm(g)
+            ep_comm = g
     dp = world // ep_size
     for i in range(ep_size):
         ranks = list(range(i, world, ep_size))
-        g = dist.new_group(ranks) if dp < world else dist.group.WORLD
+        g = comm.new_group(ranks)
         if rank in ranks:
-            edp_comm = Comm(g)
+            edp_comm = g
     return ep_comm, edp_comm
 
 

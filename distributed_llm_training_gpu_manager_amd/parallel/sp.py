@@ -31,18 +31,19 @@ from .. import ops
 from .comm import Comm
 
 
-def build_sp_comm(sp_size: int) -> Optional[Comm]:
+def build_sp_comm(sp_size: int, comm: Optional[Comm] = None) -> Optional[Comm]:
     """Contiguous rank blocks [0..sp-1], [sp..2sp-1], ...; every rank must call this collectively."""
-    if sp_size <= 1 or not dist.is_initialized():
+    comm = comm or Comm()
+    if sp_size <= 1 or comm.world == 1:
         return None
-    world, rank = dist.get_world_size(), dist.get_rank()
+    world, rank = comm.world, comm.rank
     assert world % sp_size == 0, "world size must be a multiple of sequence_parallel_size"
     mine = None
     for b in range(world // sp_size):
         ranks = list(range(b * sp_size, (b + 1) * sp_size))
-        g = dist.new_group(ranks) if sp_size < world else dist.group.WORLD
+        g = comm.new_group(ranks)
         if rank in ranks:
-            mine = Comm(g)
+            mine = g
     return mine
 
 

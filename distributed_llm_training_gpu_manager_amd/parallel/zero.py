@@ -93,6 +93,8 @@ class EngineConfig:
     max_reuse_distance: Any = 1e9
     prefetch_bucket_size: float = 5e8
     live_hbm_fraction: float = 0.12
+    # 'hbm' residency / W^T-cache sizing leaves at least this fraction of the device free (planner.zero3_budgets)
+    hbm_headroom: float = 0.10
     seed: int = 1234
     expert_parallel_size: int = 1
     # Ulysses sequence parallelism (parallel/sp.py): seq_len is then the LOCAL chunk per rank and a
@@ -117,7 +119,7 @@ class EngineConfig:
     # input-gradient GEMMs then run with both operands K-contiguous (refreshed once per optimizer step)
     transposed_weight_cache: bool = True
     # ZeRO-3 (P > 1): groups the residency plan holds gathered for the whole step get the W^T cache too,
-    # while the caches fit in this fraction of HBM (Llama-3-8B: 14 GiB)
+    # while the caches fit in this fraction of HBM (Llama-3-8B: 14 GiB) and in what the HBM plan leaves
     tcache_hbm_fraction: float = 0.08
     init_device: str = "auto"  # "cpu" gives bit-identical init on any device (tests); auto: cpu below 1e9 params
     # replay the GA micro-batches of a step (forward + backward + gradient accumulation) as ONE captured
@@ -125,6 +127,9 @@ class EngineConfig:
     # step is launch-bound (GPT-2-small, small Llama). Needs a step with no collective and no host sync
     # inside the micro-batch loop (single rank, dense model, no offload, bf16); otherwise eager.
     hip_graphs: bool = False
+    # once a step has non-finite gradients every later update is skipped on the device too (halt-on-NaN
+    # jobs whose host runs a step ahead: the state at exit is the state before the poisoned step)
+    nan_latch: bool = False
     fp16: bool = False  # dynamic loss scaling path (reference fp16 block)
     loss_scale: float = 0.0  # 0 = dynamic
     initial_scale_power: int = 16
@@ -223,7 +228,7 @@ class ZeroEngine:
         self.ep_size = max(1, cfg.expert_parallel_size) if model_cfg.n_experts else 1
         if self.ep_size > 1 and self.W > 1:
             from .ep import build_ep_comms
-            self.ep_comm, self.edp_comm = build_ep_comms(self.ep_size)
+            self.ep_comm, self.edp_comm = build_ep_comms(self.ep_size, self.comm)
         else:
             self.ep_size = 1
             self.ep_comm, self.edp_comm = None, self.comm
@@ -232,14 +237,13 @@ class ZeroEngine:
         self.sp_size, self.sp_comm = max(1, cfg.sequence_parallel_size), None
         if self.sp_size > 1 and self.W > 1:
             from .sp import build_sp_comm
-            self.sp_comm = build_sp_comm(self.sp_size)
+            self.sp_comm = build_sp_comm(self.sp_size, self.comm)
         else:
             self.sp_size = 1
         ep_rank = self.ep_comm.rank if self.ep_comm is not None else 0
         self.gather_comm = self.comm
         if cfg.separate_gather_comm and self.W > 1 and self.stage > 0:
-            import torch.distributed as dist
-            self.gather_comm = Comm(dist.new_group(list(range(self.W))))
+            self.gather_comm = self.comm.duplicate()
         groups, stages = build_model(model_cfg, ep_rank, self.ep_size)
         self.stages = [(u, tuple(gi) if isinstance(gi, (tuple, list)) else (gi,)) for u, gi in stages]
         self.groups = []
@@ -261,6 +265,13 @@ class ZeroEngine:
             soff += g.shard_numel
             foff += g.numel
         self.shard_total, self.full_total = soff, foff
+        # local fp32 gradients exist only for groups that are reduce-scattered (P > 1); a P == 1 group
+        # (e.g. experts at EP == W) accumulates straight into its fp32 shard
+        goff = 0
+        for g in self.groups:
+            g.gfull_off = goff
+            goff += g.numel if g.P > 1 else 0
+        self.gfull_total = goff
         # MI355X compute dtype is bf16 (fp16 requests keep the loss-scaler path but compute in bf16)
         self.dtype = torch.bfloat16
         self.is_cuda = device.type == "cuda"
@@ -281,7 +292,12 @@ class ZeroEngine:
                         self._tnames[g.idx] = names
         self.step_count = 0
         self.scaler = LossScaler(cfg, device) if cfg.fp16 else None
-        self.stats = torch.zeros(2, dtype=torch.float32, device=device)
+        # [sum g^2, #non-finite, host flags]: the flags slot rides the stats all-reduce, so ranks agree on
+        # host-side events (preemption) without a collective or a host read of their own
+        self.stats = torch.zeros(3, dtype=torch.float32, device=device)
+        self.host_flag = 0.0  # set by the trainer before a step (e.g. 1.0 = preemption notice on this rank)
+        self.sync_flags = False  # all-reduce the flag even when nothing else needs a collective (P == 1, W > 1)
+        self._nan_latch = torch.zeros(1, dtype=torch.float32, device=device) if cfg.nan_latch else None
         self.loss_acc = torch.zeros((), dtype=torch.float32, device=device)
         from ..ops.rope import rope_tables
         if model_cfg.arch in ("llama", "mixtral"):
@@ -338,7 +354,7 @@ class ZeroEngine:
             self.p16_full = torch.zeros(self.full_total, dtype=self.dtype, device=dev)
         self.local_grads = self._want_local_grads()
         if self.stage == 1 or self.local_grads:
-            self.grad_full = torch.zeros(self.full_total, **f32)
+            self.grad_full = torch.zeros(self.gfull_total, **f32)
 
     def _want_local_grads(self) -> bool:
         """ZeRO-2/3: accumulate fp32 gradients locally across micro-batches (one reduce-scatter per step)?"""
@@ -351,7 +367,7 @@ class ZeroEngine:
             if self.cfg.grad_accum <= 1 or not self.is_cuda:
                 return False
             hbm = torch.cuda.get_device_properties(self.device).total_memory
-            return self.full_total * 4 <= self.cfg.local_grad_hbm_fraction * hbm
+            return self.gfull_total * 4 <= self.cfg.local_grad_hbm_fraction * hbm
         return bool(v)
 
     def _init_params(self) -> None:
@@ -440,20 +456,43 @@ class ZeroEngine:
         which gathered groups stay resident between them (parallel/residency.py)."""
         n = len(self.stages)
         visits = [self.stages[si][1] for si in range(n)] + [self.stages[si][1] for si in range(n - 1, -1, -1)]
-        hbm = lambda: (self.cfg.live_hbm_fraction * torch.cuda.get_device_properties(self.device).total_memory  # noqa: E731
-                       / self.p16_shard.element_size()) if self.is_cuda else math.inf
+        gathered = [self.stage == 3 and g.P > 1 for g in self.groups]
+        self._tcache_budget = lambda resident_bytes: math.inf  # noqa: E731
+        hbm = lambda: math.inf  # noqa: E731
+        if self.is_cuda:
+            from .planner import zero3_budgets
+            live, self._tcache_budget = zero3_budgets(
+                torch.cuda.get_device_properties(self.device).total_memory, self._hbm_committed(gathered),
+                self.cfg.live_hbm_fraction, self.cfg.tcache_hbm_fraction, self.cfg.hbm_headroom)
+            hbm = lambda: live  # noqa: E731
         max_live = resolve_limit(self.cfg.max_live_parameters, hbm)
         max_reuse = resolve_limit(self.cfg.max_reuse_distance, hbm, unbounded_for_hbm=True)
-        gathered = [self.stage == 3 and g.P > 1 for g in self.groups]
         self.live_plan = ResidencyPlan(visits, [g.numel for g in self.groups], gathered, max_live, max_reuse)
+
+    def _hbm_committed(self, gathered: List[bool]) -> float:
+        """Bytes this rank will hold at its peak besides the optional ZeRO-3 residency / W^T caches: what is
+        allocated now (shards, optimizer state, local gradients) + the planner's activation, scratch and
+        in-flight-gather estimates (parallel/planner.py, the same rules it applies to a whole config)."""
+        from .planner import _activation_bytes, runtime_reserve
+        c = self.cfg
+        now = float(torch.cuda.memory_allocated(self.device))
+        extra = sum(_activation_bytes(self.mcfg, c.micro_batch_size * c.seq_len, c.seq_len,
+                                      c.activation_checkpointing, self.ep_size).values())
+        red = [g.numel for g in self.groups if g.P > 1]
+        if self.stage in (2, 3) and red:
+            extra += 4.0 * max(red) * (1 + 1.0 / self.W)
+        sizes = sorted((sum(self.groups[gi].numel for gi in gis if gathered[gi]) for _, gis in self.stages),
+                       reverse=True)
+        if sizes:
+            extra += 2.0 * (sizes[0] + (sizes[1] if len(sizes) > 1 else 0))
+        return now + extra + runtime_reserve(now + extra)
 
     def _add_resident_tcache(self) -> None:
         """ZeRO-3, P > 1: a gathered group the residency plan holds through the whole step is as stationary
         between optimizer steps as a ZeRO-1/2 weight, so its dX GEMMs get the cached W^T as well (built on
         the first fetch after the step's all-gather, reused by every micro-batch). Without this a ZeRO-3
         run on N > 1 GPUs would lose the K-contiguous dX layout the single-GPU run has."""
-        budget = (self.cfg.tcache_hbm_fraction * torch.cuda.get_device_properties(self.device).total_memory
-                  if self.is_cuda else math.inf)
+        budget = self._tcache_budget(self.live_plan.resident_params * self.p16_shard.element_size())
         used = 0
         for g in self.groups:
             if g.P == 1 or g.idx in self._tnames or not self.live_plan.held_through_step(g.idx):
@@ -499,7 +538,7 @@ class ZeroEngine:
         if g.P == 1:
             return self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
         if self.stage == 1 or self.local_grads:
-            return self.grad_full.narrow(0, g.full_off, g.numel)
+            return self.grad_full.narrow(0, g.gfull_off, g.numel)
         return None
 
     def _finish_direct(self, g: FlatGroup, tgt: torch.Tensor, pending: List[Tuple[Handle, Any]]) -> None:
@@ -669,25 +708,37 @@ class ZeroEngine:
         self._live.clear()
 
     def _global_grad_stats(self) -> None:
-        """stats = [sum g^2, #non-finite] over the whole model, each element counted once."""
+        """stats = [sum g^2, #non-finite, flags] over the whole model, each gradient element counted once;
+        flags = sum over ranks of host_flag."""
+        st = self.stats
         if not self.has_experts:
-            ops.grad_stats([self.grad_shard], self.stats)
+            ops.grad_stats([self.grad_shard], st)
+            st[2].fill_(self.host_flag)
             if self.P > 1:
-                self.comm.all_reduce(self.stats, async_op=False).wait()
-            return
-        sl = lambda g: self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
-        dense = torch.zeros(2, dtype=torch.float32, device=self.device)
-        exp = torch.zeros(2, dtype=torch.float32, device=self.device)
-        ops.grad_stats([sl(g) for g in self.groups if g.kind != "expert"], dense)
-        ops.grad_stats([sl(g) for g in self.groups if g.kind == "expert"], exp)
-        if self.P > 1:
-            self.comm.all_reduce(dense, async_op=False).wait()
-        if self.ep_comm is not None and self.ep_comm.world > 1:
-            self.ep_comm.all_reduce(exp, async_op=False).wait()
-        eg = next(g for g in self.groups if g.kind == "expert")
-        if eg.P > 1:
-            eg.comm.all_reduce(exp, async_op=False).wait()
-        self.stats.copy_(dense + exp)
+                self.comm.all_reduce(st, async_op=False).wait()
+            elif self.sync_flags and self.W > 1:
+                self.comm.all_reduce(st[2:3], async_op=False).wait()
+        else:
+            sl = lambda g: self.grad_shard.narrow(0, g.shard_off, g.shard_numel)  # noqa: E731
+            dense = torch.zeros(3, dtype=torch.float32, device=self.device)
+            exp = torch.zeros(2, dtype=torch.float32, device=self.device)
+            ops.grad_stats([sl(g) for g in self.groups if g.kind != "expert"], dense)
+            ops.grad_stats([sl(g) for g in self.groups if g.kind == "expert"], exp)
+            dense[2].fill_(self.host_flag)
+            if self.P > 1:
+                self.comm.all_reduce(dense, async_op=False).wait()
+            elif self.sync_flags and self.W > 1:
+                self.comm.all_reduce(dense[2:3], async_op=False).wait()
+            if self.ep_comm is not None and self.ep_comm.world > 1:
+                self.ep_comm.all_reduce(exp, async_op=False).wait()
+            eg = next(g for g in self.groups if g.kind == "expert")
+            if eg.P > 1:
+                eg.comm.all_reduce(exp, async_op=False).wait()
+            st.copy_(dense)
+            st[:2] += exp
+        if self._nan_latch is not None:
+            torch.maximum(self._nan_latch, st[1:2], out=self._nan_latch)
+            st[1:2].copy_(self._nan_latch)
 
     def optimizer_step(self) -> Dict[str, Any]:
         t0 = self.timers.mark()
@@ -730,7 +781,7 @@ class ZeroEngine:
         """Host AdamW over the offloaded partition; the clip / overflow decision needs the stats on the host
         (same formula as the device kernel, csrc/kernels/optim.hip clip_coef)."""
         cfg = self.cfg
-        sumsq, nonfinite = (float(x) for x in self.stats.tolist())
+        sumsq, nonfinite = (float(x) for x in self.stats[:2].tolist())
         if nonfinite > 0:
             return
         coef = inv_scale
@@ -862,7 +913,7 @@ class ZeroEngine:
             "grad_shard_GiB": self.shard_total * 4 / gb,
             "param_shard_GiB": self.shard_total * 2 / gb,
             "param_full_GiB": (self.full_total * 2 / gb) if self.p16_full is not None else 0.0,
-            "grad_full_GiB": (self.full_total * 4 / gb) if self.grad_full is not None else 0.0,
+            "grad_full_GiB": (self.gfull_total * 4 / gb) if self.grad_full is not None else 0.0,
             "weight_T_cache_GiB": sum(t.numel() * t.element_size() for _, c in self._tcache.values()
                                       for t in c.values()) / gb,
             "zero3_resident_gathered_GiB": self.live_plan.resident_params * self.p16_shard.element_size() / gb,
