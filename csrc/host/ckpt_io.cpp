@@ -18,6 +18,7 @@
 #include <string.h>
 #include <sys/stat.h>
 #include <unistd.h>
+#include <zlib.h>
 
 #include <algorithm>
 #include <atomic>
@@ -62,7 +63,11 @@ uint32_t crc32c_sw(const uint8_t* p, size_t n, uint32_t crc) {
 
 bool have_sse42() { return __builtin_cpu_supports("sse4.2"); }
 
-int run_chunks(int fd, uint8_t* buf, size_t n, size_t chunk, int nthreads, uint32_t* crcs, bool write) {
+// pwrite/pread `n` bytes of `buf` at file offset `file_off` in `chunk`-byte pieces on `nthreads` threads.
+// Per chunk (relative to `buf`): CRC32C into `crcs` (our manifests) and, when `zcrcs` is given, the zip
+// CRC-32 (zlib polynomial) that a torch-zip (.pt) record header carries -- combined by the caller.
+int run_chunks(int fd, uint8_t* buf, size_t n, size_t file_off, size_t chunk, int nthreads, uint32_t* crcs,
+               uint32_t* zcrcs, bool write) {
   const size_t nchunks = (n + chunk - 1) / chunk;
   std::atomic<size_t> next{0};
   std::atomic<int> err{0};
@@ -75,9 +80,10 @@ int run_chunks(int fd, uint8_t* buf, size_t n, size_t chunk, int nthreads, uint3
       const size_t len = std::min(chunk, n - off);
       size_t done = 0;
       if (write && crcs) crcs[i] = hw ? crc32c_hw(buf + off, len, 0) : crc32c_sw(buf + off, len, 0);
+      if (write && zcrcs) zcrcs[i] = (uint32_t)crc32_z(0L, buf + off, len);
       while (done < len) {
-        ssize_t r = write ? pwrite(fd, buf + off + done, len - done, (off_t)(off + done))
-                          : pread(fd, buf + off + done, len - done, (off_t)(off + done));
+        ssize_t r = write ? pwrite(fd, buf + off + done, len - done, (off_t)(file_off + off + done))
+                          : pread(fd, buf + off + done, len - done, (off_t)(file_off + off + done));
         if (r < 0) {
           if (errno == EINTR) continue;
           err.store(-errno);
@@ -131,7 +137,7 @@ int dlgm_write_file(const char* path, const void* ptr, size_t n, size_t chunk, i
     close(fd);
     return e;
   }
-  int rc = run_chunks(fd, (uint8_t*)ptr, n, chunk, nthreads, crcs, true);
+  int rc = run_chunks(fd, (uint8_t*)ptr, n, 0, chunk, nthreads, crcs, nullptr, true);
   if (rc == 0 && do_fsync && fsync(fd) != 0) rc = -errno;
   if (close(fd) != 0 && rc == 0) rc = -errno;
   return rc;
@@ -145,9 +151,58 @@ int dlgm_read_file(const char* path, void* ptr, size_t n, size_t chunk, int nthr
     close(fd);
     return -EIO;
   }
-  int rc = run_chunks(fd, (uint8_t*)ptr, n, chunk, nthreads, crcs, false);
+  int rc = run_chunks(fd, (uint8_t*)ptr, n, 0, chunk, nthreads, crcs, nullptr, false);
   close(fd);
   return rc;
+}
+
+// pread of `n` bytes starting at `file_off` (a tensor record inside a .pt zip), per-chunk CRC32C.
+int dlgm_read_file_at(const char* path, void* ptr, size_t n, size_t file_off, size_t chunk, int nthreads,
+                      uint32_t* crcs) {
+  int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return -errno;
+  struct stat st;
+  if (fstat(fd, &st) != 0 || (size_t)st.st_size < file_off + n) {
+    close(fd);
+    return -EIO;
+  }
+  int rc = run_chunks(fd, (uint8_t*)ptr, n, file_off, chunk, nthreads, crcs, nullptr, false);
+  close(fd);
+  return rc;
+}
+
+// pwrite at an arbitrary file offset with per-chunk CRC32C and zip CRC-32 (either list may be null).
+int dlgm_pwrite_at2(int fd, const void* ptr, size_t n, size_t file_off, size_t chunk, int nthreads, uint32_t* crcs,
+                    uint32_t* zcrcs) {
+  return run_chunks(fd, (uint8_t*)ptr, n, file_off, chunk, nthreads, crcs, zcrcs, true);
+}
+
+// zip CRC-32 of B appended to A, from crc(A), crc(B) and len(B) (zlib crc32_combine).
+uint32_t dlgm_crc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) {
+  return (uint32_t)crc32_combine64(crc_a, crc_b, (z_off64_t)len_b);
+}
+
+// zip CRC-32 of a small buffer (headers / pickles).
+uint32_t dlgm_crc32_zip(const void* p, size_t n) { return (uint32_t)crc32_z(0L, (const Bytef*)p, n); }
+
+// Per-chunk CRC32C of an in-memory buffer on `nthreads` threads (verifying a /dev/shm snapshot tier).
+void dlgm_crc32c_chunks(const void* ptr, size_t n, size_t chunk, int nthreads, uint32_t* crcs) {
+  const size_t nchunks = (n + chunk - 1) / chunk;
+  std::atomic<size_t> next{0};
+  const bool hw = have_sse42();
+  auto worker = [&]() {
+    for (;;) {
+      const size_t i = next.fetch_add(1);
+      if (i >= nchunks) return;
+      const uint8_t* b = (const uint8_t*)ptr + i * chunk;
+      const size_t len = std::min(chunk, n - i * chunk);
+      crcs[i] = hw ? crc32c_hw(b, len, 0) : crc32c_sw(b, len, 0);
+    }
+  };
+  nthreads = std::max(1, std::min<int>(nthreads, (int)std::max<size_t>(nchunks, 1)));
+  std::vector<std::thread> ts;
+  for (int t = 0; t < nthreads; ++t) ts.emplace_back(worker);
+  for (auto& t : ts) t.join();
 }
 
 // AdamW on host fp32 state (ZeRO-Offload). g may be pre-scaled; gscale multiplies it.

@@ -33,6 +33,20 @@ def lib():
         L.dlgm_pwrite_at.restype = ctypes.c_int
         L.dlgm_pwrite_at.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
                                      ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)]
+        L.dlgm_read_file_at.restype = ctypes.c_int
+        L.dlgm_read_file_at.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                        ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)]
+        L.dlgm_pwrite_at2.restype = ctypes.c_int
+        L.dlgm_pwrite_at2.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                      ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32),
+                                      ctypes.POINTER(ctypes.c_uint32)]
+        L.dlgm_crc32_combine.restype = ctypes.c_uint32
+        L.dlgm_crc32_combine.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
+        L.dlgm_crc32_zip.restype = ctypes.c_uint32
+        L.dlgm_crc32_zip.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        L.dlgm_crc32c_chunks.restype = None
+        L.dlgm_crc32c_chunks.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
+                                         ctypes.POINTER(ctypes.c_uint32)]
         L.dlgm_close_file.restype = ctypes.c_int
         L.dlgm_close_file.argtypes = [ctypes.c_int, ctypes.c_int]
         L.dlgm_aio_create.restype = ctypes.c_void_p
@@ -107,6 +121,19 @@ def read_tensor(path: str, t: torch.Tensor) -> List[int]:
         f.readinto(memoryview(arr))
     mv = memoryview(arr)
     return [_crc_py(mv[i * CHUNK:(i + 1) * CHUNK]) for i in range(nch)]
+
+
+def crc32c_chunks(t: torch.Tensor) -> List[int]:
+    """Per-CHUNK CRC32C of a contiguous CPU tensor's bytes (8 threads; verifies a /dev/shm snapshot)."""
+    n = t.numel() * t.element_size()
+    nch = (n + CHUNK - 1) // CHUNK
+    L = lib()
+    if L is None:
+        mv = memoryview(t.view(torch.uint8).numpy())
+        return [_crc_py(mv[i * CHUNK:(i + 1) * CHUNK]) for i in range(nch)]
+    crcs = (ctypes.c_uint32 * max(nch, 1))()
+    L.dlgm_crc32c_chunks(ctypes.c_void_p(t.data_ptr()), n, CHUNK, THREADS, crcs)
+    return list(crcs)[:nch]
 
 
 def cpu_adamw_(p, m, v, g, p16, lr, b1, b2, eps, wd, bc1, bc2, gscale=1.0) -> None:

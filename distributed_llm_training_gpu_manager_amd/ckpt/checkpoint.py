@@ -1,54 +1,61 @@
-"""Asynchronous sharded checkpoints with a DeepSpeed-style layout, integrity manifests and resharding.
+"""Asynchronous sharded checkpoints: DeepSpeed file layout, a /dev/shm snapshot tier, agreed restore, resharding.
 
-The reference has no checkpoint code at all; its README claims
-auto-resume (``README.md:14``) and its config asks DeepSpeed to gather 16-bit
-weights on save (``ai_engine/deepspeed_launcher.py:74, :192``). This module is the
-MI355X implementation (§2.5 N8):
+The reference has no checkpoint code at all; its README claims auto-resume
+(``README.md:14``) and its config asks DeepSpeed to gather 16-bit weights on save
+(``ai_engine/deepspeed_launcher.py:74, :192``). This module is the MI355X implementation (§2.5 N8).
 
 Capture (training thread, no host sync)
-    ``device`` mode: the rank's fp32 master / exp_avg / exp_avg_sq shards are copied
-    D2D into a spare-HBM snapshot on a side stream (ZeRO-3 at W=8 is 12 B/param/8 --
-    milliseconds at HBM bandwidth); ``host`` mode (not enough free HBM, e.g. W=1):
-    D2H with ``non_blocking`` into pinned host memory. The next optimizer step
-    waits for the capture event *on the GPU* (``stream.wait_event``), so training
-    never blocks on the host.
-Write-out (background thread, off the critical path)
-    device mode streams the snapshot D2H through a 2-slot pinned ring; the C++ host
-    runtime (``csrc/host/ckpt_io.cpp``) pwrites each piece with 8 threads and a CRC32C
-    per 64 MiB chunk; files are fsync'ed; every rank writes ``manifest_r<r>.json``;
-    rank 0 waits for all manifests, writes ``COMPLETE``, renames ``<tag>.tmp`` ->
-    ``<tag>`` and atomically updates ``latest`` (no collectives from the writer thread).
-Layout (names follow DeepSpeed; tensors in raw ``.bin`` files, metadata in ``.pt``
-files loadable with ``torch.load(weights_only=True)``)::
+    The rank's fp32 master / exp_avg / exp_avg_sq shards and its bf16 compute shard are copied on a side
+    stream into a snapshot buffer: a ``/dev/shm`` file mapped and page-locked (``hipHostRegister``) when the
+    host has room ("shm" tier -- it outlives a SIGKILLed rank, so an auto-resume on the same node restores
+    from host RAM instead of disk), else spare HBM ("device": D2D at HBM speed) or pinned host memory. The
+    next optimizer step waits for the capture *on the GPU* (``stream.wait_event``), so training never
+    blocks on the host.
+Write-out (background thread)
+    Files are real ``torch.save``-format zips (``ckpt/ptzip.py``: pickle generated up front, tensor bytes
+    pwritten by the C++ host runtime with 8 threads, CRC32C per 64 MiB chunk for our manifest and the zip
+    CRC-32 in the record headers), so ``torch.load(path, weights_only=True)`` reads every one of them::
 
-    <save_dir>/latest                                    "global_step120"
-    <save_dir>/global_step120/mp_rank_00_model_states.pt  engine/model metadata, group layout, client state
-    <save_dir>/global_step120/zero_pp_rank_{r}_mp_rank_00_optim_states.pt   per-rank file index
-    <save_dir>/global_step120/zero_pp_rank_{r}_mp_rank_00_optim_states.{master,exp_avg,exp_avg_sq}.bin
-    <save_dir>/global_step120/manifest_r{r}.json  COMPLETE
+        <save_dir>/latest                                              "global_step120"
+        <save_dir>/global_step120/mp_rank_00_model_states.pt           engine/model metadata, client state
+        <save_dir>/global_step120/zero_pp_rank_{r}_mp_rank_00_model_states.pt   rank r's bf16 parameter shard
+        <save_dir>/global_step120/zero_pp_rank_{r}_mp_rank_00_optim_states.pt   rank r's fp32 master, exp_avg,
+                                                                                exp_avg_sq (DeepSpeed keys)
+        <save_dir>/global_step120/manifest_r{r}.json  COMPLETE
 
-Restore verifies sizes and CRCs while reading, falls back to the previous complete
-tag when a file is missing or corrupt (rollback), and reshards when the world size
-changed (elastic restart).
+    Every save carries a save id (step, restart count, save counter); rank 0 publishes the tag (writes
+    ``COMPLETE``, renames ``<tag>.tmp`` -> ``<tag>``, updates ``latest``) only when every writer's manifest
+    of THIS save is present, so a manifest left by a crashed earlier attempt cannot publish a half-written tag.
+Restore
+    Candidates newest first (the shm snapshot when every rank holds the same newest step, then the disk
+    tags). Each rank loads and CRC-verifies its part, then all ranks agree (MIN all-reduce of "ok") before
+    a candidate is accepted, so no rank can resume from a different step than the others (rollback is
+    collective). A world-size or EP-size change reshards: every group is reassembled from the old
+    shards -- expert groups expert by expert across the old EP ranks -- and re-sliced for the new layout.
 """
 from __future__ import annotations
 
+import hashlib
 import json
+import math
 import os
 import queue
 import re
 import shutil
 import threading
 import time
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
 
 from .. import _host
+from .ptzip import PtWriter, Slot, read_slot
 
 STATE = ("master", "exp_avg", "exp_avg_sq")
 TAG_RE = re.compile(r"^global_step(\d+)$")
+MODEL0 = "mp_rank_00_model_states.pt"
+DS_VERSION = "0.13.1+dlgm-mi355x"  # the DeepSpeed release the reference pins (requirements.txt:6)
 
 
 class CorruptCheckpoint(RuntimeError):
@@ -59,91 +66,194 @@ def _tag(step: int) -> str:
     return f"global_step{step}"
 
 
-def _optim_prefix(rank: int) -> str:
-    return f"zero_pp_rank_{rank}_mp_rank_00_optim_states"
+def optim_file(rank: int) -> str:
+    return f"zero_pp_rank_{rank}_mp_rank_00_optim_states.pt"
+
+
+def model_file(rank: int) -> str:
+    return f"zero_pp_rank_{rank}_mp_rank_00_model_states.pt"
+
+
+def _layout(eng) -> Dict[str, Any]:
+    """What a rank's shard files hold: enough to reassemble every group under any new layout."""
+    ep = eng.ep_size
+    return {"rank": eng.rank, "world": eng.W, "zero_stage": eng.stage, "ep_size": ep,
+            "ep_rank": eng.ep_comm.rank if (ep > 1 and eng.ep_comm is not None) else 0,
+            "shard_total": eng.shard_total,
+            "groups": [{"name": g.name, "kind": g.kind, "numel": g.numel, "shard_numel": g.shard_numel,
+                        "shard_off": g.shard_off, "P": g.P,
+                        "prank": (g.comm.rank if g.P > 1 else 0),
+                        "params": [[s.name, g.layout[s.name][0], list(s.shape), int(s.experts)] for s in g.specs]}
+                       for g in eng.groups]}
+
+
+def _writer_ranks(eng) -> List[int]:
+    """Ranks whose state is not a copy of a lower rank's: every rank under ZeRO-1/2/3; under ZeRO-0 rank 0,
+    plus one rank per EP position when experts are split over EP ranks (ranks 0..ep-1)."""
+    if eng.stage > 0:
+        return list(range(eng.W))
+    return list(range(eng.ep_size)) if eng.ep_size > 1 else [0]
+
+
+def _source_rank(eng) -> int:
+    """The writer rank whose files restore this rank (itself, or its ZeRO-0 twin)."""
+    if eng.stage > 0:
+        return eng.rank
+    return eng.rank % eng.ep_size if eng.ep_size > 1 else 0
+
+
+class _Agree:
+    """Cross-rank agreement on small integers (restore decisions), over the engine's communicator."""
+
+    def __init__(self, eng):
+        self.comm, self.dev = eng.comm, eng.device
+
+    def min(self, x: float) -> float:
+        if self.comm.world == 1:
+            return x
+        t = torch.tensor([-float(x)], dtype=torch.float64 if self.dev.type == "cpu" else torch.float32,
+                         device=self.dev)
+        self.comm.all_reduce_max(t)
+        return -float(t.item())
+
+    def max(self, x: float) -> float:
+        if self.comm.world == 1:
+            return x
+        t = torch.tensor([float(x)], dtype=torch.float64 if self.dev.type == "cpu" else torch.float32,
+                         device=self.dev)
+        self.comm.all_reduce_max(t)
+        return float(t.item())
 
 
 class AsyncCheckpointer:
     def __init__(self, engine, save_dir: str, mode: str = "auto", keep_last: int = 3,
-                 ring_bytes: int = 1 << 30, manifest_timeout_s: float = 600.0):
-        self.engine = engine
-        self.save_dir = save_dir
+                 ring_bytes: int = 1 << 30, manifest_timeout_s: float = 600.0, shm: Any = "auto",
+                 disk: bool = True):
+        self.engine = eng = engine
+        self.save_dir = os.path.abspath(save_dir)
         self.keep_last = keep_last
-        self.rank = engine.rank if engine.P > 1 else 0
-        self.P = engine.P
-        self.is_writer_rank0 = engine.rank == 0
-        # stage 0 (P == 1): every rank holds the full state; only rank 0 writes it
-        self.active = self.P > 1 or engine.rank == 0
-        self.n = engine.shard_total
-        self.dev = engine.device
+        self.rank = eng.rank
+        self.writers = _writer_ranks(eng)
+        self.active = self.rank in self.writers
+        self.is_rank0 = eng.rank == 0
+        self.n = eng.shard_total
+        self.dev = eng.device
         self.cuda = self.dev.type == "cuda"
+        self.disk = disk
         self.ring_elems = max(_host.CHUNK // 4, (ring_bytes // 4) // (_host.CHUNK // 4) * (_host.CHUNK // 4))
         self.manifest_timeout_s = manifest_timeout_s
-        self.mode = self._pick_mode(mode)
-        self._snap: Optional[torch.Tensor] = None  # device: [3, n] fp32; host: pinned [3, n]
+        self.layout = _layout(eng)
+        self.sig = hashlib.sha1(json.dumps(self.layout, sort_keys=True).encode()).hexdigest()[:16]
+        key = hashlib.sha1(self.save_dir.encode()).hexdigest()[:12]
+        self.shm_path = f"/dev/shm/dlgm-ckpt-{key}-r{self.rank}.snap"
+        self.shm_meta = self.shm_path[:-5] + ".json"
+        # restore reads the snapshot of the rank whose files restore this one (a ZeRO-0 twin reads its writer's)
+        self.src_rank = _source_rank(eng)
+        self.shm_src_path = f"/dev/shm/dlgm-ckpt-{key}-r{self.src_rank}.snap"
+        self.shm_src_meta = self.shm_src_path[:-5] + ".json"
+        self.mode = self._pick_mode(mode, shm)
+        self._snap: Optional[torch.Tensor] = None  # uint8 [14 n]: fp32 master | exp_avg | exp_avg_sq | bf16 params
+        self._pinned_shm = False
         self._ring: List[torch.Tensor] = []
         self._stream = torch.cuda.Stream(self.dev) if self.cuda else None
-        self._capture_ev: Optional[torch.cuda.Event] = None
+        self._capture_ev = None
         self._pending = 0
+        self._saves = 0
+        self._restart = os.environ.get("DLGM_RESTART", "0")
         self._plock = threading.Lock()
         self._q: "queue.Queue" = queue.Queue()
         self._errors: List[str] = []
         self.history: List[Dict[str, Any]] = []
+        self.rollbacks: List[str] = []
+        self.restored_from: Optional[str] = None
         self._thread = threading.Thread(target=self._writer, daemon=True, name="ckpt-writer")
         self._thread.start()
-        engine.pre_step_hooks.append(self._before_optimizer_step)
-        os.makedirs(save_dir, exist_ok=True)
+        eng.pre_step_hooks.append(self._before_optimizer_step)
+        os.makedirs(self.save_dir, exist_ok=True)
 
     # ------------------------------------------------------------------ policy
-    def _pick_mode(self, mode: str) -> str:
+    @property
+    def snap_bytes(self) -> int:
+        return 14 * self.n
+
+    def _pick_mode(self, mode: str, shm: Any) -> str:
+        if mode in ("device", "host", "shm"):
+            return mode
+        if not self.active:
+            return "host"
+        want_shm = shm is True or (shm == "auto" and self.cuda)
+        if want_shm and os.path.isdir("/dev/shm"):
+            st = os.statvfs("/dev/shm")
+            if st.f_bavail * st.f_frsize > self.snap_bytes + (8 << 30):
+                return "shm"
         if not self.cuda or getattr(self.engine, "offload", None) is not None:
             return "host"  # offloaded optimizer state already lives in host memory
-        if mode != "auto":
-            return mode
         free, _ = torch.cuda.mem_get_info(self.dev)
-        need = 3 * self.n * 4
-        return "device" if free > need + (24 << 30) else "host"
+        return "device" if free > self.snap_bytes + (24 << 30) else "host"
 
     def _before_optimizer_step(self, engine) -> None:
         # GPU-side ordering only: the next AdamW must not overwrite master/m/v before the capture read them
         if self._capture_ev is not None and self.cuda:
             torch.cuda.current_stream(self.dev).wait_event(self._capture_ev)
 
+    def _alloc_snapshot(self) -> None:
+        nb = self.snap_bytes
+        if self.mode == "shm":
+            fd = os.open(self.shm_path, os.O_RDWR | os.O_CREAT, 0o600)
+            try:
+                os.ftruncate(fd, nb)
+            finally:
+                os.close(fd)
+            self._snap = torch.from_file(self.shm_path, shared=True, size=nb, dtype=torch.uint8)
+            if self.cuda:
+                rc = torch.cuda.cudart().cudaHostRegister(self._snap.data_ptr(), nb, 0)
+                self._pinned_shm = int(rc) == 0
+        elif self.mode == "device":
+            self._snap = torch.empty(nb, dtype=torch.uint8, device=self.dev)
+            self._ring = [torch.empty(self.ring_elems, dtype=torch.float32, pin_memory=True) for _ in range(2)]
+        else:
+            self._snap = torch.empty(nb, dtype=torch.uint8, pin_memory=self.cuda)
+
+    def _views(self, snap: torch.Tensor) -> Dict[str, torch.Tensor]:
+        n = self.n
+        f = snap[:12 * n].view(torch.float32).view(3, n)
+        return {"master": f[0], "exp_avg": f[1], "exp_avg_sq": f[2], "bf16": snap[12 * n:14 * n].view(torch.bfloat16)}
+
     # ------------------------------------------------------------------ save
     def save(self, step: int, client_state: Optional[Dict[str, Any]] = None, blocking: bool = False) -> str:
         t0 = time.time()
+        tag = _tag(step)
+        self._saves += 1
         if not self.active:
-            return _tag(step)
+            return tag
         if self.busy:  # previous write-out still streaming from the snapshot buffer
             self.wait()
-        tag = _tag(step)
-        tmp = os.path.join(self.save_dir, tag + ".tmp")
-        os.makedirs(tmp, exist_ok=True)
-        eng = self.engine
-        srcs = [eng.master, eng.exp_avg, eng.exp_avg_sq]
+        save_id = f"{step}.{self._restart}.{self._saves}"
         if self._snap is None:
-            if self.mode == "device":
-                self._snap = torch.empty((3, self.n), dtype=torch.float32, device=self.dev)
-                self._ring = [torch.empty(self.ring_elems, dtype=torch.float32, pin_memory=True) for _ in range(2)]
-            else:
-                self._snap = torch.empty((3, self.n), dtype=torch.float32, pin_memory=self.cuda)
+            self._alloc_snapshot()
+        if self.mode == "shm" and os.path.exists(self.shm_meta):
+            os.unlink(self.shm_meta)  # the snapshot is about to change: never restore a torn one
+        eng = self.engine
+        v = self._views(self._snap)
+        srcs = [(v["master"], eng.master), (v["exp_avg"], eng.exp_avg), (v["exp_avg_sq"], eng.exp_avg_sq),
+                (v["bf16"], eng.p16_shard)]
         if self.cuda:
             cur = torch.cuda.current_stream(self.dev)
             self._stream.wait_stream(cur)
             with torch.cuda.stream(self._stream):
-                for i, s in enumerate(srcs):
-                    self._snap[i].copy_(s, non_blocking=True)
+                for dst, s in srcs:
+                    dst.copy_(s, non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(self._stream)
             self._capture_ev = ev
         else:
-            for i, s in enumerate(srcs):
-                self._snap[i].copy_(s)
+            for dst, s in srcs:
+                dst.copy_(s)
             ev = None
         meta = self._meta(step, client_state or {})
         with self._plock:
             self._pending += 1
-        self._q.put((tag, tmp, step, ev, meta, t0))
+        self._q.put((tag, step, save_id, ev, meta, t0))
         if blocking:
             self.wait()
         return tag
@@ -153,12 +263,16 @@ class AsyncCheckpointer:
         ecfg = {k: (str(v) if isinstance(v, torch.dtype) else list(v) if isinstance(v, tuple) else v)
                 for k, v in vars(eng.cfg).items()}
         groups = [{"name": g.name, "numel": g.numel, "shard_numel": g.shard_numel, "shard_off": g.shard_off,
-                   "params": [[s.name, g.layout[s.name][0], list(s.shape)] for s in g.specs]} for g in eng.groups]
-        return {"ds_version": "dlgm-mi355x-0.1", "global_steps": step, "dp_world_size": eng.W,
-                "partition_count": self.P, "zero_stage": eng.stage, "model_config": eng.mcfg.to_dict(),
-                "engine_config": ecfg, "groups": groups, "shard_total": self.n, "client_state": client_state,
-                "lr_scheduler": {"step": step}, "param_shapes": {g["name"]: {p[0]: p[2] for p in g["params"]}
-                                                                  for g in groups}}
+                   "kind": g.kind, "params": [[s.name, g.layout[s.name][0], list(s.shape)] for s in g.specs]}
+                  for g in eng.groups]
+        return {"ds_version": DS_VERSION, "global_steps": step, "global_samples": step * eng.cfg.micro_batch_size
+                * eng.cfg.grad_accum * eng.W, "dp_world_size": eng.W, "mp_world_size": 1,
+                "partition_count": eng.P, "zero_stage": eng.stage, "ep_size": eng.ep_size,
+                "model_config": eng.mcfg.to_dict(), "engine_config": ecfg, "groups": groups, "writers": self.writers,
+                "client_state": client_state, "lr_scheduler": {"last_batch_iteration": step},
+                "param_shapes": [{f"{g['name']}.{p[0]}": p[2] for p in g["params"]} for g in groups],
+                "buffer_names": [], "module": None,
+                "loss_scaler": ({"cur_scale": eng.scaler.scale} if eng.scaler is not None else None)}
 
     @property
     def busy(self) -> bool:
@@ -172,74 +286,131 @@ class AsyncCheckpointer:
         if self._errors:
             raise RuntimeError("checkpoint write failed: " + "; ".join(self._errors))
 
+    def wait_published(self, step: int, timeout_s: float = 600.0) -> bool:
+        """Block until tag `step` is complete on disk (published by rank 0) -- fault drills kill after this."""
+        t0 = time.time()
+        while time.time() - t0 < timeout_s:
+            if os.path.exists(os.path.join(self.save_dir, _tag(step), "COMPLETE")) or not self.disk:
+                return True
+            time.sleep(0.01)
+        return False
+
     def _writer(self) -> None:
         while True:
-            tag, tmp, step, ev, meta, t0 = self._q.get()
+            job = self._q.get()
             try:
-                self._write_one(tag, tmp, step, ev, meta, t0)
+                self._write_one(*job)
             except Exception as e:  # noqa: BLE001
-                self._errors.append(f"{tag}: {e}")
+                self._errors.append(f"{job[0]}: {type(e).__name__}: {e}")
             finally:
                 with self._plock:
                     self._pending -= 1
 
-    def _write_one(self, tag: str, tmp: str, step: int, ev, meta: Dict[str, Any], t0: float) -> None:
+    def _host_piece(self, src: torch.Tensor, off: int, ln: int, k: int) -> torch.Tensor:
+        """Elements [off, off+ln) of snapshot tensor `src` as a contiguous CPU tensor (device mode: via the ring)."""
+        if self.mode != "device":
+            return src[off:off + ln]
+        slot = self._ring[k % 2].view(torch.uint8)[:ln * src.element_size()].view(src.dtype)
+        with torch.cuda.stream(self._stream):
+            slot.copy_(src[off:off + ln], non_blocking=True)
+            e2 = torch.cuda.Event()
+            e2.record(self._stream)
+        e2.synchronize()  # this background thread only
+        return slot
+
+    def _stream_slot(self, w: PtWriter, name: str, src: torch.Tensor) -> None:
+        per = self.ring_elems * 4 // src.element_size()
+        for k, off in enumerate(range(0, src.numel(), per)):
+            ln = min(per, src.numel() - off)
+            w.write(name, self._host_piece(src, off, ln, k), off * src.element_size())
+
+    def _write_one(self, tag: str, step: int, save_id: str, ev, meta: Dict[str, Any], t0: float) -> None:
         if ev is not None:
             while not ev.query():
                 time.sleep(0.0005)
         t_cap = time.time()
-        prefix = _optim_prefix(self.rank)
-        files = {}
-        for i, name in enumerate(STATE):
-            fname = f"{prefix}.{name}.bin"
-            path = os.path.join(tmp, fname)
-            nbytes = self.n * 4
-            w = _host.StreamWriter(path, nbytes)
-            if self.mode == "device":
-                for k, off in enumerate(range(0, self.n, self.ring_elems)):
-                    ln = min(self.ring_elems, self.n - off)
-                    slot = self._ring[k % 2]
-                    with torch.cuda.stream(self._stream):
-                        slot[:ln].copy_(self._snap[i, off:off + ln], non_blocking=True)
-                        e2 = torch.cuda.Event()
-                        e2.record(self._stream)
-                    e2.synchronize()  # this background thread only
-                    w.write(slot[:ln], off * 4)
-            else:
-                w.write(self._snap[i], 0)
-            crcs = w.close(fsync=True)
-            files[fname] = {"bytes": nbytes, "chunk": _host.CHUNK, "crc": crcs, "algo": _host.algo(), "tensor": name}
-        torch.save({"rank": self.rank, "partition_count": self.P, "shard_numel": self.n, "files": sorted(files),
-                    "optimizer": {"type": "AdamW", "step": step}}, os.path.join(tmp, prefix + ".pt"))
-        if self.is_writer_rank0:
-            torch.save(meta, os.path.join(tmp, "mp_rank_00_model_states.pt"))
-        man = {"rank": self.rank, "partition_count": self.P, "step": step, "files": files}
+        v = self._views(self._snap)
+        rec: Dict[str, Any] = {"tag": tag, "step": step, "capture_s": t_cap - t0, "mode": self.mode,
+                               "bytes": self.snap_bytes}
+        if self.mode == "shm":
+            crcs = _host.crc32c_chunks(self._snap)
+            tmpm = self.shm_meta + ".tmp"
+            with open(tmpm, "w") as f:
+                json.dump({"save_dir": self.save_dir, "step": step, "save_id": save_id, "sig": self.sig,
+                           "bytes": self.snap_bytes, "crc": crcs, "algo": _host.algo(), "meta": meta}, f)
+            os.replace(tmpm, self.shm_meta)
+            rec["shm_s"] = time.time() - t_cap
+        if not self.disk:
+            self.history.append(rec)
+            return
+        tmp = os.path.join(self.save_dir, tag + ".tmp")
+        os.makedirs(tmp, exist_ok=True)
+        eng = self.engine
+        lay = self.layout
+        files: Dict[str, Dict[str, Any]] = {}
+        # optimizer states: DeepSpeed's ZeRO keys (fp32_flat_groups + the Adam state of the flat group)
+        optim = {"optimizer_state_dict": {
+            "zero_stage": eng.stage, "partition_count": eng.P, "loss_scaler": meta["loss_scaler"],
+            "dynamic_loss_scale": eng.scaler is not None and eng.scaler.dynamic, "overflow": False,
+            "fp32_flat_groups": [Slot("master", torch.float32, (self.n,))],
+            "optimizer_state_dict": {"state": {0: {"step": step, "exp_avg": Slot("exp_avg", torch.float32, (self.n,)),
+                                                   "exp_avg_sq": Slot("exp_avg_sq", torch.float32, (self.n,))}},
+                                     "param_groups": [{"lr": None, "betas": list(eng.cfg.betas), "eps": eng.cfg.eps,
+                                                       "weight_decay": eng.cfg.weight_decay, "params": [0]}]}},
+            "ds_config": meta["engine_config"], "ds_version": DS_VERSION, "dlgm_layout": lay}
+        path = os.path.join(tmp, optim_file(self.rank))
+        w = PtWriter(path, optim)
+        for name in STATE:
+            self._stream_slot(w, name, v[name])
+        files[optim_file(self.rank)] = w.close(fsync=True)
+        model = {"module": {}, "buffer_names": [], "param_shapes": meta["param_shapes"],
+                 "bf16_param_shard": Slot("bf16", torch.bfloat16, (self.n,)), "ds_version": DS_VERSION,
+                 "global_steps": step, "dp_world_size": eng.W, "mp_world_size": 1, "dlgm_layout": lay}
+        path = os.path.join(tmp, model_file(self.rank))
+        w = PtWriter(path, model)
+        self._stream_slot(w, "bf16", v["bf16"])
+        files[model_file(self.rank)] = w.close(fsync=True)
+        if self.is_rank0:
+            torch.save(meta, os.path.join(tmp, MODEL0))
+        man = {"rank": self.rank, "save_id": save_id, "step": step, "layout": lay, "files": files}
         mtmp = os.path.join(tmp, f".manifest_r{self.rank}.json")
         with open(mtmp, "w") as f:
             json.dump(man, f)
         os.replace(mtmp, os.path.join(tmp, f"manifest_r{self.rank}.json"))
-        rec = {"tag": tag, "step": step, "capture_s": t_cap - t0, "write_s": time.time() - t_cap,
-               "bytes": 3 * self.n * 4, "mode": self.mode}
-        if self.is_writer_rank0:
-            deadline = time.time() + self.manifest_timeout_s
-            while time.time() < deadline:
-                if all(os.path.exists(os.path.join(tmp, f"manifest_r{r}.json")) for r in range(self.P)):
-                    break
-                time.sleep(0.05)
-            else:
-                raise TimeoutError(f"{tag}: not all ranks wrote their manifests")
-            open(os.path.join(tmp, "COMPLETE"), "w").write(str(step))
-            final = os.path.join(self.save_dir, tag)
-            if os.path.exists(final):
-                shutil.rmtree(final)
-            os.replace(tmp, final)
-            ltmp = os.path.join(self.save_dir, ".latest.tmp")
-            with open(ltmp, "w") as f:
-                f.write(tag)
-            os.replace(ltmp, os.path.join(self.save_dir, "latest"))
-            self._prune()
+        rec["write_s"] = time.time() - t_cap
+        if self.is_rank0:
+            self._publish(tag, tmp, step, save_id)
             rec["published_s"] = time.time() - t0
         self.history.append(rec)
+
+    def _publish(self, tag: str, tmp: str, step: int, save_id: str) -> None:
+        deadline = time.time() + self.manifest_timeout_s
+        while time.time() < deadline:
+            ok = True
+            for r in self.writers:
+                p = os.path.join(tmp, f"manifest_r{r}.json")
+                try:
+                    with open(p) as f:
+                        ok = ok and json.load(f).get("save_id") == save_id
+                except (OSError, ValueError):
+                    ok = False
+                if not ok:
+                    break
+            if ok:
+                break
+            time.sleep(0.05)
+        else:
+            raise TimeoutError(f"{tag}: not every rank wrote its manifest for save {save_id}")
+        open(os.path.join(tmp, "COMPLETE"), "w").write(str(step))
+        final = os.path.join(self.save_dir, tag)
+        if os.path.exists(final):
+            shutil.rmtree(final)
+        os.replace(tmp, final)
+        ltmp = os.path.join(self.save_dir, ".latest.tmp")
+        with open(ltmp, "w") as f:
+            f.write(tag)
+        os.replace(ltmp, os.path.join(self.save_dir, "latest"))
+        self._prune()
 
     def _prune(self) -> None:
         tags = complete_tags(self.save_dir)
@@ -247,81 +418,249 @@ class AsyncCheckpointer:
             shutil.rmtree(os.path.join(self.save_dir, t), ignore_errors=True)
 
     # ------------------------------------------------------------------ restore
-    def load(self, tag: str = "auto", verify: bool = True) -> Optional[Dict[str, Any]]:
-        """Restore engine state; returns the client state (None when no checkpoint exists).
+    def _shm_step(self) -> int:
+        try:
+            with open(self.shm_src_meta) as f:
+                m = json.load(f)
+            if m.get("save_dir") == self.save_dir and m.get("sig") == self._src_sig() and \
+                    os.path.getsize(self.shm_src_path) >= m["bytes"]:
+                return int(m["step"])
+        except (OSError, ValueError, KeyError):
+            pass
+        return -1
 
-        ``tag="auto"``: newest complete tag whose files verify -- a corrupt or partial
-        newest tag is skipped (rolled back) with a warning recorded in ``self.rollbacks``.
-        """
-        self.rollbacks: List[str] = []
-        cands = [tag] if tag not in ("auto", "latest") else list(reversed(complete_tags(self.save_dir)))
-        for t in cands:
+    def load(self, tag: str = "auto", verify: bool = True) -> Optional[Dict[str, Any]]:
+        """Restore engine state; returns the client state (None when no checkpoint exists). Collective.
+
+        ``tag="auto"``: the newest candidate that loads and verifies on EVERY rank -- the shm snapshot tier
+        when all ranks hold the same newest step, else the disk tags newest first; a candidate that fails
+        on any rank is rolled back on all of them (recorded in ``self.rollbacks``)."""
+        self.rollbacks = []
+        agree = _Agree(self.engine)
+        auto = tag in ("auto", "latest")
+        disk = list(reversed(complete_tags(self.save_dir))) if auto else [tag]
+        newest_disk = int(TAG_RE.match(disk[0]).group(1)) if disk and TAG_RE.match(disk[0]) else -1
+        cands: List[Tuple[str, str]] = []
+        if auto:
+            s = self._shm_step()
+            lo, hi = agree.min(s), agree.max(s)
+            if lo >= 0 and lo == hi and lo >= newest_disk:
+                cands.append(("shm", _tag(int(lo))))
+        cands += [("disk", t) for t in disk]
+        for kind, t in cands:
+            err = ""
+            cs: Optional[Dict[str, Any]] = None
             try:
-                return self._load_tag(t, verify)
-            except (CorruptCheckpoint, FileNotFoundError, OSError, KeyError) as e:
-                self.rollbacks.append(f"{t}: {e}")
-                if tag not in ("auto", "latest"):
-                    raise
+                cs = self._load_shm() if kind == "shm" else self._load_tag(t, verify)
+            except (CorruptCheckpoint, FileNotFoundError, OSError, KeyError, ValueError, RuntimeError) as e:
+                err = f"{type(e).__name__}: {e}"
+            if agree.min(0.0 if err else 1.0) > 0:
+                self.engine.sync_params_from_master()
+                self.restored_from = f"{kind}:{t}"
+                return cs
+            self.rollbacks.append(f"{kind}:{t}: {err or 'failed on another rank'}")
+            if not auto:
+                raise CorruptCheckpoint(f"{t}: {err or 'failed on another rank'}")
         return None
+
+    def _src_sig(self) -> str:
+        lay = dict(self.layout, rank=self.src_rank)
+        return hashlib.sha1(json.dumps(lay, sort_keys=True).encode()).hexdigest()[:16]
+
+    def _load_shm(self) -> Dict[str, Any]:
+        with open(self.shm_src_meta) as f:
+            m = json.load(f)
+        snap = torch.from_file(self.shm_src_path, shared=False, size=m["bytes"], dtype=torch.uint8)
+        if m["algo"] == _host.algo() and _host.crc32c_chunks(snap) != m["crc"]:
+            raise CorruptCheckpoint("shm snapshot: checksum mismatch")
+        v = self._views(snap)
+        eng = self.engine
+        for name in STATE:
+            getattr(eng, name).copy_(v[name])
+        eng.step_count = int(m["meta"]["global_steps"])
+        return m["meta"].get("client_state", {})
 
     def _load_tag(self, tag: str, verify: bool) -> Dict[str, Any]:
         d = os.path.join(self.save_dir, tag)
         if not os.path.exists(os.path.join(d, "COMPLETE")):
             raise CorruptCheckpoint("missing COMPLETE marker")
-        meta = torch.load(os.path.join(d, "mp_rank_00_model_states.pt"), weights_only=True)
-        eng = self.engine
-        oldP = meta["partition_count"]
+        meta = torch.load(os.path.join(d, MODEL0), weights_only=True)
         mans = {}
-        for r in range(oldP):
+        for r in meta["writers"]:
             with open(os.path.join(d, f"manifest_r{r}.json")) as f:
                 mans[r] = json.load(f)
-            for fname, info in mans[r]["files"].items():
-                p = os.path.join(d, fname)
-                if os.path.getsize(p) != info["bytes"]:
-                    raise CorruptCheckpoint(f"{fname}: size mismatch")
-        if oldP == self.P and [g["numel"] for g in meta["groups"]] == [g.numel for g in eng.groups]:
-            buf = torch.empty(self.n, dtype=torch.float32, pin_memory=self.cuda)
-            prefix = _optim_prefix(self.rank)
+            for fname in mans[r]["files"]:
+                if not os.path.exists(os.path.join(d, fname)):
+                    raise CorruptCheckpoint(f"{fname}: missing")
+        src = _source_rank(self.engine)
+        old = mans.get(src)
+        same = old is not None and json.dumps(old["layout"], sort_keys=True) == json.dumps(
+            dict(self.layout, rank=src), sort_keys=True)
+        if same:
+            info = old["files"][optim_file(src)]
+            path = os.path.join(d, optim_file(src))
             for name in STATE:
-                fname = f"{prefix}.{name}.bin"
-                crcs = _host.read_tensor(os.path.join(d, fname), buf)
-                info = mans[self.rank]["files"][fname]
-                if verify and info["algo"] == _host.algo() and crcs != info["crc"]:
-                    raise CorruptCheckpoint(f"{fname}: checksum mismatch")
-                getattr(eng, name).copy_(buf, non_blocking=False)
+                self._read_into(path, info[name], getattr(self.engine, name), verify)
         else:
             self._reshard_from(d, meta, mans, verify)
-        eng.step_count = int(meta["global_steps"])
-        eng.sync_params_from_master()
+        self.engine.step_count = int(meta["global_steps"])
         return meta.get("client_state", {})
 
+    def _read_into(self, path: str, info: Dict[str, Any], dst: torch.Tensor, verify: bool) -> None:
+        """Stream one slot into `dst` (device or host) through a pinned ring, verifying chunk CRCs."""
+        n = dst.numel()
+        if info["bytes"] != n * 4:
+            raise CorruptCheckpoint(f"{os.path.basename(path)}: size mismatch")
+        per = self.ring_elems
+        ring = torch.empty(per, dtype=torch.float32, pin_memory=self.cuda)
+        check = verify and info.get("algo") == _host.algo()
+        for off in range(0, n, per):
+            ln = min(per, n - off)
+            crcs = read_slot(path, ring[:ln], info["offset"] + off * 4)
+            first = off * 4 // _host.CHUNK
+            if check and crcs != info["crc"][first:first + len(crcs)]:
+                raise CorruptCheckpoint(f"{os.path.basename(path)}: checksum mismatch")
+            dst[off:off + ln].copy_(ring[:ln], non_blocking=False)
+
     def _reshard_from(self, d: str, meta: Dict[str, Any], mans: Dict[int, Any], verify: bool) -> None:
-        """Elastic restore: rebuild this rank's shards from the old world's shard files."""
+        """Elastic restore: rebuild this rank's shards from a checkpoint written under another layout."""
+        src = ShardSource(d, mans, verify)
         eng = self.engine
-        oldP = meta["partition_count"]
-        old_groups = {g["name"]: g for g in meta["groups"]}
+        ep_rank = self.layout["ep_rank"]
         for name in STATE:
-            maps = [np.memmap(os.path.join(d, f"{_optim_prefix(r)}.{name}.bin"), dtype=np.float32, mode="r")
-                    for r in range(oldP)]
             dst = getattr(eng, name)
             for g in eng.groups:
-                og = old_groups[g.name]
-                full = np.zeros(g.numel, dtype=np.float32)
-                n = min(og["numel"], g.numel)
-                pos = 0
-                for r in range(oldP):
-                    seg = maps[r][og["shard_off"]:og["shard_off"] + og["shard_numel"]]
-                    take = max(0, min(len(seg), n - pos))
-                    full[pos:pos + take] = seg[:take]
-                    pos += len(seg)
-                r0 = (eng.rank if self.P > 1 else 0) * g.shard_numel
+                full = src.assemble(g.name, g.kind, [(s.name, g.layout[s.name][0], list(s.shape), int(s.experts))
+                                                     for s in g.specs], g.numel, name, ep_rank)
+                r0 = (g.comm.rank if g.P > 1 else 0) * g.shard_numel
                 dst.narrow(0, g.shard_off, g.shard_numel).copy_(torch.from_numpy(full[r0:r0 + g.shard_numel]))
-            del maps
 
-    def close(self) -> None:
+    def discard_shm(self) -> None:
+        """Drop the host-RAM snapshot tier (after a clean finish: nothing to resume)."""
+        for p in (self.shm_meta, self.shm_path):
+            try:
+                os.unlink(p)
+            except OSError:
+                pass
+
+    def close(self, discard_shm: bool = False) -> None:
         self.wait()
         if self._before_optimizer_step in self.engine.pre_step_hooks:
             self.engine.pre_step_hooks.remove(self._before_optimizer_step)
+        if self._pinned_shm and self._snap is not None:
+            torch.cuda.cudart().cudaHostUnregister(self._snap.data_ptr())
+            self._pinned_shm = False
+        self._snap = None
+        if discard_shm:
+            self.discard_shm()
+
+
+class ShardSource:
+    """Old shard files of one checkpoint tag, memory-mapped; reassembles groups under any new layout.
+
+    Dense groups are the concatenation of the old partition ranks' shards. Expert groups are rebuilt
+    expert by expert: global expert j lived on old EP rank j // E_local_old (sharded over that EP
+    position's expert-data-parallel ranks), so a new EP size just re-slices the global expert list."""
+
+    def __init__(self, d: str, mans: Dict[int, Any], verify: bool = True):
+        self.d, self.verify = d, verify
+        self.mans = {int(r): m for r, m in mans.items()}
+        self._maps: Dict[Tuple[int, str], np.ndarray] = {}
+        self._verified: set = set()
+        any_lay = next(iter(self.mans.values()))["layout"]
+        self.W, self.stage, self.ep = any_lay["world"], any_lay["zero_stage"], any_lay["ep_size"]
+
+    def _map(self, rank: int, state: str) -> np.ndarray:
+        key = (rank, state)
+        if key not in self._maps:
+            info = self.mans[rank]["files"][optim_file(rank)][state]
+            path = os.path.join(self.d, optim_file(rank))
+            mm = np.memmap(path, dtype=np.float32, mode="r", offset=info["offset"], shape=(info["bytes"] // 4,))
+            if self.verify and info.get("algo") == _host.algo() and key not in self._verified:
+                ch = _host.CHUNK // 4
+                got = [_host.crc32c_chunks(torch.from_numpy(np.array(mm[i:i + ch])))[0]
+                       for i in range(0, mm.shape[0], ch)]
+                if got != info["crc"][:len(got)]:
+                    raise CorruptCheckpoint(f"{optim_file(rank)}:{state}: checksum mismatch")
+                self._verified.add(key)
+            self._maps[key] = mm
+        return self._maps[key]
+
+    def _group(self, rank: int, gname: str) -> Dict[str, Any]:
+        for g in self.mans[rank]["layout"]["groups"]:
+            if g["name"] == gname:
+                return g
+        raise KeyError(f"group {gname} not in rank {rank}'s checkpoint")
+
+    def _old_flat(self, gname: str, state: str, ranks: List[int]) -> np.ndarray:
+        """Full flat segment of group `gname` from the shards of `ranks` (in partition order)."""
+        parts = []
+        for r in ranks:
+            g = self._group(r, gname)
+            parts.append(self._map(r, state)[g["shard_off"]:g["shard_off"] + g["shard_numel"]])
+        return np.concatenate(parts) if len(parts) > 1 else np.asarray(parts[0])
+
+    def _holders(self, gname: str, kind: str, ep_rank: int) -> List[int]:
+        """Old writer ranks holding group `gname` (for experts: of old EP position ep_rank), partition order."""
+        if kind != "expert" or self.ep == 1:
+            if self.stage == 0:
+                return [0]
+            return sorted(self.mans, key=lambda r: self._group(r, gname)["prank"])
+        rs = [r for r in self.mans if self.mans[r]["layout"]["ep_rank"] == ep_rank]
+        return sorted(rs, key=lambda r: self._group(r, gname)["prank"])
+
+    def assemble(self, gname: str, kind: str, params: List[Any], numel: int, state: str,
+                 new_ep_rank: int = 0) -> np.ndarray:
+        """The new full flat segment (numel elements) of group `gname` for new EP position `new_ep_rank`."""
+        full = np.zeros(numel, dtype=np.float32)
+        if kind != "expert":
+            old = self._old_flat(gname, state, self._holders(gname, kind, 0))
+            ref = self._group(self._holders(gname, kind, 0)[0], gname)
+            old_off = {p[0]: p[1] for p in ref["params"]}
+            for name, off, shape, _ in params:
+                n = math.prod(shape)
+                full[off:off + n] = old[old_off[name]:old_off[name] + n]
+            return full
+        cache: Dict[int, Tuple[np.ndarray, Dict[str, Any]]] = {}
+        for name, off, shape, el_new in params:
+            el_new = el_new or shape[0]
+            per = math.prod(shape[1:])
+            for k in range(el_new):
+                j = new_ep_rank * el_new + k  # global expert id
+                ref0 = self._group(next(iter(self.mans)), gname)
+                el_old = next(p[3] or p[2][0] for p in ref0["params"] if p[0] == name)
+                eo, lj = divmod(j, el_old)
+                if eo not in cache:
+                    holders = self._holders(gname, kind, eo)
+                    if not holders:
+                        raise CorruptCheckpoint(f"{gname}: no shard of old EP rank {eo}")
+                    cache[eo] = (self._old_flat(gname, state, holders), self._group(holders[0], gname))
+                old, og = cache[eo]
+                ooff = next(p[1] for p in og["params"] if p[0] == name)
+                full[off + k * per:off + (k + 1) * per] = old[ooff + lj * per:ooff + (lj + 1) * per]
+        return full
+
+    def consolidate(self, groups: List[Dict[str, Any]], state: str = "master") -> Dict[str, np.ndarray]:
+        """Full named tensors (experts concatenated in global order) from the checkpoint alone."""
+        out: Dict[str, np.ndarray] = {}
+        for g in groups:
+            if g.get("kind", "dense") != "expert" or self.ep == 1:
+                holders = self._holders(g["name"], "dense", 0)
+                flat = self._old_flat(g["name"], state, holders)
+                for name, off, shape in (p[:3] for p in g["params"]):
+                    out[f"{g['name']}.{name}"] = np.array(flat[off:off + math.prod(shape)]).reshape(shape)
+                continue
+            per_ep = []
+            for eo in range(self.ep):
+                holders = self._holders(g["name"], "expert", eo)
+                per_ep.append((self._old_flat(g["name"], state, holders), self._group(holders[0], g["name"])))
+            for name, _, shape in (p[:3] for p in g["params"]):
+                pieces = []
+                for flat, og in per_ep:
+                    ooff, oshape = next((p[1], p[2]) for p in og["params"] if p[0] == name)
+                    pieces.append(np.array(flat[ooff:ooff + math.prod(oshape)]).reshape(oshape))
+                out[f"{g['name']}.{name}"] = np.concatenate(pieces)
+        return out
 
 
 def complete_tags(save_dir: str) -> List[str]:

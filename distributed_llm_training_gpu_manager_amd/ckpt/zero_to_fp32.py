@@ -4,14 +4,16 @@ DeepSpeed ships ``zero_to_fp32.py`` inside every checkpoint directory for this j
 "plus ``zero_to_fp32.py`` recovery"); this is the equivalent for the layout written by
 :class:`ckpt.checkpoint.AsyncCheckpointer`::
 
-    <save_dir>/<tag>/mp_rank_00_model_states.pt                               meta (weights_only)
-    <save_dir>/<tag>/zero_pp_rank_{r}_mp_rank_00_optim_states.master.bin       rank r's fp32 shards
+    <save_dir>/<tag>/mp_rank_00_model_states.pt                      meta (torch.load weights_only)
+    <save_dir>/<tag>/zero_pp_rank_{r}_mp_rank_00_optim_states.pt      rank r's fp32 shards (torch.save zip)
+    <save_dir>/<tag>/manifest_r{r}.json                               where each record's bytes start
 
-Each flat group (one transformer block, the embedding, the head) is partitioned in P equal
-shards; rank r's file holds its shard of every group at the group's ``shard_off``. The full group
-is the concatenation of the P shards, and each parameter sits at its recorded offset inside it.
-The shard files are memory-mapped, so consolidating a 70B checkpoint needs host memory for one
-group at a time plus the output.
+Each flat group (one transformer block, the embedding, the head) is partitioned in P equal shards; the
+full group is the concatenation of the P shards and each parameter sits at its recorded offset inside
+it. Expert groups (Mixtral, EP > 1) are concatenated over the EP ranks in global expert order, which is
+what ``ZeroEngine.full_params()`` returns. The shard records are memory-mapped straight out of the
+``.pt`` zips (they are stored, 64-byte aligned), so consolidating a 70B checkpoint needs host memory for
+one group at a time plus the output.
 
     python -m distributed_llm_training_gpu_manager_amd.ckpt.zero_to_fp32 <save_dir> out.safetensors \\
         [--tag global_step120] [--dtype bf16]
@@ -20,15 +22,13 @@ from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
 import sys
 from typing import Dict, Optional
 
-import numpy as np
 import torch
 
-from .checkpoint import STATE, _optim_prefix, complete_tags
+from .checkpoint import MODEL0, STATE, ShardSource, complete_tags
 
 
 def _resolve_tag(save_dir: str, tag: Optional[str]) -> str:
@@ -49,21 +49,13 @@ def consolidate(save_dir: str, tag: Optional[str] = None, state: str = "master",
     """Full parameters (or an optimizer moment, ``state`` = exp_avg / exp_avg_sq) of one checkpoint."""
     assert state in STATE, state
     d = os.path.join(save_dir, _resolve_tag(save_dir, tag))
-    meta = torch.load(os.path.join(d, "mp_rank_00_model_states.pt"), weights_only=True)
-    ep = int(meta.get("engine_config", {}).get("expert_parallel_size", 1) or 1)
-    if ep > 1:
-        raise NotImplementedError("expert-parallel checkpoints hold different experts per EP rank; "
-                                  "consolidate them through ZeroEngine.full_params() under the same EP size")
-    P = int(meta["partition_count"])
-    maps = [np.memmap(os.path.join(d, f"{_optim_prefix(r)}.{state}.bin"), dtype=np.float32, mode="r")
-            for r in range(P)]
-    out: Dict[str, torch.Tensor] = {}
-    for g in meta["groups"]:
-        full = np.concatenate([m[g["shard_off"]:g["shard_off"] + g["shard_numel"]] for m in maps])
-        for name, off, shape in g["params"]:
-            n = math.prod(shape)
-            out[f"{g['name']}.{name}"] = torch.from_numpy(np.array(full[off:off + n])).view(*shape).to(dtype)
-    return out
+    meta = torch.load(os.path.join(d, MODEL0), weights_only=True)
+    mans = {}
+    for r in meta["writers"]:
+        with open(os.path.join(d, f"manifest_r{r}.json")) as f:
+            mans[r] = json.load(f)
+    src = ShardSource(d, mans, verify=False)
+    return {k: torch.from_numpy(v).to(dtype) for k, v in src.consolidate(meta["groups"], state).items()}
 
 
 def main(argv=None) -> int:

@@ -120,6 +120,8 @@ class Trainer:
         self.mcfg = get_config(args.model, **over)
         if args.deepspeed_config:
             self.ecfg, self.notes = engine_config_from_ds(args.deepspeed_config, args.seq_len, seed=args.seed)
+            with open(args.deepspeed_config) as f:
+                self._ds_elastic = bool(json.load(f).get("elasticity", {}).get("enabled", False))
         else:
             self.ecfg, self.notes = EngineConfig(zero_stage=args.zero_stage, micro_batch_size=args.micro_batch,
                                                  seq_len=args.seq_len, grad_accum=args.grad_accum, lr=args.lr,
@@ -140,11 +142,14 @@ class Trainer:
             self.ecfg.hip_graphs = True
         if args.halt_on_nan and not self.ecfg.fp16:
             self.ecfg.nan_latch = True  # the host runs one step ahead of the NaN decision (see NanTrap)
+        self.global_batch = self._elastic_batch(args)
+        save_dir = args.save_dir or os.environ.get("DLGM_SAVE_DIR")
         self.engine = ZeroEngine(self.mcfg, self.ecfg, self.env.device, self.comm)
         self.monitor = LossSpikeMonitor(MonitorConfig())
         self.trap = NanTrap(self.env.device, self.monitor)
-        save_dir = args.save_dir or os.environ.get("DLGM_SAVE_DIR")
-        self.ckpt = AsyncCheckpointer(self.engine, save_dir, mode=args.ckpt_mode) if save_dir else None
+        shm = {"auto": "auto", "on": True, "off": False}[args.ckpt_shm]
+        self.ckpt = AsyncCheckpointer(self.engine, save_dir, mode=args.ckpt_mode, keep_last=args.keep_last, shm=shm,
+                                      disk=bool(args.ckpt_disk)) if save_dir else None
         self.data = SyntheticData(self.mcfg.vocab_size, self.ecfg.micro_batch_size, args.seq_len,
                                   self.ecfg.grad_accum, args.seed, self.env.rank // self.sp, self.env.device,
                                   sp_rank=self.env.rank % self.sp, sp_size=self.sp)
@@ -157,6 +162,29 @@ class Trainer:
 
     def _on_preempt(self, signum, frame) -> None:
         self.preempt = True
+
+    def _elastic_batch(self, args) -> int:
+        """Elastic training (DeepSpeed ``elasticity`` block, reference ``deepspeed_launcher.py:78, 226-238``):
+        the global batch of the first launch is kept across restarts at other world sizes by rescaling the
+        gradient accumulation; the number travels in the checkpoint's client state."""
+        e = self.ecfg
+        dp = max(1, self.env.world // max(1, e.sequence_parallel_size))
+        gb = e.micro_batch_size * e.grad_accum * dp
+        elastic = getattr(args, "elastic", False) or bool(getattr(self, "_ds_elastic", False))
+        save_dir = args.save_dir or os.environ.get("DLGM_SAVE_DIR")
+        if not elastic or not save_dir or args.resume in ("none", ""):
+            return gb
+        from ..ckpt.checkpoint import MODEL0, complete_tags
+        tags = complete_tags(save_dir)
+        if tags:
+            meta = torch.load(os.path.join(save_dir, tags[-1], MODEL0), weights_only=True)
+            gb = int(meta.get("client_state", {}).get("global_batch", gb))
+        ga = max(1, round(gb / (e.micro_batch_size * dp)))
+        if ga != e.grad_accum:
+            self.notes.append(f"elastic: world {self.env.world} -> grad_accum {e.grad_accum} -> {ga} "
+                              f"(global batch {gb}{'' if ga * e.micro_batch_size * dp == gb else ' not divisible: now ' + str(ga * e.micro_batch_size * dp)})")
+            e.grad_accum = ga
+        return ga * e.micro_batch_size * dp
 
     def _say(self, msg: str) -> None:
         if self.env.rank == 0:
@@ -203,7 +231,8 @@ class Trainer:
         if rec["preempt"]:
             t0 = time.time()
             if self.ckpt is not None:
-                self.ckpt.save(last_issued, client_state={"step": last_issued, "preempted": True}, blocking=True)
+                self.ckpt.save(last_issued, client_state={"step": last_issued, "preempted": True,
+                                                                 "global_batch": self.global_batch}, blocking=True)
             self._say(f"preemption: emergency checkpoint at step {last_issued} in {time.time() - t0:.2f}s; exiting")
             return EXIT_PREEMPTED
         return None
@@ -216,7 +245,7 @@ class Trainer:
             cs = self.ckpt.load("auto" if a.resume in ("auto", "latest") else a.resume)
             if cs is not None:
                 start = int(cs.get("step", self.engine.step_count))
-                self._say(f"resumed from step {start} in {time.time() - t0:.2f}s "
+                self._say(f"resumed from step {start} in {time.time() - t0:.2f}s via {self.ckpt.restored_from} "
                           f"(rollbacks: {getattr(self.ckpt, 'rollbacks', [])})")
                 self.monitor.reset()
         for n in self.notes:
@@ -255,12 +284,15 @@ class Trainer:
                 if stop is not None:
                     rc = stop
                     break
-                self.ckpt.save(step, client_state={"step": step})
+                self.ckpt.save(step, client_state={"step": step, "global_batch": self.global_batch})
             else:
                 prev = (step, issued)
-            if a.kill_at_step == step and first_attempt and self.env.rank == 0:
-                if self.ckpt is not None:
-                    self.ckpt.wait()  # the drill kills after the last interval checkpoint is durable
+            if a.kill_at_step == step and first_attempt and self.env.rank == a.kill_rank:
+                if self.ckpt is not None:  # the drill kills after the last interval checkpoint is published
+                    self.ckpt.wait()
+                    last_saved = step - step % a.save_interval if a.save_interval > 0 else 0
+                    if last_saved > 0:
+                        self.ckpt.wait_published(last_saved)
                 os.kill(os.getpid(), signal.SIGKILL)
             if a.preempt_at_step == step and first_attempt:
                 os.kill(os.getpid(), signal.SIGUSR1)
@@ -275,7 +307,8 @@ class Trainer:
                         break
                 t0 = time.time()
                 if self.ckpt is not None:
-                    self.ckpt.save(step, client_state={"step": step, "preempted": True}, blocking=True)
+                    self.ckpt.save(step, client_state={"step": step, "preempted": True,
+                                                          "global_batch": self.global_batch}, blocking=True)
                 self._say(f"preemption: emergency checkpoint at step {step} in {time.time() - t0:.2f}s; exiting")
                 rc = EXIT_PREEMPTED
                 break
@@ -285,12 +318,15 @@ class Trainer:
         if rc == 0 and self.preempt and self.env.world == 1:
             # a notice that arrived after the last step was queued (one rank: no agreement needed)
             if self.ckpt is not None:
-                self.ckpt.save(last, client_state={"step": last, "preempted": True}, blocking=True)
+                self.ckpt.save(last, client_state={"step": last, "preempted": True,
+                                                      "global_batch": self.global_batch}, blocking=True)
             rc = EXIT_PREEMPTED
         if self.ckpt is not None:
             self.ckpt.wait()
             if rc == 0 and a.export:
                 export_consolidated(self.engine, a.export)
+            # a finished job has nothing to resume: give the host RAM of the shm snapshot tier back
+            self.ckpt.close(discard_shm=rc == 0)
         self.trap.close()
         self.pusher.close()
         if a.log_json and self.env.rank == 0:
@@ -320,12 +356,19 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--save-dir", default=None)
     ap.add_argument("--save-interval", type=int, default=0)
-    ap.add_argument("--ckpt-mode", default="auto", choices=["auto", "device", "host"])
+    ap.add_argument("--ckpt-mode", default="auto", choices=["auto", "device", "host", "shm"])
+    ap.add_argument("--ckpt-shm", default="auto", choices=["auto", "on", "off"],
+                    help="/dev/shm snapshot tier (outlives a SIGKILLed rank; restored first on auto-resume)")
+    ap.add_argument("--ckpt-disk", type=int, default=1, help="0: snapshot tier only, no disk tags")
+    ap.add_argument("--keep-last", type=int, default=3, help="complete disk tags kept")
+    ap.add_argument("--elastic", action="store_true",
+                    help="keep the first launch's global batch across restarts at other world sizes")
     ap.add_argument("--resume", default="none")
     ap.add_argument("--export", default=None, help="consolidated bf16 safetensors at the end (16-bit gather on save)")
     ap.add_argument("--inject-nan-step", type=int, default=-1)
     ap.add_argument("--kill-at-step", type=int, default=-1, help="fault drill: SIGKILL this rank after the step "
                     "(first attempt only)")
+    ap.add_argument("--kill-rank", type=int, default=0, help="rank the SIGKILL drill kills")
     ap.add_argument("--preempt-at-step", type=int, default=-1, help="spot drill: deliver SIGUSR1 after the step")
     ap.add_argument("--halt-on-nan", type=int, default=1)
     ap.add_argument("--metrics-url", default=os.environ.get("DLGM_METRICS_URL"))

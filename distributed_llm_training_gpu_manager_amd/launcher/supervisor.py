@@ -10,11 +10,19 @@ and the README's auto-resume claim (``README.md:14``) has no implementation. Her
 * stdout/stderr go to ``<run_dir>/job.log`` (no pipes to fill up);
 * the training ranks publish progress to ``<run_dir>/status.json``
   (``DLGM_STATUS_FILE``): a stale heartbeat is treated like a crash;
-* on a non-zero exit (SIGKILL'd rank, NaN halt = exit code 3, hang) the supervisor
-  relaunches the job with ``--resume=auto`` (the engine rolls back to the newest
-  checkpoint tag whose manifest verifies) up to ``max_restarts`` times, and records
+* on a non-zero exit (SIGKILL'd rank, hang) the supervisor relaunches the job with
+  ``--resume=auto`` (the engine rolls back to the newest checkpoint -- /dev/shm snapshot
+  tier first -- that verifies on every rank) up to ``max_restarts`` times, and records
   MTTR = time of the first completed step after the restart - time the failure was
-  detected.
+  detected (SURVEY.md §5.3);
+* a NaN halt (exit code 3) is retried ``max_nan_restarts`` times with the learning rate
+  scaled by ``nan_lr_backoff`` (the loss monitor's remediation, ``loss_monitor.py:135``:
+  "Restore from last checkpoint and retry with lower LR"); the same data would otherwise
+  hit the same NaN again, so a repeated halt ends the job as ``nan_halt``;
+* elastic jobs (``elastic=True``; DeepSpeed ``elasticity`` block, reference
+  ``deepspeed_launcher.py:78, 226-238``) relaunch at the largest world size that fits the
+  healthy GPUs and divides the global batch; the trainer rescales gradient accumulation and
+  the checkpoint reshards (``ckpt.checkpoint.ShardSource``).
 """
 from __future__ import annotations
 
@@ -44,6 +52,14 @@ class JobSpec:
     heartbeat_timeout_s: float = 0.0  # 0 = disabled
     resume_arg: str = "--resume=auto"
     restart_on_preempt: bool = False
+    max_nan_restarts: int = 1
+    nan_lr_backoff: float = 0.5
+    # elastic relaunch: world sizes in [min_world, max_world] with global_batch % (micro_batch * w) == 0
+    elastic: bool = False
+    min_world: int = 1
+    max_world: int = 0
+    global_batch: int = 0
+    micro_batch: int = 1
 
 
 class Job:
@@ -59,6 +75,9 @@ class Job:
         self.exit_codes: List[int] = []
         self.events: List[Dict] = []
         self.mttr_s: List[float] = []
+        self.world_history: List[int] = []
+        self.nan_halts = 0
+        self.lr_scale = 1.0
         self.created = time.time()
         self.ended: Optional[float] = None
         self._proc: Optional[subprocess.Popen] = None
@@ -81,6 +100,7 @@ class Job:
             "job_id": self.spec.job_id, "status": self.status, "pid": self.pid, "restarts": self.restarts,
             "exit_codes": list(self.exit_codes), "log_path": self.log_path, "run_dir": self.run_dir,
             "mttr_s": list(self.mttr_s), "events": list(self.events[-50:]), "progress": self.progress(),
+            "world_history": list(self.world_history), "nan_halts": self.nan_halts, "lr_scale": self.lr_scale,
             "command": self.spec.argv, "created": self.created, "ended": self.ended,
         }
 
@@ -92,11 +112,57 @@ class Supervisor(threading.Thread):
         self.poll_s = poll_s
         self._first = first_proc
 
+    @staticmethod
+    def nproc_of(argv: List[str]) -> Optional[int]:
+        for i, a in enumerate(argv):
+            for key in ("--nproc-per-node", "--nproc_per_node"):
+                if a == key and i + 1 < len(argv):
+                    return int(argv[i + 1])
+                if a.startswith(key + "="):
+                    return int(a.split("=", 1)[1])
+        return None
+
+    @staticmethod
+    def with_nproc(argv: List[str], n: int) -> List[str]:
+        out = list(argv)
+        for i, a in enumerate(out):
+            for key in ("--nproc-per-node", "--nproc_per_node"):
+                if a == key and i + 1 < len(out):
+                    out[i + 1] = str(n)
+                    return out
+                if a.startswith(key + "="):
+                    out[i] = f"{key}={n}"
+                    return out
+        raise ValueError("elastic job argv has no --nproc-per-node")
+
+    def available_world(self, current: int) -> int:
+        """Ranks the next attempt can use: an operator / health monitor may write the count to
+        <run_dir>/available_world; otherwise one GPU is assumed lost with the failed rank."""
+        p = os.path.join(self.job.run_dir, "available_world")
+        try:
+            with open(p) as f:
+                return int(f.read().strip())
+        except (OSError, ValueError):
+            return max(1, current - 1)
+
+    def elastic_world(self, current: int) -> int:
+        spec = self.job.spec
+        avail = min(self.available_world(current), spec.max_world or current)
+        gb = spec.global_batch or 0
+        for w in range(avail, spec.min_world - 1, -1):
+            if not gb or gb % (spec.micro_batch * w) == 0:
+                return w
+        return 0
+
     def _start(self, resume: bool) -> subprocess.Popen:
         spec = self.job.spec
         argv = list(spec.argv)
+        if self.job.world_history and self.nproc_of(argv) is not None:
+            argv = self.with_nproc(argv, self.job.world_history[-1])
         if resume and spec.resume_arg not in argv:
             argv.append(spec.resume_arg)
+        if self.job.lr_scale != 1.0:
+            argv += ["--lr-scale", str(self.job.lr_scale)]
         env = {**os.environ, **spec.env, "DLGM_STATUS_FILE": self.job.status_path, "DLGM_JOB_ID": spec.job_id,
                "DLGM_RESTART": str(self.job.restarts)}
         if spec.save_dir:
@@ -129,6 +195,9 @@ class Supervisor(threading.Thread):
 
     def run(self) -> None:
         job, spec = self.job, self.job.spec
+        w0 = self.nproc_of(spec.argv)
+        if w0 is not None:
+            job.world_history.append(w0)
         proc = self._first if self._first is not None else self._start(resume=False)
         failure_t: Optional[float] = None
         step_at_failure = -1
@@ -165,6 +234,14 @@ class Supervisor(threading.Thread):
             if preempted and not spec.restart_on_preempt:
                 job.status = "preempted"
                 break
+            nan = rc == EXIT_NAN_HALT
+            if nan:
+                job.nan_halts += 1
+                if job.nan_halts > spec.max_nan_restarts:
+                    job.status = "nan_halt"
+                    job.event("nan_halt", halts=job.nan_halts)
+                    break
+                job.lr_scale *= spec.nan_lr_backoff
             if spec.auto_resume and job.restarts < spec.max_restarts:
                 # make sure no straggler rank of the failed attempt survives
                 try:
@@ -173,9 +250,17 @@ class Supervisor(threading.Thread):
                     pass
                 failure_t = time.time()
                 step_at_failure = (prog or {}).get("step", -1)
+                if spec.elastic and not nan and job.world_history:
+                    w = self.elastic_world(job.world_history[-1])
+                    if w < 1:
+                        job.status = "failed"
+                        job.event("elastic_no_valid_world", last=job.world_history[-1])
+                        break
+                    job.world_history.append(w)
                 job.restarts += 1
                 job.status = "restarting"
-                job.event("restarting", attempt=job.restarts, reason="nan_halt" if rc == EXIT_NAN_HALT else "crash")
+                job.event("restarting", attempt=job.restarts, reason="nan_halt" if nan else "crash",
+                          world=job.world_history[-1] if job.world_history else None, lr_scale=job.lr_scale)
                 proc = self._start(resume=True)
                 attempt_t0 = time.time()
                 continue
@@ -272,11 +357,19 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--heartbeat-timeout", type=float, default=0.0)
     ap.add_argument("--restart-on-preempt", action="store_true")
     ap.add_argument("--no-auto-resume", action="store_true")
+    ap.add_argument("--max-nan-restarts", type=int, default=1)
+    ap.add_argument("--elastic", action="store_true", help="relaunch at a smaller world size after a rank failure")
+    ap.add_argument("--min-world", type=int, default=1)
+    ap.add_argument("--max-world", type=int, default=0)
+    ap.add_argument("--global-batch", type=int, default=0)
+    ap.add_argument("--micro-batch", type=int, default=1)
     a = ap.parse_args(argv[:cut])
     cmd = argv[cut + 1:]
     spec = JobSpec(job_id=a.job_id, argv=cmd, auto_resume=not a.no_auto_resume, max_restarts=a.max_restarts,
                    save_dir=a.save_dir, run_dir=a.run_dir, heartbeat_timeout_s=a.heartbeat_timeout,
-                   restart_on_preempt=a.restart_on_preempt)
+                   restart_on_preempt=a.restart_on_preempt, max_nan_restarts=a.max_nan_restarts,
+                   elastic=a.elastic, min_world=a.min_world, max_world=a.max_world, global_batch=a.global_batch,
+                   micro_batch=a.micro_batch)
     job = Job(spec)
     sup = Supervisor(job)
     for sig in (signal.SIGTERM, signal.SIGINT):

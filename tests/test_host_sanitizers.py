@@ -20,7 +20,7 @@ def test_host_runtime_asan_ubsan(tmp_path):
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
            "-fno-sanitize-recover=all", "-fopenmp", "-mavx2", "-mfma", "-msse4.2",
            os.path.join(ROOT, "tests", "native", "host_runtime_test.cpp"),
-           os.path.join(ROOT, "csrc", "host", "ckpt_io.cpp"), "-o", exe, "-lpthread"]
+           os.path.join(ROOT, "csrc", "host", "ckpt_io.cpp"), "-o", exe, "-lpthread", "-lz"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     # verify_asan_link_order=0: the environment may preload its own (non-allocator) library first

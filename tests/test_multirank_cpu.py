@@ -1,0 +1,427 @@
+"""World sizes 4 and 8 on CPU/gloo: the configurations the 8-GPU driver run and
+BASELINE configs 3-5 exercise, checked against single-process training before they meet RCCL.
+
+* ZeRO-1/2/3 at W=4 (local gradient accumulation on and off) and ZeRO-3 at W=8;
+* ZeRO-3 non-resident (max_live_parameters = 0: per-micro-batch gathers and reduce-scatters, the 70B path);
+* Mixtral EP=4 and EP=8 (one expert per rank) including experts that receive no tokens;
+* checkpoints: W=8 -> W=4 / W=2 resharding, EP=4 -> EP=2, a corrupt shard on ONE rank rolls every
+  rank back to the same tag, the /dev/shm snapshot tier, torch.load(weights_only=True) of every file;
+* elastic relaunch: one of four ranks SIGKILLed -> the supervisor restarts at world 2 and the run finishes.
+"""
+import json
+import os
+import socket
+import sys
+import time
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from distributed_llm_training_gpu_manager_amd.models import get_config
+from distributed_llm_training_gpu_manager_amd.parallel.comm import Comm
+from distributed_llm_training_gpu_manager_amd.parallel.zero import EngineConfig, ZeroEngine
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _model(name):
+    if name == "mixtral-8e":
+        import dataclasses
+        return dataclasses.replace(get_config("mixtral-tiny"), n_experts=8, name="mixtral-8e")
+    return get_config(name)
+
+
+def _data(model, steps, n_micro, seq=32, mbs=2, seed=11):
+    mc = _model(model)
+    g = torch.Generator().manual_seed(seed)
+    return [[torch.randint(0, mc.vocab_size, (mbs, seq + 1), generator=g) for _ in range(n_micro)]
+            for _ in range(steps)]
+
+
+def _cfg(stage, ga, **kw):
+    c = EngineConfig(zero_stage=stage, micro_batch_size=2, seq_len=32, grad_accum=ga, lr=1e-2, scheduler="constant",
+                     init_device="cpu", grad_clip=1.0, comm_dtype=torch.float32)
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+def _init(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _train_worker(rank, world, port, model, stage, ga, steps, kw, out):
+    _init(rank, world, port)
+    eng = ZeroEngine(_model(model), _cfg(stage, ga, **kw), torch.device("cpu"), Comm())
+    grads0 = None
+    for mbs in _data(model, steps, world * ga):
+        mine = mbs[rank * ga:(rank + 1) * ga]
+        eng.train_step([(t[:, :-1], t[:, 1:]) for t in mine])
+        if grads0 is None:
+            grads0 = eng.full_grads()
+    params = eng.full_params()
+    if rank == 0:
+        torch.save({"params": params, "grads0": grads0, "live": eng.live_plan.resident_params,
+                    "gathers": eng.live_plan.gathers_per_step(ga), "local": eng.local_grads}, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _single(model, stage, ga_total, steps, **kw):
+    eng = ZeroEngine(_model(model), _cfg(stage, ga_total, **kw), torch.device("cpu"))
+    grads0 = None
+    for mbs in _data(model, steps, ga_total):
+        eng.train_step([(t[:, :-1], t[:, 1:]) for t in mbs])
+        if grads0 is None:
+            grads0 = eng.full_grads()
+    return eng.full_params(), grads0
+
+
+def _compare(got, ref_params, ref_grads0, steps, lr=1e-2, gtol=2e-2):
+    for k, v in ref_grads0.items():
+        err = float((got["grads0"][k] - v).abs().max() / v.abs().max().clamp_min(1e-8))
+        assert err < gtol, ("grad", k, err)
+    for k, v in ref_params.items():
+        d = (got["params"][k] - v).abs()
+        assert float(d.max()) <= 2 * lr * steps + 1e-3, ("param max", k, float(d.max()))
+        assert float((d > 0.1 * lr).float().mean()) < 0.12, ("param frac", k)  # Adam sign flips of ~0 grads
+
+
+@pytest.mark.parametrize("stage,local", [(1, False), (2, False), (2, True), (3, False), (3, True)])
+def test_zero_world4_matches_single(tmp_path, stage, local):
+    out = str(tmp_path / "w4.pt")
+    kw = {"local_grad_accum": local}
+    mp.spawn(_train_worker, args=(4, _port(), "llama-tiny", stage, 2, 2, kw, out), nprocs=4, join=True)
+    got = torch.load(out, weights_only=True)
+    assert got["local"] == (local and stage in (2, 3))
+    ref_params, ref_grads0 = _single("llama-tiny", stage, 8, 2)
+    _compare(got, ref_params, ref_grads0, 2)
+
+
+def test_zero3_world8_matches_single(tmp_path):
+    out = str(tmp_path / "w8.pt")
+    mp.spawn(_train_worker, args=(8, _port(), "llama-tiny", 3, 1, 2, {}, out), nprocs=8, join=True)
+    ref_params, ref_grads0 = _single("llama-tiny", 3, 8, 2)
+    _compare(torch.load(out, weights_only=True), ref_params, ref_grads0, 2)
+
+
+def test_zero3_nonresident_world4_matches_single(tmp_path):
+    """max_live_parameters = max_reuse_distance = 0: every visit gathers again and every micro-batch
+    reduce-scatters (the Llama-3-70B path, where gathered blocks do not all fit)."""
+    out = str(tmp_path / "nr.pt")
+    kw = {"max_live_parameters": 0, "max_reuse_distance": 0, "local_grad_accum": False}
+    mp.spawn(_train_worker, args=(4, _port(), "llama-tiny", 3, 2, 2, kw, out), nprocs=4, join=True)
+    got = torch.load(out, weights_only=True)
+    assert got["live"] == 0 and got["gathers"] > 2 * 4  # far more gathers than groups: re-gathered per visit
+    ref_params, ref_grads0 = _single("llama-tiny", 3, 8, 2)
+    _compare(got, ref_params, ref_grads0, 2)
+
+
+def _block_last_expert():
+    """Route no token to the last expert (its router logit forced to -inf): an expert with an empty segment."""
+    from distributed_llm_training_gpu_manager_amd import ops
+    if getattr(ops.router_topk, "_blocked", False):
+        return
+    orig = ops.router_topk
+
+    def rt(logits, k):
+        logits = logits.clone()
+        logits[:, -1] = float("-inf")
+        return orig(logits, k)
+    rt._blocked = True
+    ops.router_topk = rt
+
+
+def _ep_worker(rank, world, port, model, stage, out):
+    _init(rank, world, port)
+    _block_last_expert()
+    mc = _model(model)
+    cfg = _cfg(stage, 1, expert_parallel_size=world)
+    eng = ZeroEngine(mc, cfg, torch.device("cpu"), Comm())
+    counts = []
+    from distributed_llm_training_gpu_manager_amd.models import mixtral
+    orig = mixtral.MixtralBlock.moe_forward
+
+    def spy(self, p, hn2, ctx):
+        out_ = orig(self, p, hn2, ctx)
+        counts.append(list(out_[1][6].local_counts))
+        return out_
+    mixtral.MixtralBlock.moe_forward = spy
+    t = _data(model, 1, world, seq=8, mbs=1)[0][rank]
+    eng.cfg.seq_len = 8
+    eng.cfg.micro_batch_size = 1
+    eng.micro_step(t[:, :-1], t[:, 1:], first=True, last=True)
+    grads = eng.full_grads()
+    zero = [0 in c for c in counts]
+    gathered = [None] * world
+    dist.all_gather_object(gathered, zero)
+    if rank == 0:
+        torch.save({"grads": grads, "zero_token_expert": any(any(z) for z in gathered)}, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,model", [(4, "mixtral-tiny"), (8, "mixtral-8e")])
+def test_mixtral_expert_parallel_matches_single(tmp_path, world, model):
+    """EP = W (1 expert per rank at W=8) with 8 tokens per rank: some experts get no tokens at all."""
+    out = str(tmp_path / "ep.pt")
+    mp.spawn(_ep_worker, args=(world, _port(), model, 3, out), nprocs=world, join=True)
+    got = torch.load(out, weights_only=True)
+    assert got["zero_token_expert"], "the last expert must receive no tokens"
+    _block_last_expert()
+    eng = ZeroEngine(_model(model), _cfg(3, world, seq_len=8, micro_batch_size=1), torch.device("cpu"))
+    for i, t in enumerate(_data(model, 1, world, seq=8, mbs=1)[0]):
+        eng.micro_step(t[:, :-1], t[:, 1:], first=i == 0, last=i == world - 1)
+    ref = eng.full_grads()
+    assert set(got["grads"]) == set(ref)
+    for k, v in ref.items():
+        err = float((got["grads"][k] - v).abs().max() / v.abs().max().clamp_min(1e-8))
+        assert err < 2e-2, (k, err)
+        if k.endswith("experts.w_down"):
+            assert float(got["grads"][k][-1].abs().max()) == 0.0  # the empty expert gets an exact zero gradient
+
+
+# ---------------------------------------------------------------------------------------------- checkpoints
+def _save_worker(rank, world, port, model, stage, ep, save_dir, out):
+    from distributed_llm_training_gpu_manager_amd.ckpt.checkpoint import AsyncCheckpointer
+
+    _init(rank, world, port)
+    eng = ZeroEngine(_model(model), _cfg(stage, 1, expert_parallel_size=ep), torch.device("cpu"), Comm())
+    for mbs in _data(model, 2, world):
+        t = mbs[rank]
+        eng.train_step([(t[:, :-1], t[:, 1:])])
+    ck = AsyncCheckpointer(eng, save_dir, shm=False)
+    ck.save(2, {"step": 2}, blocking=True)
+    ck.wait_published(2)
+    full = {k: v.clone() for k, v in eng.full_params().items()}
+    m = eng._gather_flat(eng.exp_avg)
+    ck.close()
+    if rank == 0:
+        torch.save({"params": full, "exp_avg": m}, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _load_worker(rank, world, port, model, stage, ep, save_dir, out):
+    from distributed_llm_training_gpu_manager_amd.ckpt.checkpoint import AsyncCheckpointer
+
+    _init(rank, world, port)
+    eng = ZeroEngine(_model(model), _cfg(stage, 1, expert_parallel_size=ep, seed=777), torch.device("cpu"), Comm())
+    ck = AsyncCheckpointer(eng, save_dir, shm=False)
+    cs = ck.load("auto")
+    full = eng.full_params()
+    m = eng._gather_flat(eng.exp_avg)
+    if rank == 0:
+        torch.save({"params": full, "exp_avg": m, "cs": cs, "step": eng.step_count, "from": ck.restored_from,
+                    "rollbacks": ck.rollbacks}, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_checkpoint_world8_restores_at_world4_and_world2(tmp_path):
+    save = str(tmp_path / "ck")
+    ref = str(tmp_path / "ref.pt")
+    mp.spawn(_save_worker, args=(8, _port(), "llama-tiny", 3, 1, save, ref), nprocs=8, join=True)
+    want = torch.load(ref, weights_only=True)
+    for w, stage in ((4, 3), (2, 1)):
+        out = str(tmp_path / f"l{w}.pt")
+        mp.spawn(_load_worker, args=(w, _port(), "llama-tiny", stage, 1, save, out), nprocs=w, join=True)
+        got = torch.load(out, weights_only=True)
+        assert got["step"] == 2 and got["from"] == "disk:global_step2"
+        for k, v in want["params"].items():
+            assert torch.equal(got["params"][k], v), (w, k)
+            assert torch.equal(got["exp_avg"][k], want["exp_avg"][k]), (w, k)
+
+
+def test_checkpoint_expert_parallel_reshard_ep4_to_ep2(tmp_path):
+    """Experts live on different EP ranks: the reshard reassembles them expert by expert (global order)."""
+    save = str(tmp_path / "ck")
+    ref = str(tmp_path / "ref.pt")
+    mp.spawn(_save_worker, args=(4, _port(), "mixtral-tiny", 3, 4, save, ref), nprocs=4, join=True)
+    want = torch.load(ref, weights_only=True)
+    out = str(tmp_path / "l2.pt")
+    mp.spawn(_load_worker, args=(2, _port(), "mixtral-tiny", 3, 2, save, out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    for k, v in want["params"].items():
+        assert torch.equal(got["params"][k], v), k
+    # offline consolidation of the EP=4 checkpoint (no engine) gives the same global tensors
+    from distributed_llm_training_gpu_manager_amd.ckpt import zero_to_fp32
+    off = zero_to_fp32.consolidate(save)
+    assert set(off) == set(want["params"])
+    for k, v in want["params"].items():
+        assert torch.equal(off[k], v.float()), k
+
+
+def test_checkpoint_zero0_expert_parallel_saves_every_ep_rank(tmp_path):
+    """ZeRO-0 + EP: ranks 0..ep-1 each hold different experts, so each writes."""
+    save = str(tmp_path / "ck")
+    ref = str(tmp_path / "ref.pt")
+    mp.spawn(_save_worker, args=(2, _port(), "mixtral-tiny", 0, 2, save, ref), nprocs=2, join=True)
+    want = torch.load(ref, weights_only=True)
+    tag = os.path.join(save, "global_step2")
+    assert os.path.exists(os.path.join(tag, "zero_pp_rank_1_mp_rank_00_optim_states.pt"))
+    out = str(tmp_path / "l.pt")
+    mp.spawn(_load_worker, args=(2, _port(), "mixtral-tiny", 0, 2, save, out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    for k, v in want["params"].items():
+        assert torch.equal(got["params"][k], v), k
+
+
+def _two_tag_worker(rank, world, port, save_dir):
+    from distributed_llm_training_gpu_manager_amd.ckpt.checkpoint import AsyncCheckpointer
+
+    _init(rank, world, port)
+    eng = ZeroEngine(_model("llama-tiny"), _cfg(3, 1), torch.device("cpu"), Comm())
+    ck = AsyncCheckpointer(eng, save_dir, shm=False)
+    for step, mbs in enumerate(_data("llama-tiny", 2, world), 1):
+        t = mbs[rank]
+        eng.train_step([(t[:, :-1], t[:, 1:])])
+        ck.save(step, {"step": step}, blocking=True)
+        ck.wait_published(step)
+    ck.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_corrupt_shard_on_one_rank_rolls_back_every_rank(tmp_path):
+    """a rank whose newest shard fails its CRC must not resume alone from an older tag."""
+    save = str(tmp_path / "ck")
+    mp.spawn(_two_tag_worker, args=(2, _port(), save), nprocs=2, join=True)
+    f = os.path.join(save, "global_step2", "zero_pp_rank_1_mp_rank_00_optim_states.pt")
+    man = json.load(open(os.path.join(save, "global_step2", "manifest_r1.json")))
+    off = man["files"]["zero_pp_rank_1_mp_rank_00_optim_states.pt"]["exp_avg"]["offset"]
+    with open(f, "r+b") as fh:
+        fh.seek(off + 8)
+        b = fh.read(1)
+        fh.seek(off + 8)
+        fh.write(bytes([b[0] ^ 0xFF]))
+    outs = []
+    for r in range(2):
+        outs.append(str(tmp_path / f"o{r}.pt"))
+    mp.spawn(_agree_worker, args=(2, _port(), save, str(tmp_path)), nprocs=2, join=True)
+    got = [torch.load(str(tmp_path / f"agree{r}.pt"), weights_only=True) for r in range(2)]
+    assert [g["step"] for g in got] == [1, 1]
+    assert all("global_step2" in g["rollbacks"][0] for g in got)
+
+
+def _agree_worker(rank, world, port, save_dir, outdir):
+    from distributed_llm_training_gpu_manager_amd.ckpt.checkpoint import AsyncCheckpointer
+
+    _init(rank, world, port)
+    eng = ZeroEngine(_model("llama-tiny"), _cfg(3, 1), torch.device("cpu"), Comm())
+    ck = AsyncCheckpointer(eng, save_dir, shm=False)
+    cs = ck.load("auto")
+    torch.save({"step": eng.step_count, "cs": cs, "rollbacks": ck.rollbacks},
+               os.path.join(outdir, f"agree{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_stale_manifest_of_a_crashed_attempt_cannot_publish(tmp_path):
+    """a leftover <tag>.tmp manifest from an earlier attempt does not count for a new save."""
+    from distributed_llm_training_gpu_manager_amd.ckpt.checkpoint import AsyncCheckpointer
+
+    save = tmp_path / "ck"
+    eng = ZeroEngine(_model("llama-tiny"), _cfg(3, 1), torch.device("cpu"))
+    ck = AsyncCheckpointer(eng, str(save), shm=False, manifest_timeout_s=1.0)
+    ck.writers = [0, 1]  # pretend a second writer whose manifest is stale
+    tmp = save / "global_step5.tmp"
+    tmp.mkdir(parents=True)
+    (tmp / "manifest_r1.json").write_text(json.dumps({"rank": 1, "save_id": "5.0.99"}))
+    ck.save(5, {"step": 5})
+    with pytest.raises(RuntimeError, match="manifest"):
+        ck.wait()
+    assert not (save / "global_step5").exists()
+
+
+def test_pt_files_load_with_weights_only(tmp_path):
+    from distributed_llm_training_gpu_manager_amd.ckpt.checkpoint import AsyncCheckpointer
+
+    eng = ZeroEngine(_model("llama-tiny"), _cfg(3, 1), torch.device("cpu"))
+    eng.master.normal_()
+    eng.exp_avg.uniform_()
+    eng.sync_params_from_master()
+    ck = AsyncCheckpointer(eng, str(tmp_path), shm=False)
+    ck.save(7, {"step": 7}, blocking=True)
+    d = tmp_path / "global_step7"
+    opt = torch.load(d / "zero_pp_rank_0_mp_rank_00_optim_states.pt", weights_only=True)
+    osd = opt["optimizer_state_dict"]
+    assert torch.equal(osd["fp32_flat_groups"][0], eng.master)
+    assert torch.equal(osd["optimizer_state_dict"]["state"][0]["exp_avg"], eng.exp_avg)
+    assert osd["zero_stage"] == 3 and osd["partition_count"] == 1
+    mod = torch.load(d / "zero_pp_rank_0_mp_rank_00_model_states.pt", weights_only=True, mmap=True)
+    assert torch.equal(mod["bf16_param_shard"], eng.p16_shard)
+    meta = torch.load(d / "mp_rank_00_model_states.pt", weights_only=True)
+    assert meta["global_steps"] == 7 and meta["client_state"]["step"] == 7
+    import zipfile
+    assert zipfile.ZipFile(d / "zero_pp_rank_0_mp_rank_00_optim_states.pt").testzip() is None
+
+
+def test_shm_snapshot_tier_restores_first_and_falls_back(tmp_path):
+    from distributed_llm_training_gpu_manager_amd.ckpt.checkpoint import AsyncCheckpointer
+
+    save = str(tmp_path / "ck")
+    eng = ZeroEngine(_model("llama-tiny"), _cfg(3, 1), torch.device("cpu"))
+    eng.master.normal_()
+    ck = AsyncCheckpointer(eng, save, shm=True)
+    assert ck.mode == "shm"
+    ck.save(3, {"step": 3}, blocking=True)
+    eng.master.add_(1.0)
+    ck.save(4, {"step": 4}, blocking=True)
+    want = eng.master.clone()
+    ck.close()  # keeps the snapshot (a crashed rank never gets to discard it)
+    import shutil
+    shutil.rmtree(os.path.join(save, "global_step4"))  # the disk copy of step 4 never made it
+    e2 = ZeroEngine(_model("llama-tiny"), _cfg(3, 1, seed=5), torch.device("cpu"))
+    ck2 = AsyncCheckpointer(e2, save, shm=True)
+    assert ck2.load("auto")["step"] == 4 and ck2.restored_from == "shm:global_step4"
+    assert torch.equal(e2.master, want)
+    # a corrupted snapshot is rejected: roll back to the newest disk tag
+    snap = torch.from_file(ck2.shm_path, shared=True, size=os.path.getsize(ck2.shm_path), dtype=torch.uint8)
+    snap[10] ^= 0xFF
+    del snap
+    e3 = ZeroEngine(_model("llama-tiny"), _cfg(3, 1, seed=6), torch.device("cpu"))
+    ck3 = AsyncCheckpointer(e3, save, shm=True)
+    assert ck3.load("auto")["step"] == 3 and "shm:global_step4" in ck3.rollbacks[0]
+    ck3.close(discard_shm=True)
+    assert not os.path.exists(ck3.shm_path)
+
+
+def test_elastic_relaunch_four_to_two_ranks(tmp_path):
+    """A rank of a 4-rank job is SIGKILLed; the supervisor relaunches at world 2 (global batch 4 kept by
+    GA 1 -> 2), the checkpoint reshards 4 -> 2 and training continues to the last step."""
+    from distributed_llm_training_gpu_manager_amd.launcher.supervisor import JobRegistry, JobSpec
+
+    port = _port()
+    log_json = str(tmp_path / "log.json")
+    argv = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "4", "--master-addr", "127.0.0.1",
+            "--master-port", str(port), "-m", "distributed_llm_training_gpu_manager_amd.train", "--device", "cpu",
+            "--zero-stage", "3", "--steps", "6", "--seq-len", "32", "--save-interval", "2", "--kill-at-step", "3",
+            "--kill-rank", "1", "--elastic", "--ckpt-shm", "off", "--log-json", log_json]
+    reg = JobRegistry()
+    job = reg.submit(JobSpec(job_id="elastic", argv=argv, env={"PYTHONPATH": ROOT, "OMP_NUM_THREADS": "1"},
+                             save_dir=str(tmp_path / "ck"), run_dir=str(tmp_path / "run"), elastic=True,
+                             min_world=1, global_batch=4, micro_batch=1, max_restarts=2))
+    t0 = time.time()
+    while job.status not in ("succeeded", "failed", "nan_halt") and time.time() - t0 < 300:
+        time.sleep(0.2)
+    log = open(job.log_path).read()
+    assert job.status == "succeeded", log[-4000:]
+    assert job.world_history == [4, 2], job.world_history
+    assert "resumed from step 2" in log and "grad_accum 1 -> 2" in log
+    rec = json.load(open(log_json))
+    assert rec["engine"]["world"] == 2
+    steps = [r["step"] for r in rec["log"]]
+    assert steps == [3, 4, 5, 6]
+    assert all(r["loss"] == r["loss"] and r["loss"] < 10 for r in rec["log"])

@@ -44,9 +44,11 @@ def test_corrupt_latest_rolls_back(tmp_path):
     b = _train(tmp_path, "--steps", "4", "--save-interval", "2")
     b.run()
     assert complete_tags(str(tmp_path)) == ["global_step2", "global_step4"]
-    f = tmp_path / "global_step4" / "zero_pp_rank_0_mp_rank_00_optim_states.master.bin"
+    f = tmp_path / "global_step4" / "zero_pp_rank_0_mp_rank_00_optim_states.pt"
+    man = json.load(open(tmp_path / "global_step4" / "manifest_r0.json"))
+    off = man["files"]["zero_pp_rank_0_mp_rank_00_optim_states.pt"]["master"]["offset"]
     data = bytearray(f.read_bytes())
-    data[100] ^= 0xFF
+    data[off + 100] ^= 0xFF
     f.write_bytes(bytes(data))
     c = _train(tmp_path, "--steps", "4")
     cs = c.ckpt.load("auto")

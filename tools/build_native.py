@@ -107,7 +107,7 @@ def _build_host(sources: list[Path], jobs: int, verbose: bool, force: bool) -> P
             raise RuntimeError(f"compile failed: {src}\n{res.stderr}")
     out = PKG / "_dlgm_host.so"
     if force or todo or not out.exists():
-        cmd = [cxx, "-shared", "-fopenmp", *map(str, objs), "-o", str(out), "-lpthread"]
+        cmd = [cxx, "-shared", "-fopenmp", *map(str, objs), "-o", str(out), "-lpthread", "-lz"]
         res = subprocess.run(cmd, capture_output=True, text=True)
         if res.returncode != 0:
             raise RuntimeError(f"link failed: _dlgm_host.so\n{res.stderr}")
