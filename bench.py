@@ -7,8 +7,10 @@ warmup optimizer steps, then exactly K timed steps bracketed by a barrier +
 ``torch.cuda.synchronize()``; the elapsed time is the MAX over ranks; rank 0 prints
 one JSON line. ``value`` is whole-job tokens/sec (all N GPUs); per-GPU work is fixed
 (weak scaling). Data is synthetic (uniform random token ids), weights random-init of
-the real Llama-3-8B architecture; every step runs the full forward, backward,
-reduce-scatter, clipping and AdamW update.
+the real Llama-3-8B architecture; every step draws fresh tokens (generated before the
+timer starts) and runs the full forward, backward, reduce-scatter, clipping and AdamW
+update. An amdsmi sampler polls this rank's GPU (junction / HBM temperature, HBM used,
+power, xGMI links) on a side thread and its summary is reported in ``extra.telemetry``.
 """
 from __future__ import annotations
 
@@ -54,6 +56,8 @@ def main() -> int:
     ap.add_argument("--profile-steps", type=int, default=0,
                     help="after the timed steps, trace this many extra steps with torch.profiler")
     ap.add_argument("--profile-dir", default="gpurun_out/torch_trace")
+    ap.add_argument("--no-telemetry", action="store_true", help="do not poll amdsmi during the run")
+    ap.add_argument("--telemetry-interval", type=float, default=2.0)
     ap.add_argument("--n-layers", type=int, default=0,
                     help="override the preset's layer count (kernel profiling of big models on one GPU only; "
                          "the headline always runs the full preset)")
@@ -83,26 +87,36 @@ def main() -> int:
         torch.cuda.synchronize()
     init_s = time.time() - t0
 
+    # fresh synthetic tokens for every step (warmup and timed), drawn before any timing starts
     gen = torch.Generator(device=env.device)
     gen.manual_seed(1000 + env.rank)
-    batches = []
-    for _ in range(args.ga):
-        toks = torch.randint(0, mcfg.vocab_size, (args.mbs, args.seq + 1), device=env.device, generator=gen)
-        batches.append((toks[:, :-1].contiguous(), toks[:, 1:].contiguous()))
+    steps_data = []
+    for _ in range(args.warmup + args.steps + max(0, args.profile_steps)):
+        batches = []
+        for _ in range(args.ga):
+            toks = torch.randint(0, mcfg.vocab_size, (args.mbs, args.seq + 1), device=env.device, generator=gen)
+            batches.append((toks[:, :-1].contiguous(), toks[:, 1:].contiguous()))
+        steps_data.append(batches)
+    telemetry = None
+    if env.device.type == "cuda" and not args.no_telemetry:
+        # amdsmi polling of this rank's GPU (junction / HBM temperature, HBM used, power, xGMI links)
+        from distributed_llm_training_gpu_manager_amd.health.telemetry import TelemetrySampler
+        telemetry = TelemetrySampler(env.device, interval_s=args.telemetry_interval).start()
 
     def sync():
         if env.device.type == "cuda":
             torch.cuda.synchronize()
         comm.barrier()
 
-    for _ in range(args.warmup):
-        m = eng.train_step(batches)
+    for i in range(args.warmup):
+        m = eng.train_step(steps_data[i])
     sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        m = eng.train_step(batches)
+    for i in range(args.steps):
+        m = eng.train_step(steps_data[args.warmup + i])
     sync()
     elapsed = time.perf_counter() - t0
+    telem = telemetry.stop() if telemetry is not None else None
     t = torch.tensor([elapsed], dtype=torch.float64, device=env.device)
     comm.all_reduce_max(t)
     elapsed = float(t.item())
@@ -110,8 +124,8 @@ def main() -> int:
     if args.profile_steps > 0:  # outside the timed region: never part of the reported number
         from distributed_llm_training_gpu_manager_amd.utils.profiling import trace_window
         with trace_window(args.profile_dir, env.rank):
-            for _ in range(args.profile_steps):
-                eng.train_step(batches)
+            for i in range(args.profile_steps):
+                eng.train_step(steps_data[args.warmup + args.steps + i])
 
     tokens_per_step_gpu = args.mbs * args.seq * args.ga
     total_tokens = tokens_per_step_gpu * env.world * args.steps
@@ -143,7 +157,8 @@ def main() -> int:
                 "activation_checkpointing": args.ckpt,
                 "stage3_max_live_parameters": args.live_params,
                 "stage3_max_reuse_distance": args.reuse_distance,
-                "grad_reduce_scatter": "per_step" if eng.local_grads else "per_micro_batch",
+                "grad_reduce_scatter": ("none (single rank)" if eng.W == 1 else
+                                        "per_step" if eng.local_grads else "per_micro_batch"),
                 "hip_graphs": eng._graph is not None,
             },
             "extra": {
@@ -156,6 +171,7 @@ def main() -> int:
                 "zero3_allgathers_per_step": eng.live_plan.gathers_per_step(args.ga),
                 "zero3_resident_gathered_params": eng.live_plan.resident_params,
                 "mem": {k: round(v, 1) for k, v in eng.memory_report().items()},
+                "telemetry": telem,
             },
         }
         print(json.dumps(out), flush=True)

@@ -166,6 +166,7 @@ class AsyncCheckpointer:
         self.history: List[Dict[str, Any]] = []
         self.rollbacks: List[str] = []
         self.restored_from: Optional[str] = None
+        self._prep: Optional[threading.Thread] = None
         self._thread = threading.Thread(target=self._writer, daemon=True, name="ckpt-writer")
         self._thread.start()
         eng.pre_step_hooks.append(self._before_optimizer_step)
@@ -214,6 +215,14 @@ class AsyncCheckpointer:
         else:
             self._snap = torch.empty(nb, dtype=torch.uint8, pin_memory=self.cuda)
 
+    def prepare_async(self) -> None:
+        """Allocate (and page-lock) the snapshot buffer on a background thread while training runs, so the
+        first save -- often an emergency one on a spot notice -- does not pay for 14 B/param of fresh host
+        pages. Call it after any restore: the shm tier's file is the one a restore reads."""
+        if self.active and self._snap is None and self._prep is None:
+            self._prep = threading.Thread(target=self._alloc_snapshot, daemon=True, name="ckpt-prepare")
+            self._prep.start()
+
     def _views(self, snap: torch.Tensor) -> Dict[str, torch.Tensor]:
         n = self.n
         f = snap[:12 * n].view(torch.float32).view(3, n)
@@ -229,6 +238,9 @@ class AsyncCheckpointer:
         if self.busy:  # previous write-out still streaming from the snapshot buffer
             self.wait()
         save_id = f"{step}.{self._restart}.{self._saves}"
+        if self._prep is not None:
+            self._prep.join()  # background allocation / page-locking of the snapshot buffer
+            self._prep = None
         if self._snap is None:
             self._alloc_snapshot()
         if self.mode == "shm" and os.path.exists(self.shm_meta):
@@ -262,15 +274,16 @@ class AsyncCheckpointer:
         eng = self.engine
         ecfg = {k: (str(v) if isinstance(v, torch.dtype) else list(v) if isinstance(v, tuple) else v)
                 for k, v in vars(eng.cfg).items()}
-        groups = [{"name": g.name, "numel": g.numel, "shard_numel": g.shard_numel, "shard_off": g.shard_off,
-                   "kind": g.kind, "params": [[s.name, g.layout[s.name][0], list(s.shape)] for s in g.specs]}
+        groups = [{"name": g.name, "prefix": g.prefix, "numel": g.numel, "shard_numel": g.shard_numel,
+                   "shard_off": g.shard_off, "kind": g.kind,
+                   "params": [[s.name, g.layout[s.name][0], list(s.shape)] for s in g.specs]}
                   for g in eng.groups]
         return {"ds_version": DS_VERSION, "global_steps": step, "global_samples": step * eng.cfg.micro_batch_size
                 * eng.cfg.grad_accum * eng.W, "dp_world_size": eng.W, "mp_world_size": 1,
                 "partition_count": eng.P, "zero_stage": eng.stage, "ep_size": eng.ep_size,
                 "model_config": eng.mcfg.to_dict(), "engine_config": ecfg, "groups": groups, "writers": self.writers,
                 "client_state": client_state, "lr_scheduler": {"last_batch_iteration": step},
-                "param_shapes": [{f"{g['name']}.{p[0]}": p[2] for p in g["params"]} for g in groups],
+                "param_shapes": [{f"{g['prefix']}.{p[0]}": p[2] for p in g["params"]} for g in groups],
                 "buffer_names": [], "module": None,
                 "loss_scaler": ({"cur_scale": eng.scaler.scale} if eng.scaler is not None else None)}
 
@@ -468,15 +481,55 @@ class AsyncCheckpointer:
         return hashlib.sha1(json.dumps(lay, sort_keys=True).encode()).hexdigest()[:16]
 
     def _load_shm(self) -> Dict[str, Any]:
+        """Restore from the /dev/shm snapshot: the C++ reader streams CHUNK-aligned pieces of the file into two
+        pinned slots (16 threads, CRC32C computed while reading) and each piece goes on to the fp32 state on
+        the device while the next one is read -- page-cache bandwidth, not a page-faulting mmap."""
         with open(self.shm_src_meta) as f:
             m = json.load(f)
-        snap = torch.from_file(self.shm_src_path, shared=False, size=m["bytes"], dtype=torch.uint8)
-        if m["algo"] == _host.algo() and _host.crc32c_chunks(snap) != m["crc"]:
-            raise CorruptCheckpoint("shm snapshot: checksum mismatch")
-        v = self._views(snap)
-        eng = self.engine
-        for name in STATE:
-            getattr(eng, name).copy_(v[name])
+        eng, n = self.engine, self.n
+        dsts = [(k * 4 * n, getattr(eng, name).view(torch.uint8)) for k, name in enumerate(STATE)]
+        end = 12 * n  # the bf16 copy after the fp32 state is recomputed from the master, not read
+        piece = max(_host.CHUNK, self.ring_elems * 4)
+        check = m["algo"] == _host.algo()
+        slots = [torch.empty(piece, dtype=torch.uint8, pin_memory=self.cuda) for _ in range(2)]
+        evs: List[Any] = [None, None]
+        jobs = [(k, off, min(piece, end - off)) for k, off in enumerate(range(0, end, piece))]
+        q: "queue.Queue" = queue.Queue(maxsize=1)
+        free = [threading.Semaphore(1), threading.Semaphore(1)]
+
+        def reader():
+            try:
+                for k, off, ln in jobs:
+                    free[k % 2].acquire()
+                    q.put((k, off, ln, read_slot(self.shm_src_path, slots[k % 2][:ln], off)))
+            except Exception as e:  # noqa: BLE001
+                q.put(e)
+        th = threading.Thread(target=reader, daemon=True)
+        th.start()
+        for _ in jobs:
+            item = q.get()
+            if isinstance(item, Exception):
+                raise item
+            k, off, ln, crcs = item
+            first, nfull = off // _host.CHUNK, ln // _host.CHUNK  # a partial last chunk is verified below
+            if check and crcs[:nfull] != m["crc"][first:first + nfull]:
+                raise CorruptCheckpoint("shm snapshot: checksum mismatch")
+            src = slots[k % 2]
+            for base, dst in dsts:
+                lo, hi = max(off, base), min(off + ln, base + dst.numel())
+                if lo < hi:
+                    dst[lo - base:hi - base].copy_(src[lo - off:hi - off], non_blocking=True)
+            if self.cuda:
+                ev = torch.cuda.Event()
+                ev.record()
+                ev.synchronize()
+            free[k % 2].release()
+        th.join()
+        if check and end % _host.CHUNK:  # the chunk straddling the fp32/bf16 boundary: verify it whole
+            tail = torch.empty(min(_host.CHUNK, m["bytes"] - (end // _host.CHUNK) * _host.CHUNK), dtype=torch.uint8)
+            c = read_slot(self.shm_src_path, tail, (end // _host.CHUNK) * _host.CHUNK)
+            if c[0] != m["crc"][end // _host.CHUNK]:
+                raise CorruptCheckpoint("shm snapshot: checksum mismatch")
         eng.step_count = int(m["meta"]["global_steps"])
         return m["meta"].get("client_state", {})
 
@@ -605,7 +658,8 @@ class ShardSource:
         if kind != "expert" or self.ep == 1:
             if self.stage == 0:
                 return [0]
-            return sorted(self.mans, key=lambda r: self._group(r, gname)["prank"])
+            rs = sorted(self.mans, key=lambda r: self._group(r, gname)["prank"])
+            return rs[:1] if self._group(rs[0], gname)["P"] == 1 else rs  # replicated group: one copy
         rs = [r for r in self.mans if self.mans[r]["layout"]["ep_rank"] == ep_rank]
         return sorted(rs, key=lambda r: self._group(r, gname)["prank"])
 
@@ -648,7 +702,7 @@ class ShardSource:
                 holders = self._holders(g["name"], "dense", 0)
                 flat = self._old_flat(g["name"], state, holders)
                 for name, off, shape in (p[:3] for p in g["params"]):
-                    out[f"{g['name']}.{name}"] = np.array(flat[off:off + math.prod(shape)]).reshape(shape)
+                    out[f"{g.get('prefix', g['name'])}.{name}"] = np.array(flat[off:off + math.prod(shape)]).reshape(shape)
                 continue
             per_ep = []
             for eo in range(self.ep):
@@ -659,7 +713,7 @@ class ShardSource:
                 for flat, og in per_ep:
                     ooff, oshape = next((p[1], p[2]) for p in og["params"] if p[0] == name)
                     pieces.append(np.array(flat[ooff:ooff + math.prod(oshape)]).reshape(oshape))
-                out[f"{g['name']}.{name}"] = np.concatenate(pieces)
+                out[f"{g.get('prefix', g['name'])}.{name}"] = np.concatenate(pieces)
         return out
 
 

@@ -32,8 +32,10 @@ def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, **overri
         notes.append("communication_data_type fp16 mapped to bf16 (A20)")
     off_o = zo.get("offload_optimizer", {}).get("device", "none")
     off_p = zo.get("offload_param", {}).get("device", "none")
-    if off_p != "none":
-        notes.append(f"offload_param={off_p}: not needed on MI355X (288 GB HBM); parameters stay in HBM")
+    if off_p != "none" and int(zo.get("stage", 0)) != 3:
+        notes.append(f"offload_param={off_p} needs ZeRO-3 (as in DeepSpeed): parameters stay in HBM")
+    if off_p == "nvme":
+        notes.append("offload_param=nvme: the bf16 partition is served from pinned host memory")
     act = ds.get("activation_checkpointing")
     cfg = EngineConfig(
         zero_stage=int(zo.get("stage", 0)),
@@ -69,6 +71,10 @@ def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, **overri
         max_live_parameters=zo.get("stage3_max_live_parameters", 1e9),
         max_reuse_distance=zo.get("stage3_max_reuse_distance", 1e9),
         prefetch_bucket_size=float(zo.get("stage3_prefetch_bucket_size", 5e8)),
+        param_persistence_threshold=float(zo.get("stage3_param_persistence_threshold", 0.0)),
+        prescale_gradients=bool(ds.get("prescale_gradients", False)),
+        gradient_predivide_factor=float(ds.get("gradient_predivide_factor", 1.0)),
+        offload_param=off_p,
     )
     # engine knobs without a DeepSpeed key travel in the "mi355x" block (launcher.config.MI355XOptions)
     mi = ds.get("mi355x") or {}

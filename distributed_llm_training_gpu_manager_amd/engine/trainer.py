@@ -155,6 +155,11 @@ class Trainer:
                                   sp_rank=self.env.rank % self.sp, sp_size=self.sp)
         self.pusher = MetricsPusher(args.metrics_url if self.env.rank == 0 else None,
                                     os.environ.get("DLGM_JOB_ID", args.job_id))
+        self.telemetry = None
+        if self.env.device.type == "cuda" and args.telemetry_interval > 0:
+            # amdsmi polling of this rank's GPU inside the job (BASELINE config 2: thermals / HBM)
+            from ..health.telemetry import TelemetrySampler
+            self.telemetry = TelemetrySampler(self.env.device, interval_s=args.telemetry_interval).start()
         self.preempt = False
         signal.signal(signal.SIGUSR1, self._on_preempt)
         signal.signal(signal.SIGTERM, self._on_preempt)
@@ -208,9 +213,11 @@ class Trainer:
         a = self.args
         if self.env.rank == 0:
             write_status(step, loss=loss, nonfinite=bad)
+            hbm = self.telemetry.aggs["hbm_used_gib"].max if self.telemetry is not None else None
             alerts = self.monitor.ingest(TrainingMetrics(step=step, loss=loss, learning_rate=rec["lr"],
                                                          gradient_norm=rec["grad_norm"],
-                                                         tokens_per_sec=rec["tokens_per_sec"]))
+                                                         tokens_per_sec=rec["tokens_per_sec"],
+                                                         gpu_memory_used_mib=int(hbm * 1024) if hbm else 0))
             self.pusher.push({"step": step, "loss": loss if math.isfinite(loss) else 1e30,
                               "learning_rate": rec["lr"], "gradient_norm": rec["grad_norm"]
                               if math.isfinite(rec["grad_norm"]) else 1e30})
@@ -248,6 +255,8 @@ class Trainer:
                 self._say(f"resumed from step {start} in {time.time() - t0:.2f}s via {self.ckpt.restored_from} "
                           f"(rollbacks: {getattr(self.ckpt, 'rollbacks', [])})")
                 self.monitor.reset()
+        if self.ckpt is not None:
+            self.ckpt.prepare_async()  # snapshot buffer allocated / page-locked while the first steps run
         for n in self.notes:
             self._say(f"note: {n}")
         self._tokens_step = self.ecfg.micro_batch_size * self.ecfg.seq_len * self.ecfg.grad_accum * self.env.world
@@ -329,9 +338,13 @@ class Trainer:
             self.ckpt.close(discard_shm=rc == 0)
         self.trap.close()
         self.pusher.close()
+        telem = self.telemetry.stop() if self.telemetry is not None else None
+        if telem is not None:
+            self._say(f"telemetry: {json.dumps(telem)}")
         if a.log_json and self.env.rank == 0:
             with open(a.log_json, "w") as f:
                 json.dump(json_safe({"log": self.log, "ckpt": self.ckpt.history if self.ckpt else [],
+                                     "telemetry": telem,
                                      "trap": self.trap.records, "monitor": self.monitor.get_summary(),
                                      "engine": {"zero_stage": self.ecfg.zero_stage, "world": self.env.world,
                                                 "backend": self.env.backend, "device": str(self.env.device),
@@ -374,6 +387,8 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--metrics-url", default=os.environ.get("DLGM_METRICS_URL"))
     ap.add_argument("--job-id", default=os.environ.get("DLGM_JOB_ID", "local"))
     ap.add_argument("--log-interval", type=int, default=1)
+    ap.add_argument("--telemetry-interval", type=float, default=5.0,
+                    help="seconds between amdsmi samples of this rank's GPU (0: off)")
     ap.add_argument("--log-json", default=None)
     ap.add_argument("--n-layers", type=int, default=0, help="override the preset's depth (drills only)")
     ap.add_argument("--wall-clock-breakdown", action="store_true", help="per-phase HIP-event timers in the log")

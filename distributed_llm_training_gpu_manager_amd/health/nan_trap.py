@@ -36,6 +36,7 @@ class NanTrap:
         self.trip_time: Optional[float] = None
         self.records: List[Tuple[int, float, float]] = []  # (step, grad_sumsq, nonfinite)
         self.values: Dict[int, List[float]] = {}  # step -> report vector, until get() takes it
+        self.waited = 0  # get() calls that found their step still running on the device (host ran ahead)
         self._cuda = device.type == "cuda"
         self._ring = [torch.zeros(width, dtype=torch.float32, pin_memory=self._cuda) for _ in range(ring)]
         self._slot = 0
@@ -119,6 +120,8 @@ class NanTrap:
                     ev = e
                     break
         if ev is not None:
+            if not ev.query():
+                self.waited += 1
             ev.synchronize()
         with self._done:
             while step not in self.values:

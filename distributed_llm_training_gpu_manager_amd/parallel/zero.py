@@ -101,6 +101,10 @@ class EngineConfig:
     # group of sequence_parallel_size consecutive ranks holds one sequence of seq_len * size tokens
     sequence_parallel_size: int = 1
     offload_optimizer: str = "none"  # none | cpu | nvme (ZeRO-Offload parity path: parallel/offload.py)
+    # ZeRO-Infinity parameter offload (reference offload_param, deepspeed_launcher.py:40, 205-212; ZeRO-3 only):
+    # the bf16 parameter partition lives in pinned host memory; each gather stages the shard H2D on a side
+    # stream and all-gathers from there ("nvme" is served from host memory too)
+    offload_param: str = "none"
     nvme_path: Optional[str] = None
     # ZeRO-2/3 gradients: True = accumulate fp32 locally and reduce-scatter once per optimizer step;
     # False = reduce-scatter every micro-batch (DeepSpeed); "hbm" = True when GA > 1 and the full fp32
@@ -130,6 +134,16 @@ class EngineConfig:
     # once a step has non-finite gradients every later update is skipped on the device too (halt-on-NaN
     # jobs whose host runs a step ahead: the state at exit is the state before the poisoned step)
     nan_latch: bool = False
+    # DeepSpeed prescale_gradients / gradient_predivide_factor (reference deepspeed_launcher.py:61-62, 168-169):
+    # prescale: every gradient contribution is pre-divided by the factor (folded into the loss-gradient scale),
+    # reduced with SUM and post-multiplied by factor / world (folded into the accumulate alpha); otherwise
+    # reductions average (AVG)
+    prescale_gradients: bool = False
+    gradient_predivide_factor: float = 1.0
+    # stage3_param_persistence_threshold (reference :73, :191): under ZeRO-3 with W > 1, parameters with fewer
+    # elements stay replicated on every rank (their own P == 1 group per unit: never gathered, gradients
+    # all-reduced); 0 disables
+    param_persistence_threshold: float = 0.0
     fp16: bool = False  # dynamic loss scaling path (reference fp16 block)
     loss_scale: float = 0.0  # 0 = dynamic
     initial_scale_power: int = 16
@@ -148,6 +162,7 @@ class FlatGroup:
     def __init__(self, idx: int, name: str, specs: List[ParamSpec], part_world: int, kind: str = "dense",
                  comm: Optional[Comm] = None):
         self.idx, self.name, self.specs = idx, name, specs
+        self.prefix = name[:-len(".persist")] if name.endswith(".persist") else name  # parameter-name prefix
         self.kind, self.P, self.comm = kind, part_world, comm
         self.layout: Dict[str, Tuple[int, Tuple[int, ...]]] = {}
         off = 0
@@ -167,6 +182,14 @@ class FlatGroup:
             off, shape = self.layout[s.name]
             out[s.name] = flat.narrow(0, off, s.numel).view(shape)
         return out
+
+
+class _Scaled:
+    """Pending-reduction payload: multiply `t` by `factor` once the collective completed (prescale post-scale);
+    `keep` holds the collective's input alive until then."""
+
+    def __init__(self, t: torch.Tensor, factor: float, keep: Any = None):
+        self.t, self.factor, self.keep = t, factor, keep
 
 
 class LossScaler:
@@ -245,6 +268,7 @@ class ZeroEngine:
         if cfg.separate_gather_comm and self.W > 1 and self.stage > 0:
             self.gather_comm = self.comm.duplicate()
         groups, stages = build_model(model_cfg, ep_rank, self.ep_size)
+        groups, stages, self._orig_groups = self._split_persistent(groups, stages)
         self.stages = [(u, tuple(gi) if isinstance(gi, (tuple, list)) else (gi,)) for u, gi in stages]
         self.groups = []
         for i, grp in enumerate(groups):
@@ -253,6 +277,8 @@ class ZeroEngine:
             if kind == "expert":
                 comm_g = self.edp_comm if self.edp_comm is not None else Comm()
                 P_g = 1 if self.stage == 0 else comm_g.world
+            elif kind == "persist":
+                comm_g, P_g = self.comm, 1  # replicated on every rank, gradients all-reduced
             else:
                 comm_g, P_g = self.comm, self.P
             fg = FlatGroup(i, name, specs, P_g, kind, comm_g)
@@ -327,6 +353,38 @@ class ZeroEngine:
         self.hooks: List[Any] = []  # callables(engine, metrics) after each step (NaN trap, monitors)
         self.pre_step_hooks: List[Any] = []  # callables(engine) before the optimizer touches master/m/v
 
+    def _split_persistent(self, groups, stages):
+        """stage3_param_persistence_threshold: move each unit's small tensors (norm weights, biases) into a
+        replicated "<unit>.persist" group beside the partitioned one. Returns (groups, stages, originals);
+        originals = [(original index, name, specs, new group indices)] keeps initialisation identical to the
+        unsplit layout."""
+        thr = self.cfg.param_persistence_threshold
+        orig = []
+        if not (thr > 0 and self.stage == 3 and self.W > 1):
+            for i, grp in enumerate(groups):
+                orig.append((i, grp[0], grp[1], (i,)))
+            return groups, stages, orig
+        out, remap = [], {}
+        for i, grp in enumerate(groups):
+            name, specs = grp[0], grp[1]
+            kind = grp[2] if len(grp) > 2 else "dense"
+            small = [sp for sp in specs if sp.numel < thr] if kind == "dense" else []
+            big = [sp for sp in specs if sp not in small]
+            idx = []
+            if big:
+                idx.append(len(out))
+                out.append((name, big, kind))
+            if small:
+                idx.append(len(out))
+                out.append((name + ".persist" if big else name, small, "persist"))
+            remap[i] = tuple(idx)
+            orig.append((i, name, specs, tuple(idx)))
+        new_stages = []
+        for u, gi in stages:
+            gis = tuple(gi) if isinstance(gi, (tuple, list)) else (gi,)
+            new_stages.append((u, tuple(j for g in gis for j in remap[g])))
+        return out, new_stages, orig
+
     # ------------------------------------------------------------------ storage
     def _alloc(self) -> None:
         dev, n = self.device, self.shard_total
@@ -345,7 +403,13 @@ class ZeroEngine:
             self.exp_avg = torch.zeros(n, **f32)
             self.exp_avg_sq = torch.zeros(n, **f32)
         self.grad_shard = torch.zeros(n, **f32)
-        self.p16_shard = torch.zeros(n, dtype=self.dtype, device=dev)
+        self.param_host = self.cfg.offload_param in ("cpu", "nvme") and self.stage == 3
+        if self.param_host:
+            self.p16_shard = torch.zeros(n, dtype=self.dtype, pin_memory=self.is_cuda)
+            self._h2d = torch.cuda.Stream(dev) if self.is_cuda else None
+            self._p16_ready = None  # event: host bf16 partition final (after the device AdamW's D2H)
+        else:
+            self.p16_shard = torch.zeros(n, dtype=self.dtype, device=dev)
         self.p16_full = None
         self.grad_full = None
         if self.stage == 0:
@@ -375,18 +439,31 @@ class ZeroEngine:
         if init_dev == "auto":
             init_dev = "cpu" if sum(g.real_numel for g in self.groups) < 1e9 else self.device.type
         gen = torch.Generator(device=init_dev)
-        for g in self.groups:
-            full = torch.zeros(g.numel, dtype=torch.float32, device=init_dev)
-            views = g.views(full)
-            gseed = self.cfg.seed * 1000003 + g.idx
+        for oi, oname, ospecs, new_idx in self._orig_groups:
+            # initialise the ORIGINAL unit layout (seeded by its index), so a persistence split does not change
+            # any value; then scatter its tensors into the group(s) that hold them now
+            og = FlatGroup(oi, oname, ospecs, 1)
+            full = torch.zeros(og.numel, dtype=torch.float32, device=init_dev)
+            views = og.views(full)
+            gseed = self.cfg.seed * 1000003 + oi
             gen.manual_seed(gseed)
-            for s in g.specs:
+            for s in ospecs:
                 init_param(s, views[s.name], gen, gseed)
-            full = full.to(self.device)
-            r0 = (g.comm.rank if g.P > 1 else 0) * g.shard_numel
-            self.master.narrow(0, g.shard_off, g.shard_numel).copy_(full.narrow(0, r0, g.shard_numel))
-            if self.p16_full is not None and self.p16_full is not self.p16_shard:
-                self.p16_full.narrow(0, g.full_off, g.numel).copy_(full)
+            for gi in new_idx:
+                g = self.groups[gi]
+                if len(new_idx) == 1 and g.numel == og.numel:
+                    gfull = full.to(self.device)
+                else:
+                    gfull = torch.zeros(g.numel, dtype=torch.float32, device=init_dev)
+                    gv = g.views(gfull)
+                    for s in g.specs:
+                        gv[s.name].copy_(views[s.name])
+                    gfull = gfull.to(self.device)
+                r0 = (g.comm.rank if g.P > 1 else 0) * g.shard_numel
+                self.master.narrow(0, g.shard_off, g.shard_numel).copy_(gfull.narrow(0, r0, g.shard_numel))
+                if self.p16_full is not None and self.p16_full is not self.p16_shard:
+                    self.p16_full.narrow(0, g.full_off, g.numel).copy_(gfull)
+                del gfull
             del full
         self._p16_from_master()
 
@@ -394,10 +471,50 @@ class ZeroEngine:
         self._pver = getattr(self, "_pver", 0) + 1
         if self.offload is not None:
             self.offload.push_params(self.p16_shard)
+        elif self.param_host:
+            self._p16_to_host()
         elif self.dtype == torch.bfloat16:
             ops.cast_f32_bf16_(self.p16_shard, self.master)
         else:
             self.p16_shard.copy_(self.master)
+
+    def _p16_to_host(self) -> None:
+        """offload_param with the optimizer on the device: bf16(master) chunk by chunk into a device scratch,
+        then D2H into the pinned host partition (stream-ordered, no host sync)."""
+        n, step = self.shard_total, 1 << 26
+        scratch = torch.empty(min(n, step), dtype=self.dtype, device=self.device)
+        for off in range(0, n, step):
+            ln = min(step, n - off)
+            if self.is_cuda:
+                ops.cast_f32_bf16_(scratch[:ln], self.master.narrow(0, off, ln))
+            else:
+                scratch[:ln].copy_(self.master.narrow(0, off, ln))
+            self.p16_shard.narrow(0, off, ln).copy_(scratch[:ln], non_blocking=True)
+        if self.is_cuda:
+            self._p16_ready = torch.cuda.Event()
+            self._p16_ready.record()
+
+    def _gather_from_host(self, g: FlatGroup) -> Tuple[torch.Tensor, Handle]:
+        """offload_param: stage the host shard H2D on the side stream and all-gather from there (the RCCL work
+        is ordered after the copy, not after the compute queued so far)."""
+        host = self._shard16(g)
+        if not self.is_cuda:
+            stage = host.clone()
+            if g.P == 1:
+                return stage, DONE
+            buf = torch.empty(g.numel, dtype=self.dtype, device=self.device)
+            return buf, g.gcomm.all_gather(buf, stage, async_op=True)
+        with torch.cuda.stream(self._h2d):
+            if self._p16_ready is not None:
+                self._h2d.wait_event(self._p16_ready)
+            stage = torch.empty(g.shard_numel, dtype=self.dtype, device=self.device)
+            stage.copy_(host, non_blocking=True)
+            if g.P == 1:
+                ev = torch.cuda.Event()
+                ev.record(self._h2d)
+                return stage, Handle(post=lambda: torch.cuda.current_stream(self.device).wait_event(ev))
+            buf = torch.empty(g.numel, dtype=self.dtype, device=self.device)
+            return buf, g.gcomm.all_gather(buf, stage, async_op=True)
 
     # ------------------------------------------------------------------ params
     def _shard16(self, g: FlatGroup) -> torch.Tensor:
@@ -410,6 +527,8 @@ class ZeroEngine:
         if self.stage < 3:
             flat = self.p16_full.narrow(0, g.full_off, g.numel)
             self._live[gi] = (flat, DONE)
+        elif self.param_host:
+            self._live[gi] = self._gather_from_host(g)
         elif g.P == 1:
             self._live[gi] = (self._shard16(g), DONE)
         else:
@@ -426,6 +545,8 @@ class ZeroEngine:
             self._issue_gather(gi)
             flat, h = self._live[gi]
             h.wait()
+            if self.param_host and self.is_cuda:
+                flat.record_stream(torch.cuda.current_stream(self.device))  # allocated on the H2D stream
             views = self.groups[gi].views(flat)
             out.update(views)
             if gi in self._tnames:
@@ -541,39 +662,47 @@ class ZeroEngine:
             return self.grad_full.narrow(0, g.gfull_off, g.numel)
         return None
 
+    def _post(self, g: FlatGroup) -> float:
+        """Factor applied after group g's gradient reduction: 1 (AVG reductions) or, with
+        prescale_gradients, predivide_factor / reduce world (SUM reductions of pre-divided gradients)."""
+        if not self.cfg.prescale_gradients:
+            return 1.0
+        return self.cfg.gradient_predivide_factor / max(1, g.comm.world)
+
     def _finish_direct(self, g: FlatGroup, tgt: torch.Tensor, pending: List[Tuple[Handle, Any]]) -> None:
         """Boundary work for a direct group after its last backward visit of the last micro-batch."""
         if g.kind == "expert" and self.ep_size > 1:
             # an expert sees the tokens of every EP rank, each scaled by 1/(its own tokens): divide by the
             # EP size so expert grads are the global mean like the dense grads (which are AVG-reduced)
             tgt.mul_(1.0 / self.ep_size)
+        avg, post = not self.cfg.prescale_gradients, self._post(g)
         if g.P > 1 and self.local_grads and self.cfg.comm_dtype != tgt.dtype:
             # ZeRO-2/3 local accumulation: one reduce-scatter per step in comm_dtype (half the bytes of
             # fp32), then the shard is written (beta = 0) from the reduced chunk
             src = tgt.to(self.cfg.comm_dtype)
             out = torch.empty(g.shard_numel, dtype=src.dtype, device=self.device)
             shard_tgt = self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
-            pending.append((g.comm.reduce_scatter(out, src, avg=True, async_op=True),
-                            (shard_tgt, out, 0.0, None, 1.0, src)))
+            pending.append((g.comm.reduce_scatter(out, src, avg=avg, async_op=True),
+                            (shard_tgt, out, 0.0, None, post, src)))
         elif g.P > 1:  # ZeRO-1 (or fp32 comm): reduce-scatter the local accumulator into this rank's shard
             out = self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
-            pending.append((g.comm.reduce_scatter(out, tgt, avg=True, async_op=True), tgt))
-        elif g.comm.world > 1:  # ZeRO-0: plain data parallel
-            pending.append((g.comm.all_reduce(tgt, avg=True, async_op=True), None))
+            pending.append((g.comm.reduce_scatter(out, tgt, avg=avg, async_op=True), _Scaled(out, post, tgt)))
+        elif g.comm.world > 1:  # ZeRO-0 / persistent (replicated) group: plain data parallel
+            pending.append((g.comm.all_reduce(tgt, avg=avg, async_op=True), _Scaled(tgt, post)))
 
     def _reduce_group_grad(self, gi: int, gbuf: torch.Tensor, first_micro: bool,
                            pending: List[Tuple[Handle, Any]]) -> None:
         """Scratch path (ZeRO-2/3, P > 1): reduce-scatter this micro-batch's bf16 gradient segment now."""
         g = self.groups[gi]
         beta = 0.0 if first_micro else 1.0
-        alpha = 1.0 / self.ep_size if g.kind == "expert" else 1.0
+        alpha = (1.0 / self.ep_size if g.kind == "expert" else 1.0) * self._post(g)
         shard_tgt = self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
         src = gbuf
         if self.cfg.comm_dtype != gbuf.dtype:
             src = gbuf.to(self.cfg.comm_dtype)
             self._release_gbuf(gbuf)
         out = torch.empty(g.shard_numel, dtype=src.dtype, device=self.device)
-        h = g.comm.reduce_scatter(out, src, avg=True, async_op=True)
+        h = g.comm.reduce_scatter(out, src, avg=not self.cfg.prescale_gradients, async_op=True)
         pending.append((h, (shard_tgt, out, beta, src, alpha)))
 
     def _acquire_gbuf(self, numel: int) -> torch.Tensor:
@@ -592,7 +721,10 @@ class ZeroEngine:
         while len(pending) > keep:
             h, payload = pending.pop(0)
             h.wait()
-            if isinstance(payload, tuple):
+            if isinstance(payload, _Scaled):
+                if payload.factor != 1.0:
+                    payload.t.mul_(payload.factor)
+            elif isinstance(payload, tuple):
                 shard_tgt, out, beta, src, alpha = payload[:5]  # payload[5]: input kept alive until here
                 ops.accumulate_(shard_tgt, out, alpha, beta)
                 if src is not None and src.dtype == self.dtype:
@@ -602,6 +734,8 @@ class ZeroEngine:
     def _context(self, ids: torch.Tensor, labels: torch.Tensor) -> StepContext:
         B, S = ids.shape
         gs = 1.0 / (B * S * self.cfg.grad_accum)
+        if self.cfg.prescale_gradients:
+            gs /= self.cfg.gradient_predivide_factor  # pre-divided before the SUM reductions
         if self.scaler is not None:
             gs *= self.scaler.scale
         return StepContext(batch=B, seq_len=S, input_ids=ids, labels=labels, grad_scale=gs, rope=self.rope,
@@ -711,7 +845,8 @@ class ZeroEngine:
         """stats = [sum g^2, #non-finite, flags] over the whole model, each gradient element counted once;
         flags = sum over ranks of host_flag."""
         st = self.stats
-        if not self.has_experts:
+        simple = not self.has_experts and (self.P == 1 or all(g.P > 1 for g in self.groups))
+        if simple:
             ops.grad_stats([self.grad_shard], st)
             st[2].fill_(self.host_flag)
             if self.P > 1:
@@ -719,23 +854,28 @@ class ZeroEngine:
             elif self.sync_flags and self.W > 1:
                 self.comm.all_reduce(st[2:3], async_op=False).wait()
         else:
+            # partitioned dense groups: summed over ranks; replicated groups (ZeRO-0, persistent): counted
+            # once; expert groups: summed over their expert-data-parallel and EP ranks
             sl = lambda g: self.grad_shard.narrow(0, g.shard_off, g.shard_numel)  # noqa: E731
             dense = torch.zeros(3, dtype=torch.float32, device=self.device)
+            rep = torch.zeros(2, dtype=torch.float32, device=self.device)
             exp = torch.zeros(2, dtype=torch.float32, device=self.device)
-            ops.grad_stats([sl(g) for g in self.groups if g.kind != "expert"], dense)
+            ops.grad_stats([sl(g) for g in self.groups if g.kind != "expert" and g.P > 1], dense)
+            ops.grad_stats([sl(g) for g in self.groups if g.kind != "expert" and g.P == 1], rep)
             ops.grad_stats([sl(g) for g in self.groups if g.kind == "expert"], exp)
             dense[2].fill_(self.host_flag)
-            if self.P > 1:
+            if any(g.P > 1 and g.kind != "expert" for g in self.groups):
                 self.comm.all_reduce(dense, async_op=False).wait()
             elif self.sync_flags and self.W > 1:
                 self.comm.all_reduce(dense[2:3], async_op=False).wait()
-            if self.ep_comm is not None and self.ep_comm.world > 1:
-                self.ep_comm.all_reduce(exp, async_op=False).wait()
-            eg = next(g for g in self.groups if g.kind == "expert")
-            if eg.P > 1:
-                eg.comm.all_reduce(exp, async_op=False).wait()
+            if self.has_experts:
+                if self.ep_comm is not None and self.ep_comm.world > 1:
+                    self.ep_comm.all_reduce(exp, async_op=False).wait()
+                eg = next(g for g in self.groups if g.kind == "expert")
+                if eg.P > 1:
+                    eg.comm.all_reduce(exp, async_op=False).wait()
             st.copy_(dense)
-            st[:2] += exp
+            st[:2] += rep + exp
         if self._nan_latch is not None:
             torch.maximum(self._nan_latch, st[1:2], out=self._nan_latch)
             st[1:2].copy_(self._nan_latch)
@@ -758,10 +898,13 @@ class ZeroEngine:
             self._offload_step(lr, inv_scale)
         else:
             ops.adamw_step_(self.master, self.exp_avg, self.exp_avg_sq, self.grad_shard,
-                            self.p16_shard if self.dtype == torch.bfloat16 else None, self.stats, lr=lr,
+                            self.p16_shard if self.dtype == torch.bfloat16 and not self.param_host else None,
+                            self.stats, lr=lr,
                             beta1=cfg.betas[0], beta2=cfg.betas[1], eps=cfg.eps, weight_decay=cfg.weight_decay,
                             step=self.step_count, grad_scale=inv_scale, max_norm=cfg.grad_clip)
-            if self.dtype != torch.bfloat16:
+            if self.param_host:
+                self._p16_to_host()
+            elif self.dtype != torch.bfloat16:
                 self.p16_shard.copy_(self.master)
         self._pver += 1  # the compute copy changes below: transposed caches are stale
         if self.stage == 3:
@@ -827,6 +970,7 @@ class ZeroEngine:
         per-phase timers (host-side event bookkeeping)."""
         c = self.cfg
         return (c.hip_graphs and self.is_cuda and self.W == 1 and not self.has_experts and self.offload is None
+                and not self.param_host
                 and self.scaler is None and not c.cpu_checkpointing and not self.timers.enabled
                 and self.sp_size == 1 and self._graph_state != "failed")
 
@@ -902,7 +1046,7 @@ class ZeroEngine:
                     parts = torch.empty((self.ep_comm.world, *v.shape), dtype=v.dtype, device=v.device)
                     self.ep_comm.all_gather(parts.view(-1), v.reshape(-1), async_op=False).wait()
                     v = parts.reshape(-1, *v.shape[1:])
-                out[f"{g.name}.{k}"] = v
+                out[f"{g.prefix}.{k}"] = v
         return out
 
     def memory_report(self) -> Dict[str, float]:
@@ -911,7 +1055,8 @@ class ZeroEngine:
             "optimizer_state_GiB": 0.0 if self.offload is not None else 3 * self.shard_total * 4 / gb,
             "optimizer_state_host_GiB": 3 * self.shard_total * 4 / gb if self.offload is not None else 0.0,
             "grad_shard_GiB": self.shard_total * 4 / gb,
-            "param_shard_GiB": self.shard_total * 2 / gb,
+            "param_shard_GiB": 0.0 if self.param_host else self.shard_total * 2 / gb,
+            "param_shard_host_GiB": self.shard_total * 2 / gb if self.param_host else 0.0,
             "param_full_GiB": (self.full_total * 2 / gb) if self.p16_full is not None else 0.0,
             "grad_full_GiB": (self.gfull_total * 4 / gb) if self.grad_full is not None else 0.0,
             "weight_T_cache_GiB": sum(t.numel() * t.element_size() for _, c in self._tcache.values()

@@ -24,8 +24,11 @@ def test_presets_map_onto_engine():
         assert cfg.offload_optimizer == off.get("device", "none")
         if "buffer_count" in off:
             assert cfg.offload_buffer_count == off["buffer_count"]
-        if zo.get("offload_param", {}).get("device", "none") != "none":
-            assert any("offload_param" in n for n in notes)
+        assert cfg.offload_param == zo.get("offload_param", {}).get("device", "none")
+        assert cfg.param_persistence_threshold == zo["stage3_param_persistence_threshold"]
+        assert cfg.prescale_gradients == ds["prescale_gradients"]
+        assert cfg.gradient_predivide_factor == ds["gradient_predivide_factor"]
+        assert not any("not needed" in n or "not applicable" in n for n in notes)
 
 
 def test_aio_and_mi355x_blocks():

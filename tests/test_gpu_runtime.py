@@ -1,0 +1,121 @@
+"""MI355X runtime paths around the kernels: live amdsmi telemetry, the /dev/shm checkpoint tier with a
+page-locked (hipHostRegister) snapshot, and the trainer's one-step-late host loop with the NaN latch."""
+import os
+import time
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_live_amdsmi_query_and_topology():
+    from distributed_llm_training_gpu_manager_amd.health.gpu_manager import GPUManager
+
+    mgr = GPUManager()
+    devs = mgr.query_amdsmi()
+    assert devs, "amdsmi sees no GPU"
+    d = devs[0]
+    assert d.memory_total_mib > 200 * 1024, d.memory_total_mib  # 288 GB HBM3E
+    assert (d.hotspot_temperature_celsius or d.temperature_celsius) > 0
+    assert d.power_limit_watts > 0
+    topo = mgr.topology()
+    assert topo["source"] in ("amdsmi", "none") and "topology_matrix" in topo
+    fleet = mgr.get_fleet_status()
+    assert fleet.total_gpus >= 1 and fleet.source in ("amdsmi", "amd-smi-cli")
+
+
+def test_in_job_telemetry_sampler():
+    from distributed_llm_training_gpu_manager_amd.health.telemetry import TelemetrySampler
+
+    s = TelemetrySampler(torch.device("cuda", 0), interval_s=0.2).start()
+    x = torch.randn(8192, 8192, device="cuda")
+    for _ in range(20):
+        x = x @ x.t()
+        x = x / x.norm()
+    torch.cuda.synchronize()
+    time.sleep(0.5)
+    out = s.stop()
+    assert out["samples"] >= 2 and out["source"] == "amdsmi", out
+    assert out["junction_temp_c"]["max"] > 0 and out["hbm_used_gib"]["max"] > 0
+
+
+def _engine(seed=0):
+    from distributed_llm_training_gpu_manager_amd.models import get_config
+    from distributed_llm_training_gpu_manager_amd.parallel.zero import EngineConfig, ZeroEngine
+
+    return ZeroEngine(get_config("llama-small"), EngineConfig(zero_stage=3, seq_len=256, micro_batch_size=1,
+                                                              grad_accum=1, seed=seed, scheduler="constant"),
+                      torch.device("cuda", 0))
+
+
+def test_shm_tier_checkpoint_roundtrip(tmp_path):
+    from distributed_llm_training_gpu_manager_amd.ckpt.checkpoint import AsyncCheckpointer
+
+    e = _engine()
+    t = torch.randint(0, 32768, (1, 257), device="cuda")
+    e.train_step([(t[:, :-1], t[:, 1:])])
+    ck = AsyncCheckpointer(e, str(tmp_path), shm=True)
+    assert ck.mode == "shm"
+    ck.save(1, {"step": 1}, blocking=True)
+    assert ck._pinned_shm, "hipHostRegister of the /dev/shm snapshot failed"
+    want = e.master.clone()
+    e.train_step([(t[:, :-1], t[:, 1:])])  # the optimizer waits for the capture on the GPU
+    ck.close()
+    e2 = _engine(seed=3)
+    ck2 = AsyncCheckpointer(e2, str(tmp_path), shm=True)
+    assert ck2.load("auto")["step"] == 1 and ck2.restored_from == "shm:global_step1"
+    assert torch.equal(e2.master, want)
+    ck2.close(discard_shm=True)
+    d = torch.load(tmp_path / "global_step1" / "zero_pp_rank_0_mp_rank_00_optim_states.pt", weights_only=True)
+    assert torch.equal(d["optimizer_state_dict"]["fp32_flat_groups"][0], want.cpu())
+
+
+def _trainer(tmp, *extra):
+    from distributed_llm_training_gpu_manager_amd.engine.trainer import Trainer, parse_args
+
+    return Trainer(parse_args(["--model", "llama-small", "--seq-len", "2048", "--device", "cuda",
+                               "--log-interval", "100", "--telemetry-interval", "0", *extra]))
+
+
+def test_trainer_runs_ahead_and_nan_latch_keeps_pre_nan_state(tmp_path):
+    from distributed_llm_training_gpu_manager_amd.launcher.supervisor import EXIT_NAN_HALT
+
+    ok = _trainer(tmp_path, "--steps", "8")
+    assert ok.run() == 0
+    # the report of step t-1 was read while step t was still queued/running on the GPU
+    assert ok.trap.waited >= 4, ok.trap.waited
+    ref = _trainer(tmp_path, "--steps", "2")
+    assert ref.run() == 0
+    bad = _trainer(tmp_path, "--steps", "8", "--inject-nan-step", "3")
+    assert bad.run() == EXIT_NAN_HALT
+    assert bad.trap.trip_step == 3 and bad.log[-1]["step"] == 3
+    # step 4 was queued before the halt decision; the device latch skipped its update too
+    assert bad.engine.step_count >= 4
+    assert torch.equal(bad.engine.master, ref.engine.master)
+
+
+def test_offload_param_on_gpu_matches_device_params():
+    """offload_param=cpu: the bf16 partition in pinned host memory, H2D-staged gathers on a side stream."""
+    from distributed_llm_training_gpu_manager_amd.models import get_config
+    from distributed_llm_training_gpu_manager_amd.parallel.zero import EngineConfig, ZeroEngine
+
+    res = {}
+    for name, off in (("dev", "none"), ("host", "cpu")):
+        torch.cuda.empty_cache()
+        e = ZeroEngine(get_config("llama-small"), EngineConfig(zero_stage=3, seq_len=512, micro_batch_size=1,
+                                                               grad_accum=2, scheduler="constant", offload_param=off),
+                       torch.device("cuda", 0))
+        g = torch.Generator(device="cuda").manual_seed(0)
+        for _ in range(2):
+            mb = [torch.randint(0, 32768, (1, 513), device="cuda", generator=g) for _ in range(2)]
+            m = e.train_step([(t[:, :-1], t[:, 1:]) for t in mb])
+        torch.cuda.synchronize()
+        res[name] = (float(m["loss"]), e.master.clone(), e.p16_shard.device.type, e.memory_report())
+        del e
+    assert res["host"][2] == "cpu" and res["dev"][2] == "cuda"
+    assert res["host"][3]["param_shard_host_GiB"] > 0 and res["host"][3]["param_shard_GiB"] == 0
+    assert abs(res["host"][0] - res["dev"][0]) < 1e-3
+    assert torch.equal(res["host"][1], res["dev"][1])

@@ -425,3 +425,92 @@ def test_elastic_relaunch_four_to_two_ranks(tmp_path):
     steps = [r["step"] for r in rec["log"]]
     assert steps == [3, 4, 5, 6]
     assert all(r["loss"] == r["loss"] and r["loss"] < 10 for r in rec["log"])
+
+
+# ---------------------------------------------------------------------------------------------- DeepSpeed knobs
+def _knob_worker(rank, world, port, kw, out):
+    _init(rank, world, port)
+    from distributed_llm_training_gpu_manager_amd.parallel import comm as comm_mod
+
+    ops_seen = []
+    orig_rs, orig_ar = comm_mod.Comm.reduce_scatter, comm_mod.Comm.all_reduce
+
+    def rs(self, o, i, avg=True, async_op=True):
+        ops_seen.append(("rs", avg, i.numel()))
+        return orig_rs(self, o, i, avg=avg, async_op=async_op)
+
+    def ar(self, t, avg=False, async_op=True):
+        ops_seen.append(("ar", avg, t.numel()))
+        return orig_ar(self, t, avg=avg, async_op=async_op)
+    comm_mod.Comm.reduce_scatter, comm_mod.Comm.all_reduce = rs, ar
+    eng = ZeroEngine(_model("llama-tiny"), _cfg(3, 2, **kw), torch.device("cpu"), Comm())
+    gathers = []
+    orig_ag = comm_mod.Comm.all_gather
+
+    def ag(self, o, i, async_op=True):
+        gathers.append(o.numel())
+        return orig_ag(self, o, i, async_op=async_op)
+    comm_mod.Comm.all_gather = ag
+    grads0 = None
+    for mbs in _data("llama-tiny", 2, world * 2):
+        eng.train_step([(t[:, :-1], t[:, 1:]) for t in mbs[rank * 2:rank * 2 + 2]])
+        if grads0 is None:
+            grads0 = eng.full_grads()
+    comm_mod.Comm.all_gather = orig_ag
+    params = eng.full_params()
+    if rank == 0:
+        torch.save({"params": params, "grads0": grads0, "ops": ops_seen, "gathers": gathers,
+                    "groups": [(g.name, g.kind, g.P, [s.name for s in g.specs]) for g in eng.groups]}, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_prescale_gradients_and_predivide_factor(tmp_path):
+    """prescale_gradients: pre-divided gradients are SUM-reduced, post-scaled by factor / world -- the same
+    averages as the default AVG reductions (reference deepspeed_launcher.py:61-62, 168-169)."""
+    res = {}
+    for name, kw in (("avg", {}), ("pre", {"prescale_gradients": True, "gradient_predivide_factor": 4.0})):
+        out = str(tmp_path / f"{name}.pt")
+        mp.spawn(_knob_worker, args=(2, _port(), kw, out), nprocs=2, join=True)
+        res[name] = torch.load(out, weights_only=True)
+    grad_ops = lambda r: {avg for op, avg, n in r["ops"] if n > 8}  # noqa: E731  (skip the stats all-reduce)
+    assert grad_ops(res["avg"]) == {True} and grad_ops(res["pre"]) == {False}
+    for k, v in res["avg"]["grads0"].items():
+        err = float((res["pre"]["grads0"][k] - v).abs().max() / v.abs().max().clamp_min(1e-8))
+        assert err < 1e-5, (k, err)
+    for k, v in res["avg"]["params"].items():
+        assert float((res["pre"]["params"][k] - v).abs().max()) < 1e-4, k
+
+
+def test_param_persistence_threshold_keeps_small_tensors_replicated(tmp_path):
+    """stage3_param_persistence_threshold: norm weights (256 elements < 1e4) live in replicated '.persist'
+    groups that are never all-gathered; training matches the fully partitioned layout."""
+    res = {}
+    for name, thr in (("part", 0.0), ("persist", 1e4)):
+        out = str(tmp_path / f"{name}.pt")
+        kw = {"param_persistence_threshold": thr, "max_live_parameters": 0, "max_reuse_distance": 0}
+        mp.spawn(_knob_worker, args=(2, _port(), kw, out), nprocs=2, join=True)
+        res[name] = torch.load(out, weights_only=True)
+    pg = [g for g in res["persist"]["groups"] if g[1] == "persist"]
+    assert pg and all(g[2] == 1 for g in pg)
+    assert all(all(n.endswith("norm") for n in g[3]) for g in pg)
+    assert not any(g[1] == "persist" for g in res["part"]["groups"])
+    # every gathered buffer is a partitioned group: fewer gathered elements per step than without the split
+    assert sum(res["persist"]["gathers"]) < sum(res["part"]["gathers"])
+    # partitioned groups round per-micro-batch gradients to bf16 (scratch path), replicated ones accumulate fp32
+    _compare(res["persist"], res["part"]["params"], res["part"]["grads0"], 2)
+
+
+def test_offload_param_matches_device_params(tmp_path):
+    """offload_param=cpu (ZeRO-Infinity): the bf16 partition is host memory, gathers stage it first; the
+    training is the same as with device-resident parameters, with and without optimizer offload."""
+    res = {}
+    for name, kw in (("dev", {}), ("par", {"offload_param": "cpu"}),
+                     ("both", {"offload_param": "cpu", "offload_optimizer": "cpu"})):
+        out = str(tmp_path / f"{name}.pt")
+        mp.spawn(_knob_worker, args=(2, _port(), kw, out), nprocs=2, join=True)
+        res[name] = torch.load(out, weights_only=True)
+    for name in ("par", "both"):
+        for k, v in res["dev"]["grads0"].items():
+            assert torch.allclose(res[name]["grads0"][k], v, atol=1e-6, rtol=1e-4), (name, k)
+        _compare(res[name], res["dev"]["params"], res["dev"]["grads0"], 2)

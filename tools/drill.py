@@ -28,7 +28,8 @@ from distributed_llm_training_gpu_manager_amd.launcher.supervisor import JobRegi
 def train_argv(a, extra):
     return [sys.executable, "-m", "distributed_llm_training_gpu_manager_amd.train", "--model", a.model,
             "--seq-len", str(a.seq), "--micro-batch", "1", "--grad-accum", str(a.ga), "--zero-stage", "3",
-            "--lr", "3e-5", *(["--n-layers", str(a.n_layers)] if a.n_layers else []), *extra]
+            "--lr", "3e-5", *(["--n-layers", str(a.n_layers)] if a.n_layers else []),
+            "--keep-last", str(a.keep_last), "--ckpt-shm", a.ckpt_shm, "--ckpt-disk", str(a.ckpt_disk), *extra]
 
 
 def run(argv, timeout):
@@ -63,12 +64,14 @@ def drill_sigkill(a, work):
         time.sleep(0.2)
     log = open(job.log_path).read()
     resumed = re.findall(r"resumed from step (\d+) in ([0-9.]+)s", log)
+    via = re.findall(r"resumed from step \d+ in [0-9.]+s via (\S+)", log)
     hist = {}
     if os.path.exists(os.path.join(work, "kill.json")):
         hist = json.load(open(os.path.join(work, "kill.json"))).get("ckpt", [])
     return {"drill": "sigkill", "status": job.status, "exit_codes": job.exit_codes, "restarts": job.restarts,
             "mttr_s": [round(x, 2) for x in job.mttr_s], "resume_load_s": [float(s) for _, s in resumed],
-            "resumed_from_step": [int(s) for s, _ in resumed], "events": job.events, "ckpt_after_resume": hist,
+            "resumed_from_step": [int(s) for s, _ in resumed], "restored_from": via, "events": job.events,
+            "ckpt_after_resume": hist,
             "tail": log[-800:]}
 
 
@@ -79,8 +82,22 @@ def drill_spot(a, work):
     em = re.findall(r"emergency checkpoint at step (\d+) in ([0-9.]+)s", out)
     rc2, out2, dt2 = run(train_argv(a, ["--steps", str(a.k + 1), "--save-dir", ck, "--resume", "auto"]), a.timeout)
     res = re.findall(r"resumed from step (\d+) in ([0-9.]+)s", out2)
+    via = re.findall(r"resumed from step \d+ in [0-9.]+s via (\S+)", out2)
     return {"drill": "spot", "exit_code_preempted": rc, "emergency_ckpt": em, "restore_exit": rc2,
-            "restore": res, "restore_process_wall_s": round(dt2, 2), "tail": (out[-300:], out2[-300:])}
+            "restore": res, "restored_from": via, "restore_process_wall_s": round(dt2, 2),
+            "tail": (out[-300:], out2[-300:])}
+
+
+def _drop_shm(save_dir: str) -> None:
+    """Remove the /dev/shm snapshot tier a drill's save dir left behind (failed runs keep it for resume)."""
+    import glob
+    import hashlib
+    key = hashlib.sha1(os.path.abspath(save_dir).encode()).hexdigest()[:12]
+    for p in glob.glob(f"/dev/shm/dlgm-ckpt-{key}-*"):
+        try:
+            os.unlink(p)
+        except OSError:
+            pass
 
 
 def main():
@@ -93,11 +110,15 @@ def main():
     ap.add_argument("--k", type=int, default=3)
     ap.add_argument("--save-interval", type=int, default=2)
     ap.add_argument("--timeout", type=float, default=900)
+    ap.add_argument("--keep-last", type=int, default=1)
+    ap.add_argument("--ckpt-shm", default="auto", choices=["auto", "on", "off"])
+    ap.add_argument("--ckpt-disk", type=int, default=1, help="0: /dev/shm snapshot tier only (no disk tags)")
     ap.add_argument("--out", default="gpurun_out/drills.json")
     ap.add_argument("--work", default=None)
     a = ap.parse_args()
     work = a.work or tempfile.mkdtemp(prefix="dlgm_drill_")
     res = {"model": a.model, "n_layers": a.n_layers or "preset", "seq": a.seq, "ga": a.ga,
+           "keep_last": a.keep_last, "ckpt_shm": a.ckpt_shm, "ckpt_disk": a.ckpt_disk,
            "data": "synthetic token ids, random-init weights"}
     for d in a.drills.split(","):
         t0 = time.time()
@@ -109,6 +130,7 @@ def main():
             json.dump(res, f, indent=1)
         for sub in ("ck", "ck_spot"):  # the box's scratch disk holds one drill's checkpoints at a time
             shutil.rmtree(os.path.join(work, sub), ignore_errors=True)
+            _drop_shm(os.path.join(work, sub))
     shutil.rmtree(work, ignore_errors=True)
 
 
