@@ -46,6 +46,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
 at::Tensor dlgm_moe_combine_fwd(const at::Tensor& y, const at::Tensor& pos, const c10::optional<at::Tensor>& gates);
 std::tuple<at::Tensor, at::Tensor> dlgm_moe_combine_bwd(const at::Tensor& dout, const at::Tensor& y,
                                                         const at::Tensor& pos, const at::Tensor& gates);
+std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_moe_permute(const at::Tensor& topi, int64_t n_experts);
 // transpose.hip
 at::Tensor dlgm_transpose(const at::Tensor& x, const c10::optional<at::Tensor>& out);
 // embedding.hip
@@ -57,6 +58,10 @@ int64_t dlgm_gemm_lt(at::Tensor out, const at::Tensor& a, const at::Tensor& b, d
 at::Tensor dlgm_gemm_lt_tune(const at::Tensor& out, const at::Tensor& a, const at::Tensor& b, double beta,
                              int64_t n_heuristic, bool all_algos, int64_t reps);
 int64_t dlgm_gemm_lt_version();
+// gemm_mfma.hip
+void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bool accumulate,
+                    const c10::optional<at::Tensor>& offsets, int64_t mode, int64_t M, int64_t N, int64_t K,
+                    int64_t G, int64_t b_gstride);
 
 TORCH_LIBRARY(dlgm, m) {
   m.def("rmsnorm_fwd(Tensor x, Tensor? residual, Tensor w, float eps) -> (Tensor, Tensor, Tensor)");
@@ -72,6 +77,7 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("flash_attn_fwd(Tensor q, Tensor k, Tensor v, float softmax_scale, bool causal) -> (Tensor, Tensor)");
   m.def("moe_combine_fwd(Tensor y, Tensor pos, Tensor? gates) -> Tensor");
   m.def("moe_combine_bwd(Tensor dout, Tensor y, Tensor pos, Tensor gates) -> (Tensor, Tensor)");
+  m.def("moe_permute(Tensor topi, int n_experts) -> (Tensor, Tensor, Tensor)");
   m.def("transpose(Tensor x, Tensor(a!)? out=None) -> Tensor");
   m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, float softmax_scale, bool causal, Tensor? dqkv=None) -> (Tensor, Tensor, Tensor)");
   m.def("embedding_fwd(Tensor table, Tensor ids) -> Tensor");
@@ -80,6 +86,7 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("gemm_lt(Tensor(a!) out, Tensor a, Tensor b, float beta, int algo) -> int");
   m.def("gemm_lt_tune(Tensor out, Tensor a, Tensor b, float beta, int n_heuristic, bool all_algos, int reps) -> Tensor");
   m.def("gemm_lt_version() -> int", &dlgm_gemm_lt_version);
+  m.def("gemm_mfma(Tensor(a!) out, Tensor a, Tensor b, bool accumulate, Tensor? offsets, int mode, int M, int N, int K, int G, int b_gstride) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dlgm, CUDA, m) {
@@ -97,10 +104,12 @@ TORCH_LIBRARY_IMPL(dlgm, CUDA, m) {
   m.impl("flash_attn_bwd", &dlgm_flash_attn_bwd);
   m.impl("moe_combine_fwd", &dlgm_moe_combine_fwd);
   m.impl("moe_combine_bwd", &dlgm_moe_combine_bwd);
+  m.impl("moe_permute", &dlgm_moe_permute);
   m.impl("transpose", &dlgm_transpose);
   m.impl("embedding_fwd", &dlgm_embedding_fwd);
   m.impl("embedding_bwd_", &dlgm_embedding_bwd_);
   m.impl("router_topk", &dlgm_router_topk);
   m.impl("gemm_lt", &dlgm_gemm_lt);
   m.impl("gemm_lt_tune", &dlgm_gemm_lt_tune);
+  m.impl("gemm_mfma", &dlgm_gemm_mfma);
 }

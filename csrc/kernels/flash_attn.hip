@@ -139,8 +139,8 @@ __device__ __forceinline__ void dma16(const void* base, int nbytes, uint32_t vof
 
 // Loop-invariant LDS-DMA plan for a tile of ROWS x D bf16 rows that is re-staged every iteration
 // (the forward's recipe): the per-lane byte offsets of this wave's pieces are computed once, a
-// tile is then PPW buffer_load...lds per wave with a scalar row advance and no VALU. Rows at or
-// past the descriptor's end (row S) read as zeros. SWZ: 0 = row image, 1 = dual image, 2 = tr image.
+// tile is then PPW buffer_load...lds per wave with a scalar row advance and no VALU. On the tail
+// tile rows at or past S re-read row S-1 (so no address leaves the tensor). SWZ: 0 = row image, 1 = dual image, 2 = tr image.
 // A wave's pieces sit NW*PR rows apart (16 at D = 128, 32 at D = 64), a multiple of every swizzle's
 // row period, so they share ONE per-lane offset (1 VGPR) and differ only by a scalar soffset step.
 template <int D, int ROWS, int SWZ, int NW = 4>
@@ -149,20 +149,32 @@ struct TileDma {
   static_assert(NP % NW == 0, "pieces must split evenly over the waves");
   static_assert((NW * PR) % 16 == 0, "piece row step must be a multiple of the swizzle period");
   uint32_t off0;
-  int wave, nbytes;
+  int wave, nbytes, nrows;
   int64_t stride;
   const bf16* base;
-  __device__ __forceinline__ TileDma(const bf16* base_, int64_t row_stride, int nrows, int wave_, int lane)
-      : wave(wave_), nbytes((int)(((int64_t)(nrows - 1) * row_stride + D) * 2)), stride(row_stride), base(base_) {
+  __device__ __forceinline__ TileDma(const bf16* base_, int64_t row_stride, int nrows_, int wave_, int lane)
+      : wave(wave_), nbytes((int)(((int64_t)(nrows_ - 1) * row_stride + D) * 2)), nrows(nrows_), stride(row_stride),
+        base(base_) {
     const int rin = lane / CH, phys = lane % CH;
     const int row = wave * PR + rin;
     const int logical = SWZ == 2 ? swz_tr<D>(row, phys) : SWZ == 1 ? swz_dual<D>(row, phys) : swz_row<D>(row, phys);
     off0 = (uint32_t)((row * row_stride + logical * 8) * 2);
   }
   __device__ __forceinline__ void issue(bf16* img, int row0) const {
-    const uint32_t soff = (uint32_t)(row0 * stride * 2), step = (uint32_t)(NW * PR * stride * 2);
+    if (row0 + ROWS <= nrows) {  // whole tile in range: scalar row advance
+      const uint32_t soff = (uint32_t)(row0 * stride * 2), step = (uint32_t)(NW * PR * stride * 2);
 #pragma unroll
-    for (int j = 0; j < PPW; ++j) dma16(base, nbytes, off0, soff + j * step, img + (wave + NW * j) * 512);
+      for (int j = 0; j < PPW; ++j) dma16(base, nbytes, off0, soff + j * step, img + (wave + NW * j) * 512);
+      return;
+    }
+    // tail tile: every address stays inside the tensor -- rows at or past nrows re-read row nrows-1
+    // (finite; masked to zero weight by the kernels) and the whole offset goes through voffset
+    const int rin = wave * PR + (int)(threadIdx.x & 63) / CH;
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      const int r = min(row0 + NW * PR * j + rin, nrows - 1);
+      dma16(base, nbytes, off0 + (uint32_t)((int64_t)(r - rin) * stride * 2), 0, img + (wave + NW * j) * 512);
+    }
   }
 };
 

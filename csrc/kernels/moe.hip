@@ -10,6 +10,13 @@
 // The same forward kernel with gate = 1 sums the K per-slot input gradients back
 // onto the token (the adjoint of the dispatch gather) -- again without atomics.
 // One wave per token row, 16 B per lane per access.
+//
+// moe_permute: the expert-sort of the (token, k) slots ON THE DEVICE, in one single-workgroup launch
+// (E <= 32): per-thread expert histograms of a contiguous slot range -> one block-wide exclusive scan
+// over the [expert][thread] counts (which is exactly each thread's first position per expert, since
+// the sorted order is expert-major and slot-ordered within an expert, i.e. a stable argsort) ->
+// positions. Outputs: offsets [E + 1] (int32: the grouped-GEMM segment bounds), pos [T, K] (slot ->
+// sorted row), src [T*K] (sorted row -> token). Nothing is read back to the host.
 #include <torch/all.h>
 #include <c10/hip/HIPStream.h>
 #include "dlgm_common.h"
@@ -73,6 +80,51 @@ __global__ __launch_bounds__(256) void moe_combine_bwd_kernel(const bf16* __rest
   }
 }
 
+constexpr int kPermThreads = 1024;
+
+__global__ __launch_bounds__(kPermThreads) void moe_permute_kernel(const int64_t* __restrict__ topi, int64_t n, int K,
+                                                                   int E, int* __restrict__ offsets,
+                                                                   int64_t* __restrict__ pos,
+                                                                   int64_t* __restrict__ src) {
+  extern __shared__ int cnt[];  // [E][kPermThreads], then the per-wave scan totals
+  int* wsum = cnt + E * kPermThreads;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t per = (n + kPermThreads - 1) / kPermThreads;
+  const int64_t lo = min<int64_t>(n, t * per), hi = min<int64_t>(n, lo + per);
+  for (int e = 0; e < E; ++e) cnt[e * kPermThreads + t] = 0;
+  for (int64_t s = lo; s < hi; ++s) cnt[(int)topi[s] * kPermThreads + t] += 1;
+  __syncthreads();
+  // exclusive scan of the E*1024 counts in [expert][thread] order: thread t owns entries E*t .. E*t+E-1
+  int local[32];
+  int run = 0;
+  for (int j = 0; j < E; ++j) {
+    local[j] = run;
+    run += cnt[t * E + j];  // flat index f = t*E + j over the [E][1024] array
+  }
+  int incl = run;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  int wbase = 0;
+  for (int i = 0; i < wv; ++i) wbase += wsum[i];
+  const int excl = wbase + incl - run;
+  __syncthreads();
+  for (int j = 0; j < E; ++j) cnt[t * E + j] = excl + local[j];  // now the first position of (e, thread)
+  __syncthreads();
+  if (t < E) offsets[t] = cnt[t * kPermThreads];  // expert t's first row = position of (t, thread 0)
+  if (t == 0) offsets[E] = (int)n;
+  for (int64_t s = lo; s < hi; ++s) {
+    const int e = (int)topi[s];
+    const int p = cnt[e * kPermThreads + t]++;
+    pos[s] = p;
+    src[p] = s / K;
+  }
+}
+
 void check(const at::Tensor& y, const at::Tensor& pos, int64_t D) {
   TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kBFloat16 && y.is_contiguous() && y.dim() == 2,
               "moe: rows must be a contiguous [N, D] bf16 GPU tensor");
@@ -105,6 +157,24 @@ at::Tensor dlgm_moe_combine_fwd(const at::Tensor& y, const at::Tensor& pos, cons
   }
   DLGM_CHECK_HIP(hipGetLastError());
   return out;
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_moe_permute(const at::Tensor& topi, int64_t n_experts) {
+  TORCH_CHECK(topi.is_cuda() && topi.scalar_type() == at::kLong && topi.is_contiguous() && topi.dim() == 2,
+              "moe_permute: topi must be a contiguous int64 [T, K] GPU tensor");
+  TORCH_CHECK(n_experts >= 1 && n_experts <= 32, "moe_permute: 1..32 experts");
+  const int64_t T = topi.size(0), K = topi.size(1), n = T * K;
+  TORCH_CHECK(n < (1ll << 31), "moe_permute: too many slots");
+  auto offsets = at::empty({n_experts + 1}, topi.options().dtype(at::kInt));
+  auto pos = at::empty({T, K}, topi.options());
+  auto src = at::empty({n}, topi.options());
+  const size_t lds = (size_t)(n_experts * kPermThreads + kPermThreads / 64) * sizeof(int);
+  auto stream = c10::hip::getCurrentHIPStream();
+  moe_permute_kernel<<<1, kPermThreads, lds, stream>>>(topi.data_ptr<int64_t>(), n, (int)K, (int)n_experts,
+                                                      offsets.data_ptr<int>(), pos.data_ptr<int64_t>(),
+                                                      src.data_ptr<int64_t>());
+  DLGM_CHECK_HIP(hipGetLastError());
+  return {offsets, pos, src};
 }
 
 std::tuple<at::Tensor, at::Tensor> dlgm_moe_combine_bwd(const at::Tensor& dout, const at::Tensor& y,

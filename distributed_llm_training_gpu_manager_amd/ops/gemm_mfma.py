@@ -1,0 +1,88 @@
+"""Python entry points of the hand-written MFMA GEMM (csrc/kernels/gemm_mfma.hip).
+
+``mfma_mm(out, a, b, acc)``   out (+)= a @ b for bf16 operand views of any unit-stride layout
+``grouped_mm(x, w, offsets)`` expert-grouped forward / input-gradient GEMM (rows split by offsets)
+``grouped_wgrad(out, a, b, offsets)`` expert-grouped weight gradient (reduction rows split by offsets)
+
+The group offsets are an int32 device tensor, so an MoE layer launches its expert GEMMs without
+reading the routing counts on the host. CPU tensors take an fp32 reference path (tests).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from .._native import hip_ops, use_native
+
+DENSE, GROUP_M, GROUP_K = 0, 1, 2
+
+
+def _ok(t: torch.Tensor) -> bool:
+    return t.dtype == torch.bfloat16 and t.data_ptr() % 16 == 0
+
+
+def supported(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Can the dense kernel take this problem? (N % 256, K % 64, unit-stride operands, 16-B rows)."""
+    if not (use_native(out) and _ok(a) and _ok(b)) or a.dim() != 2 or b.dim() != 2:
+        return False
+    M, K = a.shape
+    N = b.shape[1]
+    ak = a.stride(1) == 1
+    lda = a.stride(0) if ak else a.stride(1)
+    bk = b.stride(0) == 1 and b.stride(1) != 1
+    if not bk and b.stride(1) != 1:
+        return False
+    if not ak and a.stride(0) != 1:
+        return False
+    ldb = b.stride(1) if bk else b.stride(0)
+    return (N % 256 == 0 and K % 64 == 0 and (ak or M % 256 == 0) and lda % 8 == 0 and ldb % 8 == 0
+            and out.stride(-1) == 1 and out.stride(0) % 4 == 0 and out.dtype in (torch.float32, torch.bfloat16))
+
+
+def mfma_mm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, acc: bool = False) -> torch.Tensor:
+    if use_native(out):
+        hip_ops().gemm_mfma(out, a, b, acc, None, DENSE, a.shape[0], b.shape[1], a.shape[1], 1, 0)
+        return out
+    r = a.float() @ b.float()
+    return out.add_(r) if acc else out.copy_(r)
+
+
+def grouped_mm(x: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, transpose_w: bool = True,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out[rows of group e] = x[rows of e] @ (w[e]^T if transpose_w else w[e]); x [R, K] row-major,
+    w [G, N, K] (transpose_w) or [G, K, N]; offsets int32 [G + 1] on the device."""
+    G = w.shape[0]
+    N = w.shape[1] if transpose_w else w.shape[2]
+    R, K = x.shape
+    if out is None:
+        out = torch.empty(R, N, dtype=x.dtype, device=x.device)
+    if use_native(x):
+        b = w.transpose(1, 2) if transpose_w else w
+        hip_ops().gemm_mfma(out, x, b, False, offsets, GROUP_M, R, N, K, G, w.stride(0))
+        return out
+    offs = offsets.tolist()
+    for e in range(G):
+        lo, hi = offs[e], offs[e + 1]
+        if hi > lo:
+            we = w[e].t() if transpose_w else w[e]
+            out[lo:hi] = (x[lo:hi].float() @ we.float()).to(out.dtype)
+    return out
+
+
+def grouped_wgrad(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, offsets: torch.Tensor,
+                  acc: bool = False) -> torch.Tensor:
+    """out[e] (+)= a[rows of e]^T @ b[rows of e]: a [R, M], b [R, N] row-major (token rows), out [G, M, N]."""
+    G, M, N = out.shape
+    if use_native(out):
+        hip_ops().gemm_mfma(out, a.t(), b, acc, offsets, GROUP_K, M, N, a.shape[0], G, 0)
+        return out
+    offs = offsets.tolist()
+    for e in range(G):
+        lo, hi = offs[e], offs[e + 1]
+        r = a[lo:hi].float().t() @ b[lo:hi].float()
+        if acc:
+            out[e].add_(r.to(out.dtype))
+        else:
+            out[e].copy_(r.to(out.dtype))
+    return out

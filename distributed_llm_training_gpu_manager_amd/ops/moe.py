@@ -20,6 +20,23 @@ def router_topk(logits: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tenso
     return probs, topi, torch.softmax(topv, dim=-1).contiguous()
 
 
+def moe_permute(topi: torch.Tensor, n_experts: int) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Expert-sort of the (token, k) slots on the device -> (offsets int32 [E+1], pos [T, K] slot -> sorted
+    row, src [T*K] sorted row -> token); stable (token order within an expert), no host sync."""
+    topi = topi.contiguous()
+    if use_native(topi):
+        return hip_ops().moe_permute(topi, n_experts)
+    T, K = topi.shape
+    flat = topi.reshape(-1)
+    order = torch.argsort(flat, stable=True)
+    counts = torch.bincount(flat, minlength=n_experts)
+    offsets = torch.zeros(n_experts + 1, dtype=torch.int32, device=topi.device)
+    offsets[1:] = torch.cumsum(counts, 0).to(torch.int32)
+    pos = torch.empty_like(order)
+    pos[order] = torch.arange(order.numel(), device=order.device)
+    return offsets, pos.view(T, K), torch.div(order, K, rounding_mode="floor")
+
+
 def moe_combine(y: torch.Tensor, pos: torch.Tensor, gates: Optional[torch.Tensor]) -> torch.Tensor:
     """out[t] = sum_k gates[t,k] * y[pos[t,k]]  (gates=None -> plain sum)."""
     if use_native(y):

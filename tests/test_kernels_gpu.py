@@ -153,6 +153,8 @@ ATTN_CASES = [
     (2, 192, 4, 2, 64, True),
     (1, 256, 4, 2, 128, False),
     (1, 1024, 8, 2, 128, True),
+    (1, 40, 4, 2, 128, True),     # one partial tile only
+    (2, 200, 4, 2, 64, False),    # tail, non-causal (keys past S masked, V rows past S finite)
 ]
 
 
@@ -213,6 +215,22 @@ def test_moe_combine_fwd_bwd(K):
     dy_ref, dg_ref = moe_combine_bwd(dout, y, pos, gates)
     dy, dg = moe_combine_bwd(dout.to(DEV), y.to(DEV), pos.to(DEV), gates.to(DEV))
     assert rel_err(dy, dy_ref) < 1e-2 and rel_err(dg, dg_ref) < 1e-3
+
+
+@pytest.mark.parametrize("T,K,E", [(1, 2, 8), (133, 2, 8), (4096, 2, 8), (16384, 2, 8), (3000, 4, 32),
+                                    (777, 1, 3)])
+def test_moe_permute_matches_stable_sort(T, K, E):
+    from distributed_llm_training_gpu_manager_amd.ops.moe import moe_permute
+
+    torch.manual_seed(T)
+    topi = torch.randint(0, E, (T, K))
+    if E > 2:
+        topi[topi == E - 1] = 0  # an expert with no tokens
+    off_ref, pos_ref, src_ref = moe_permute(topi, E)
+    off, pos, src = moe_permute(topi.to(DEV), E)
+    assert off.dtype == torch.int32 and off.shape == (E + 1,)
+    assert torch.equal(off.cpu(), off_ref)
+    assert torch.equal(pos.cpu(), pos_ref) and torch.equal(src.cpu(), src_ref)
 
 
 @pytest.mark.parametrize("Hq,Hkv", [(4, 4), (8, 2)])
