@@ -57,6 +57,8 @@ def main() -> int:
                     help="after the timed steps, trace this many extra steps with torch.profiler")
     ap.add_argument("--profile-dir", default="gpurun_out/torch_trace")
     ap.add_argument("--no-telemetry", action="store_true", help="do not poll amdsmi during the run")
+    ap.add_argument("--comm-sweep", default="auto", choices=["auto", "on", "off"],
+                    help="after the timed steps, measure RCCL busbw over xGMI (auto: when WORLD_SIZE > 1)")
     ap.add_argument("--telemetry-interval", type=float, default=2.0)
     ap.add_argument("--n-layers", type=int, default=0,
                     help="override the preset's layer count (kernel profiling of big models on one GPU only; "
@@ -127,6 +129,12 @@ def main() -> int:
             for i in range(args.profile_steps):
                 eng.train_step(steps_data[args.warmup + args.steps + i])
 
+    comm_rows = None
+    if args.comm_sweep == "on" or (args.comm_sweep == "auto" and env.world > 1):
+        # outside the timed region: the xGMI bus-bandwidth curve of this node at this world size
+        from distributed_llm_training_gpu_manager_amd.utils.commbench import sweep
+        comm_rows = sweep(comm, env.device, sizes_mb=(16, 64, 256) if env.device.type == "cuda" else (1,))
+
     tokens_per_step_gpu = args.mbs * args.seq * args.ga
     total_tokens = tokens_per_step_gpu * env.world * args.steps
     tps = total_tokens / elapsed
@@ -172,6 +180,7 @@ def main() -> int:
                 "zero3_resident_gathered_params": eng.live_plan.resident_params,
                 "mem": {k: round(v, 1) for k, v in eng.memory_report().items()},
                 "telemetry": telem,
+                "comm_busbw": comm_rows,
             },
         }
         print(json.dumps(out), flush=True)

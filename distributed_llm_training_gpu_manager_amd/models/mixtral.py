@@ -4,9 +4,10 @@ Attention is the Llama block's (GQA, RoPE theta 1e6). The FFN is a routed mixtur
 
     logits = hn2 @ Wr^T                   [T, E]   (fp32 softmax)
     top-2 per token, gates = softmax over the two selected logits (Mixtral)
-    sort (token, k) slots by expert       one gather into expert order
+    sort (token, k) slots by expert       one-workgroup HIP counting sort (moe_permute), one gather
     EP all-to-all                          rows to the rank owning the expert (RCCL)
-    per local expert: SwiGLU MLP           dense hipBLASLt GEMMs on contiguous rows
+    local experts: SwiGLU MLP              grouped MFMA GEMMs, one launch for all experts, group
+                                           offsets read on the device (no host sync at EP = 1)
     EP all-to-all back, combine            out[t] = sum_k gate * y[slot]  (HIP gather kernel)
 
 Backward is hand-written: the combine adjoint gives d(expert outputs) and d(gates),
@@ -27,7 +28,8 @@ import torch
 
 from .. import ops
 from ..ops.gemm import grad_mm
-from ..ops.moe import moe_combine, moe_combine_bwd
+from ..ops import gemm_mfma as gm
+from ..ops.moe import moe_combine, moe_combine_bwd, moe_permute
 from ..parallel.ep import ExpertDispatcher
 from .common import ParamSpec, Params, StepContext, Unit
 from .config import ModelConfig
@@ -65,27 +67,36 @@ class MixtralBlock(LlamaBlock):
         c = self.cfg
         T, E, K = hn2.shape[0], c.n_experts, c.top_k
         probs, topi, gates = ops.router_topk(torch.mm(hn2, p["router"].t()), K)  # [K9]
-        flat = topi.reshape(-1)
-        order = torch.argsort(flat, stable=True)
-        counts = torch.bincount(flat, minlength=E)
-        tok = torch.div(order, K, rounding_mode="floor")
-        pos = torch.empty_like(order)
-        pos[order] = torch.arange(order.numel(), device=order.device)
-        pos = pos.view(T, K)
+        offsets, pos, tok = moe_permute(topi, E)  # expert sort on the device, no host read
+        counts = (offsets[1:] - offsets[:-1]).long()
         x_sorted = hn2.index_select(0, tok)
         disp = self.dispatcher(ctx)
-        x_local, dctx = disp.dispatch(x_sorted, counts)
-        y_local, exp_saved = self._experts_fwd(p, x_local, dctx.local_counts)
+        x_local, dctx = disp.dispatch(x_sorted, counts, offsets)
+        y_local, exp_saved = self._experts_fwd(p, x_local, dctx)
         y_sorted = disp.combine(y_local, dctx)
         out = moe_combine(y_sorted, pos, gates)
         f = counts.float() / float(T * K) * K  # fraction of tokens choosing each expert (summed over k)
         ctx.aux.setdefault("moe_aux", []).append(float(E) * (f * probs.mean(0)).sum())
         return out, (probs, topi, gates, pos, f, x_local, dctx, exp_saved, y_sorted)
 
-    def _experts_fwd(self, p: Params, x: torch.Tensor, counts: List[int]):
+    def _grouped(self, x: torch.Tensor) -> bool:
+        """Expert GEMMs as single grouped MFMA launches (csrc/kernels/gemm_mfma.hip) with the device
+        offsets: no host read of the routing counts, no per-expert launches."""
+        c = self.cfg
+        return gm.grouped_supported(x) and (2 * c.ffn_dim) % 256 == 0 and c.d_model % 256 == 0 \
+            and c.ffn_dim % 64 == 0 and c.d_model % 64 == 0
+
+    def _experts_fwd(self, p: Params, x: torch.Tensor, dctx):
         c = self.cfg
         F = c.ffn_dim
         M = x.shape[0]
+        if self._grouped(x):
+            offs = dctx.local_offsets
+            gu_all = gm.grouped_mm(x, p["w_gate_up"], offs)
+            a_all = ops.swiglu_fwd(gu_all)
+            y = gm.grouped_mm(a_all, p["w_down"], offs)
+            return y, (gu_all, a_all, dctx)
+        counts = dctx.counts()
         gu_all = x.new_empty((M, 2 * F))
         y = x.new_empty((M, c.d_model))
         off = 0
@@ -99,10 +110,20 @@ class MixtralBlock(LlamaBlock):
             if n:
                 torch.mm(a_all.narrow(0, off, n), p["w_down"][e].t(), out=y.narrow(0, off, n))
             off += n
-        return y, (gu_all, a_all, counts)
+        return y, (gu_all, a_all, dctx)
 
     def _experts_bwd(self, p: Params, g: Params, x: torch.Tensor, dy: torch.Tensor, saved, acc: bool):
-        gu_all, a_all, counts = saved
+        gu_all, a_all, dctx = saved
+        if self._grouped(x) and gm.GROUPED_WGRAD:
+            offs = dctx.local_offsets
+            dy = dy.contiguous()
+            da_all = gm.grouped_mm(dy, p["w_down"], offs, transpose_w=False)
+            gm.grouped_wgrad(g["w_down"], dy, a_all, offs, acc)
+            dgu_all = ops.swiglu_bwd(da_all, gu_all)
+            del da_all
+            gm.grouped_wgrad(g["w_gate_up"], dgu_all, x, offs, acc)
+            return gm.grouped_mm(dgu_all, p["w_gate_up"], offs, transpose_w=False)
+        counts = dctx.counts()
         dx = torch.empty_like(x)
         da_all = torch.empty_like(a_all)
         off = 0

@@ -16,6 +16,8 @@ import torch
 from .._native import hip_ops, use_native
 
 DENSE, GROUP_M, GROUP_K = 0, 1, 2
+# the grouped weight-gradient mode is used by the models only once it has passed on the hardware
+GROUPED_WGRAD = False
 
 
 def _ok(t: torch.Tensor) -> bool:
@@ -38,6 +40,11 @@ def supported(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> bool:
     ldb = b.stride(1) if bk else b.stride(0)
     return (N % 256 == 0 and K % 64 == 0 and (ak or M % 256 == 0) and lda % 8 == 0 and ldb % 8 == 0
             and out.stride(-1) == 1 and out.stride(0) % 4 == 0 and out.dtype in (torch.float32, torch.bfloat16))
+
+
+def grouped_supported(x: torch.Tensor) -> bool:
+    """Can the grouped kernels take rows `x` (bf16, row-major, 16-B aligned, on the GPU with the extension)?"""
+    return use_native(x) and _ok(x) and x.dim() == 2 and x.stride(1) == 1 and x.stride(0) % 8 == 0
 
 
 def mfma_mm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, acc: bool = False) -> torch.Tensor:

@@ -53,7 +53,15 @@ class DispatchCtx:
     send_splits: List[int]
     recv_splits: List[int]
     regroup: Optional[torch.Tensor]  # recv order -> local-expert-major order
-    local_counts: List[int]
+    local_counts: Optional[List[int]]  # host copy (None until asked for at EP = 1)
+    local_offsets: Optional[torch.Tensor] = None  # int32 [El + 1] on the device: expert row ranges
+
+    def counts(self) -> List[int]:
+        """Host per-local-expert row counts (a device sync at EP = 1; the per-expert fallback path only)."""
+        if self.local_counts is None:
+            o = self.local_offsets.tolist()
+            self.local_counts = [b - a for a, b in zip(o[:-1], o[1:])]
+        return self.local_counts
 
 
 class ExpertDispatcher:
@@ -65,11 +73,15 @@ class ExpertDispatcher:
         assert n_experts % self.W == 0, "n_experts must be divisible by the EP size"
         self.El = n_experts // self.W
 
-    def dispatch(self, x_sorted: torch.Tensor, counts: torch.Tensor) -> Tuple[torch.Tensor, DispatchCtx]:
-        """x_sorted: rows grouped by global expert id (counts[e] rows each)."""
+    def dispatch(self, x_sorted: torch.Tensor, counts: torch.Tensor,
+                 offsets: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, DispatchCtx]:
+        """x_sorted: rows grouped by global expert id (counts[e] rows each; `offsets` = the int32 exclusive
+        prefix of counts on the device, from ops.moe_permute). At EP = 1 nothing is read on the host."""
         if self.W == 1:
-            lc = counts.tolist()
-            return x_sorted, DispatchCtx([x_sorted.shape[0]], [x_sorted.shape[0]], None, lc)
+            if offsets is None:
+                offsets = torch.zeros(self.E + 1, dtype=torch.int32, device=counts.device)
+                offsets[1:] = torch.cumsum(counts, 0)
+            return x_sorted, DispatchCtx([x_sorted.shape[0]], [x_sorted.shape[0]], None, None, offsets)
         recv = torch.empty_like(counts)
         self.comm.all_to_all_single(recv, counts.contiguous())  # [src, local expert] counts
         c_send = counts.view(self.W, self.El).sum(1).tolist()
@@ -84,7 +96,9 @@ class ExpertDispatcher:
         offs = starts.view(self.W, self.El)
         idx = [torch.arange(int(offs[s, e]), int(offs[s, e] + mat[s, e])) for e in range(self.El) for s in range(self.W)]
         regroup = torch.cat(idx).to(x_sorted.device) if idx else torch.zeros(0, dtype=torch.long, device=x_sorted.device)
-        ctx = DispatchCtx(c_send, c_recv, regroup, mat.sum(0).tolist())
+        lc = mat.sum(0).tolist()
+        lo = torch.tensor([0] + lc, dtype=torch.int32).cumsum(0, dtype=torch.int32).to(x_sorted.device, non_blocking=True)
+        ctx = DispatchCtx(c_send, c_recv, regroup, lc, lo)
         return out.index_select(0, regroup), ctx
 
     def redispatch(self, rows_sorted: torch.Tensor, ctx: DispatchCtx) -> torch.Tensor:

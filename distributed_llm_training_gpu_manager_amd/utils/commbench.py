@@ -1,0 +1,68 @@
+"""RCCL collective bus-bandwidth measurement (rccl-tests conventions), shared by tools/comm_bench.py and
+the multi-GPU bench (bench.py measures the xGMI curve after its timed steps when WORLD_SIZE > 1).
+
+algbw = bytes / time; busbw = algbw * (W-1)/W for all_gather / reduce_scatter / all_to_all and
+2(W-1)/W for all_reduce. The slowest rank defines each collective's time.
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict, List, Sequence
+
+import torch
+
+from ..parallel.comm import Comm
+
+FACTOR = {"all_gather": lambda w: (w - 1) / w, "reduce_scatter": lambda w: (w - 1) / w,
+          "all_to_all": lambda w: (w - 1) / w, "all_reduce": lambda w: 2 * (w - 1) / w}
+
+
+def run(op: str, comm: Comm, nbytes: int, device, dtype, iters: int, warmup: int) -> float:
+    W = comm.world
+    esz = torch.tensor([], dtype=dtype).element_size()
+    n = max(W, nbytes // esz // W * W)
+    if op == "all_gather":
+        inp = torch.randn(n // W, device=device).to(dtype)
+        out = torch.empty(n, device=device, dtype=dtype)
+        fn = lambda: comm.all_gather(out, inp, async_op=False)  # noqa: E731
+    elif op == "reduce_scatter":
+        inp = torch.randn(n, device=device).to(dtype)
+        out = torch.empty(n // W, device=device, dtype=dtype)
+        fn = lambda: comm.reduce_scatter(out, inp, avg=False, async_op=False)  # noqa: E731
+    elif op == "all_reduce":
+        buf = torch.randn(n, device=device).to(dtype)
+        fn = lambda: comm.all_reduce(buf, async_op=False)  # noqa: E731
+    elif op == "all_to_all":
+        inp = torch.randn(n, device=device).to(dtype)
+        out = torch.empty(n, device=device, dtype=dtype)
+        fn = lambda: comm.all_to_all_single(out, inp)  # noqa: E731
+    else:
+        raise ValueError(op)
+    sync = torch.cuda.synchronize if device.type == "cuda" else (lambda: None)
+    for _ in range(warmup):
+        fn().wait()
+    sync()
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn().wait()
+    sync()
+    dt = (time.perf_counter() - t0) / iters
+    t = torch.tensor([dt], dtype=torch.float32, device=device)
+    comm.all_reduce_max(t)  # the slowest rank defines the collective's time
+    return float(t)
+
+
+
+def sweep(comm: Comm, device, ops: Sequence[str] = ("all_gather", "reduce_scatter", "all_reduce", "all_to_all"),
+          sizes_mb: Sequence[float] = (16, 64, 256), dtype=torch.bfloat16, iters: int = 5,
+          warmup: int = 2) -> List[Dict]:
+    rows = []
+    for op in ops:
+        for mb in sizes_mb:
+            nbytes = int(mb * (1 << 20))
+            dt = run(op, comm, nbytes, device, dtype, iters, warmup)
+            algbw = nbytes / dt / 1e9
+            rows.append({"op": op, "MiB": mb, "time_us": round(dt * 1e6, 1), "algbw_GBps": round(algbw, 1),
+                         "busbw_GBps": round(algbw * FACTOR[op](comm.world), 1), "world": comm.world})
+    return rows

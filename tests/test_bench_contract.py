@@ -49,6 +49,7 @@ def test_bench_single_process():
     out = _run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--model", "llama-tiny", "--seq", "64",
                 "--ga", "2"])
     _check(out, 1, 2, 1)
+    assert out["extra"]["comm_busbw"] is None
 
 
 def test_bench_torchrun_two_ranks():
@@ -57,3 +58,5 @@ def test_bench_torchrun_two_ranks():
                 "--warmup", "1", "--model", "llama-tiny", "--seq", "64", "--ga", "2"])
     _check(out, 2, 2, 1)
     assert out["extra"]["zero3_allgathers_per_step"] > 0  # partitioned: the residency plan gathers once per unit
+    ops = {r["op"] for r in out["extra"]["comm_busbw"]}  # the post-timing RCCL/xGMI sweep (gloo here)
+    assert ops == {"all_gather", "reduce_scatter", "all_reduce", "all_to_all"}

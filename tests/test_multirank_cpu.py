@@ -155,7 +155,7 @@ def _ep_worker(rank, world, port, model, stage, out):
 
     def spy(self, p, hn2, ctx):
         out_ = orig(self, p, hn2, ctx)
-        counts.append(list(out_[1][6].local_counts))
+        counts.append(list(out_[1][6].counts()))
         return out_
     mixtral.MixtralBlock.moe_forward = spy
     t = _data(model, 1, world, seq=8, mbs=1)[0][rank]

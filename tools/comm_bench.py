@@ -15,7 +15,6 @@ import argparse
 import json
 import os
 import sys
-import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -23,45 +22,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from distributed_llm_training_gpu_manager_amd.parallel.comm import Comm, init_distributed  # noqa: E402
-
-FACTOR = {"all_gather": lambda w: (w - 1) / w, "reduce_scatter": lambda w: (w - 1) / w,
-          "all_to_all": lambda w: (w - 1) / w, "all_reduce": lambda w: 2 * (w - 1) / w}
-
-
-def run(op: str, comm: Comm, nbytes: int, device, dtype, iters: int, warmup: int) -> float:
-    W = comm.world
-    esz = torch.tensor([], dtype=dtype).element_size()
-    n = max(W, nbytes // esz // W * W)
-    if op == "all_gather":
-        inp = torch.randn(n // W, device=device).to(dtype)
-        out = torch.empty(n, device=device, dtype=dtype)
-        fn = lambda: comm.all_gather(out, inp, async_op=False)  # noqa: E731
-    elif op == "reduce_scatter":
-        inp = torch.randn(n, device=device).to(dtype)
-        out = torch.empty(n // W, device=device, dtype=dtype)
-        fn = lambda: comm.reduce_scatter(out, inp, avg=False, async_op=False)  # noqa: E731
-    elif op == "all_reduce":
-        buf = torch.randn(n, device=device).to(dtype)
-        fn = lambda: comm.all_reduce(buf, async_op=False)  # noqa: E731
-    elif op == "all_to_all":
-        inp = torch.randn(n, device=device).to(dtype)
-        out = torch.empty(n, device=device, dtype=dtype)
-        fn = lambda: comm.all_to_all_single(out, inp)  # noqa: E731
-    else:
-        raise ValueError(op)
-    sync = torch.cuda.synchronize if device.type == "cuda" else (lambda: None)
-    for _ in range(warmup):
-        fn().wait()
-    sync()
-    comm.barrier()
-    t0 = time.perf_counter()
-    for _ in range(iters):
-        fn().wait()
-    sync()
-    dt = (time.perf_counter() - t0) / iters
-    t = torch.tensor([dt], dtype=torch.float32, device=device)
-    comm.all_reduce_max(t)  # the slowest rank defines the collective's time
-    return float(t)
+from distributed_llm_training_gpu_manager_amd.utils.commbench import FACTOR, run  # noqa: E402
 
 
 def main(argv=None) -> list:
