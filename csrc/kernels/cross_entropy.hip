@@ -20,13 +20,14 @@ namespace {
 constexpr int kThreads = 512;
 constexpr int kWaves = kThreads / 64;
 
-__global__ __launch_bounds__(kThreads) void ce_kernel(bf16* __restrict__ logits, const int64_t* __restrict__ labels,
+template <typename E>
+__global__ __launch_bounds__(kThreads) void ce_kernel(E* __restrict__ logits, const int64_t* __restrict__ labels,
                                                       float* __restrict__ loss, float* __restrict__ lse_out,
                                                       int64_t V, int64_t row_stride, int64_t ignore_index,
                                                       float grad_scale, bool compute_grad) {
   __shared__ float red[kWaves];
   const int64_t row = blockIdx.x;
-  bf16* x = logits + row * row_stride;
+  E* x = logits + row * row_stride;
   const int64_t label = labels[row];
   const int64_t nvec = V >> 3;
   float m = -INFINITY, s = 0.f;
@@ -72,7 +73,7 @@ __global__ __launch_bounds__(kThreads) void ce_kernel(bf16* __restrict__ logits,
   for (int64_t j = nvec * 8 + threadIdx.x; j < V; j += kThreads) {
     float g = __expf((float)x[j] - lse) * gs;
     if (j == label) g -= gs;
-    x[j] = (bf16)g;
+    x[j] = (E)g;
   }
 }
 
@@ -83,9 +84,8 @@ __global__ __launch_bounds__(kThreads) void ce_kernel(bf16* __restrict__ logits,
 std::tuple<at::Tensor, at::Tensor> dlgm_cross_entropy_(at::Tensor logits, const at::Tensor& labels,
                                                        int64_t ignore_index, double grad_scale,
                                                        bool compute_grad) {
-  TORCH_CHECK(logits.is_cuda() && logits.scalar_type() == at::kBFloat16 && logits.dim() == 2 &&
-                  logits.stride(1) == 1,
-              "cross_entropy: logits must be a [T, V] bf16 GPU tensor with unit inner stride");
+  TORCH_CHECK(logits.is_cuda() && DLGM_IS16(logits) && logits.dim() == 2 && logits.stride(1) == 1,
+              "cross_entropy: logits must be a [T, V] bf16/fp16 GPU tensor with unit inner stride");
   TORCH_CHECK(logits.stride(0) % 8 == 0, "cross_entropy: row stride must be a multiple of 8");
   TORCH_CHECK(labels.scalar_type() == at::kLong && labels.numel() == logits.size(0) && labels.is_contiguous(),
               "cross_entropy: labels must be contiguous int64 [T]");
@@ -94,9 +94,11 @@ std::tuple<at::Tensor, at::Tensor> dlgm_cross_entropy_(at::Tensor logits, const 
   auto lse = at::empty({T}, logits.options().dtype(at::kFloat));
   if (T == 0) return {loss, lse};
   auto stream = c10::hip::getCurrentHIPStream();
-  ce_kernel<<<T, kThreads, 0, stream>>>(reinterpret_cast<bf16*>(logits.data_ptr()), labels.data_ptr<int64_t>(),
-                                        loss.data_ptr<float>(), lse.data_ptr<float>(), V, logits.stride(0),
-                                        ignore_index, (float)grad_scale, compute_grad);
+  DLGM_DISPATCH_16(logits.scalar_type(), E,
+                   ce_kernel<E><<<T, kThreads, 0, stream>>>(reinterpret_cast<E*>(logits.data_ptr()),
+                                                            labels.data_ptr<int64_t>(), loss.data_ptr<float>(),
+                                                            lse.data_ptr<float>(), V, logits.stride(0), ignore_index,
+                                                            (float)grad_scale, compute_grad));
   DLGM_CHECK_HIP(hipGetLastError());
   return {loss, lse};
 }

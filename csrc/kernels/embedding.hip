@@ -37,10 +37,10 @@ __global__ __launch_bounds__(256) void embedding_fwd_kernel(const bf16* __restri
 }
 
 // sorted_ids / order: ids sorted ascending (stable) and the token index of each sorted slot.
-template <bool F32G>
+template <typename E, bool F32G>
 __global__ __launch_bounds__(256) void embedding_bwd_kernel(const int64_t* __restrict__ sorted_ids,
                                                             const int64_t* __restrict__ order,
-                                                            const bf16* __restrict__ dy, void* __restrict__ grad,
+                                                            const E* __restrict__ dy, void* __restrict__ grad,
                                                             int64_t T, int64_t D, int64_t V) {
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void embedding_bwd_kernel(const int64_t* __res
       *reinterpret_cast<f32x4*>(g) = (f32x4){a[0] + s[0], a[1] + s[1], a[2] + s[2], a[3] + s[3]};
       *reinterpret_cast<f32x4*>(g + 4) = (f32x4){b[0] + s[4], b[1] + s[5], b[2] + s[6], b[3] + s[7]};
     } else {
-      bf16* g = reinterpret_cast<bf16*>(grad) + id * D + c;
+      E* g = reinterpret_cast<E*>(grad) + id * D + c;
       store8f(g, load8f(g) + s);
     }
   }
@@ -115,8 +115,9 @@ __global__ __launch_bounds__(256) void router_topk_kernel(const float* __restric
 }  // namespace
 
 at::Tensor dlgm_embedding_fwd(const at::Tensor& table, const at::Tensor& ids) {
-  TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kBFloat16 && table.is_contiguous() && table.dim() == 2,
-              "embedding: table must be a contiguous [V, D] bf16 GPU tensor");
+  // a row copy: the 16-bit payload moves bit-exactly whether it is bf16 or fp16
+  TORCH_CHECK(table.is_cuda() && DLGM_IS16(table) && table.is_contiguous() && table.dim() == 2,
+              "embedding: table must be a contiguous [V, D] bf16/fp16 GPU tensor");
   TORCH_CHECK(ids.is_cuda() && ids.scalar_type() == at::kLong && ids.is_contiguous(), "embedding: ids must be int64");
   const int64_t V = table.size(0), D = table.size(1), T = ids.numel();
   TORCH_CHECK(D % 8 == 0, "embedding: D must be a multiple of 8");
@@ -133,8 +134,8 @@ at::Tensor dlgm_embedding_fwd(const at::Tensor& table, const at::Tensor& ids) {
 // grad (fp32 or bf16 [V, D], may be a view of the flat gradient partition) += scatter of dy rows.
 void dlgm_embedding_bwd_(at::Tensor grad, const at::Tensor& dy, const at::Tensor& sorted_ids, const at::Tensor& order) {
   TORCH_CHECK(grad.is_cuda() && grad.is_contiguous() && grad.dim() == 2, "embedding_bwd: grad must be contiguous [V, D]");
-  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.is_contiguous() && dy.numel() == sorted_ids.numel() * grad.size(1),
-              "embedding_bwd: dy must be contiguous bf16 [T, D]");
+  TORCH_CHECK(DLGM_IS16(dy) && dy.is_contiguous() && dy.numel() == sorted_ids.numel() * grad.size(1),
+              "embedding_bwd: dy must be contiguous bf16/fp16 [T, D]");
   TORCH_CHECK(sorted_ids.scalar_type() == at::kLong && order.scalar_type() == at::kLong && sorted_ids.is_contiguous() &&
                   order.is_contiguous() && order.numel() == sorted_ids.numel(),
               "embedding_bwd: sorted ids / order must be int64 [T]");
@@ -142,15 +143,17 @@ void dlgm_embedding_bwd_(at::Tensor grad, const at::Tensor& dy, const at::Tensor
   TORCH_CHECK(D % 8 == 0, "embedding_bwd: D must be a multiple of 8");
   if (T == 0) return;
   auto stream = c10::hip::getCurrentHIPStream();
-  auto dyp = reinterpret_cast<const bf16*>(dy.data_ptr());
-  if (grad.scalar_type() == at::kFloat)
-    embedding_bwd_kernel<true><<<(T + 3) / 4, 256, 0, stream>>>(sorted_ids.data_ptr<int64_t>(), order.data_ptr<int64_t>(),
-                                                                dyp, grad.data_ptr(), T, D, V);
-  else {
-    TORCH_CHECK(grad.scalar_type() == at::kBFloat16, "embedding_bwd: grad must be fp32 or bf16");
-    embedding_bwd_kernel<false><<<(T + 3) / 4, 256, 0, stream>>>(sorted_ids.data_ptr<int64_t>(),
-                                                                 order.data_ptr<int64_t>(), dyp, grad.data_ptr(), T, D, V);
-  }
+  DLGM_DISPATCH_16(dy.scalar_type(), E, {
+    auto dyp = reinterpret_cast<const E*>(dy.data_ptr());
+    if (grad.scalar_type() == at::kFloat) {
+      embedding_bwd_kernel<E, true><<<(T + 3) / 4, 256, 0, stream>>>(
+          sorted_ids.data_ptr<int64_t>(), order.data_ptr<int64_t>(), dyp, grad.data_ptr(), T, D, V);
+    } else {
+      TORCH_CHECK(grad.scalar_type() == dy.scalar_type(), "embedding_bwd: grad must be fp32 or dy's dtype");
+      embedding_bwd_kernel<E, false><<<(T + 3) / 4, 256, 0, stream>>>(
+          sorted_ids.data_ptr<int64_t>(), order.data_ptr<int64_t>(), dyp, grad.data_ptr(), T, D, V);
+    }
+  });
   DLGM_CHECK_HIP(hipGetLastError());
 }
 

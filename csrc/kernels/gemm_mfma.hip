@@ -161,26 +161,24 @@ __device__ __forceinline__ int xcd_remap(int id, int total) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + id / 8;
 }
 
-template <bool AK, bool BKM, int EPI>
+template <int MODE, bool AK, bool BKM, int EPI>
 __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[4 * TILE_BYTES];  // [buf][A | B]
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = w >> 2, wc = w & 3;
 
-  // ---- which tile (and group) this block computes
-  int id = xcd_remap(blockIdx.x, gridDim.x);
-  int tm, tn, grp = 0;
+  // ---- which tile (and group) this block computes. The mode is a template parameter: each
+  // instantiation has straight-line pointer setup (no mode-dependent phis for the operand bases).
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  int tm = 0, tn, grp = 0;
   int m_lo = 0, m_hi = p.M;  // valid rows of A / C for this block
   int k_lo = 0, k_hi = p.K;  // reduction range
-  const bf16* A = p.a;
-  const bf16* B = p.b;
-  char* C = (char*)p.c;
   constexpr int CES = EPI == kStoreBf16 ? 2 : 4;
-  if (p.mode == kDense) {
+  if constexpr (MODE == kDense) {
     tm = id / p.tiles_n;
     tn = id - tm * p.tiles_n;
-  } else if (p.mode == kGroupM) {
+  } else if constexpr (MODE == kGroupM) {
     tn = id % p.tiles_n;
     int j = id / p.tiles_n;
     grp = -1;
@@ -189,16 +187,13 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
       const int te = (hi - lo + BM - 1) / BM;
       if (j < te) {
         grp = e;
-        m_lo = lo;
+        m_lo = lo + j * BM;  // this block's first row (absolute)
         m_hi = hi;
         break;
       }
       j -= te;
     }
     if (grp < 0) return;  // spare block: the grid is sized for the worst case
-    tm = 0;
-    m_lo += j * BM;  // this block's first row (absolute)
-    B += grp * p.b_gstride;
   } else {  // grouped-K
     const int per = p.tiles_m * p.tiles_n;
     grp = id / per;
@@ -207,9 +202,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
     tn = rem - tm * p.tiles_n;
     k_lo = p.offsets[grp];
     k_hi = p.offsets[grp + 1];
-    C += (int64_t)grp * p.c_gstride * CES;
   }
-  const int m0 = p.mode == kGroupM ? m_lo : tm * BM;
+  const bf16* A = p.a;
+  const bf16* B = p.b + (MODE == kGroupM ? (int64_t)grp * p.b_gstride : 0);
+  char* C = (char*)p.c + (MODE == kGroupK ? (int64_t)grp * p.c_gstride * CES : 0);
+  const int m0 = MODE == kGroupM ? m_lo : tm * BM;
   const int n0 = tn * BN;
   const int rows_valid = min(BM, m_hi - m0);
   if (rows_valid <= 0) return;
@@ -300,14 +297,14 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
   }
 }
 
-template <bool AK, bool BKM>
+template <int MODE, bool AK, bool BKM>
 void launch_epi(int epi, dim3 grid, hipStream_t st, const GemmArgs& a) {
   if (epi == kStoreBf16)
-    gemm_mfma_kernel<AK, BKM, kStoreBf16><<<grid, NTHR, 0, st>>>(a);
+    gemm_mfma_kernel<MODE, AK, BKM, kStoreBf16><<<grid, NTHR, 0, st>>>(a);
   else if (epi == kStoreF32)
-    gemm_mfma_kernel<AK, BKM, kStoreF32><<<grid, NTHR, 0, st>>>(a);
+    gemm_mfma_kernel<MODE, AK, BKM, kStoreF32><<<grid, NTHR, 0, st>>>(a);
   else
-    gemm_mfma_kernel<AK, BKM, kAccF32><<<grid, NTHR, 0, st>>>(a);
+    gemm_mfma_kernel<MODE, AK, BKM, kAccF32><<<grid, NTHR, 0, st>>>(a);
 }
 
 }  // namespace
@@ -339,6 +336,8 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
   TORCH_CHECK(mode == kGroupK || K % BK == 0, "gemm_mfma: K must be a multiple of 64");
   // a group's reduction range ends anywhere: only the MN-contiguous images mask partial k tiles
   TORCH_CHECK(mode != kGroupK || (!ak && !bk), "gemm_mfma: grouped-K needs token-major (row = k) operands");
+  TORCH_CHECK(mode != kGroupM || ak, "gemm_mfma: grouped-M needs row-major (K-contiguous) rows");
+  TORCH_CHECK(mode == kDense || mode == kGroupM || mode == kGroupK, "gemm_mfma: bad mode");
   for (const at::Tensor* t : {&a, &b2}) {
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_mfma: operands 16-byte aligned");
   }
@@ -375,13 +374,22 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
   const int epi = !out32 ? kStoreBf16 : accumulate ? kAccF32 : kStoreF32;
   auto st = c10::hip::getCurrentHIPStream();
   dim3 grid((unsigned)nblk);
-  if (ak && bk)
-    launch_epi<true, true>(epi, grid, st, p);
-  else if (ak)
-    launch_epi<true, false>(epi, grid, st, p);
-  else if (bk)
-    launch_epi<false, true>(epi, grid, st, p);
-  else
-    launch_epi<false, false>(epi, grid, st, p);
+  if (mode == kDense) {
+    if (ak && bk)
+      launch_epi<kDense, true, true>(epi, grid, st, p);
+    else if (ak)
+      launch_epi<kDense, true, false>(epi, grid, st, p);
+    else if (bk)
+      launch_epi<kDense, false, true>(epi, grid, st, p);
+    else
+      launch_epi<kDense, false, false>(epi, grid, st, p);
+  } else if (mode == kGroupM) {  // token rows x expert weights ([G, N, K] or [G, K, N])
+    if (bk)
+      launch_epi<kGroupM, true, true>(epi, grid, st, p);
+    else
+      launch_epi<kGroupM, true, false>(epi, grid, st, p);
+  } else {  // token-major operands (checked above)
+    launch_epi<kGroupK, false, false>(epi, grid, st, p);
+  }
   DLGM_CHECK_HIP(hipGetLastError());
 }

@@ -25,9 +25,9 @@ using namespace dlgm;
 
 namespace {
 
-template <int K>
-__global__ __launch_bounds__(256) void moe_combine_fwd_kernel(const bf16* __restrict__ y, const int64_t* __restrict__ pos,
-                                                              const float* __restrict__ gates, bf16* __restrict__ out,
+template <typename E, int K>
+__global__ __launch_bounds__(256) void moe_combine_fwd_kernel(const E* __restrict__ y, const int64_t* __restrict__ pos,
+                                                              const float* __restrict__ gates, E* __restrict__ out,
                                                               int64_t T, int64_t D) {
   const int lane = threadIdx.x & 63;
   const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -47,10 +47,10 @@ __global__ __launch_bounds__(256) void moe_combine_fwd_kernel(const bf16* __rest
   }
 }
 
-template <int K>
-__global__ __launch_bounds__(256) void moe_combine_bwd_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ y,
+template <typename E, int K>
+__global__ __launch_bounds__(256) void moe_combine_bwd_kernel(const E* __restrict__ dout, const E* __restrict__ y,
                                                               const int64_t* __restrict__ pos,
-                                                              const float* __restrict__ gates, bf16* __restrict__ dy,
+                                                              const float* __restrict__ gates, E* __restrict__ dy,
                                                               float* __restrict__ dgates, int64_t T, int64_t D) {
   const int lane = threadIdx.x & 63;
   const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -126,8 +126,8 @@ __global__ __launch_bounds__(kPermThreads) void moe_permute_kernel(const int64_t
 }
 
 void check(const at::Tensor& y, const at::Tensor& pos, int64_t D) {
-  TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kBFloat16 && y.is_contiguous() && y.dim() == 2,
-              "moe: rows must be a contiguous [N, D] bf16 GPU tensor");
+  TORCH_CHECK(y.is_cuda() && DLGM_IS16(y) && y.is_contiguous() && y.dim() == 2,
+              "moe: rows must be a contiguous [N, D] bf16/fp16 GPU tensor");
   TORCH_CHECK(D % 8 == 0, "moe: D must be a multiple of 8");
   TORCH_CHECK(pos.scalar_type() == at::kLong && pos.is_contiguous() && pos.dim() == 2, "moe: pos must be int64 [T, K]");
 }
@@ -146,15 +146,17 @@ at::Tensor dlgm_moe_combine_fwd(const at::Tensor& y, const at::Tensor& pos, cons
   if (T == 0) return out;
   auto stream = c10::hip::getCurrentHIPStream();
   const dim3 grid((T + 3) / 4);
-  auto yp = reinterpret_cast<const bf16*>(y.data_ptr());
   auto gp = has_g ? gates->data_ptr<float>() : nullptr;
-  auto op = reinterpret_cast<bf16*>(out.data_ptr());
-  switch (K) {
-    case 1: moe_combine_fwd_kernel<1><<<grid, 256, 0, stream>>>(yp, pos.data_ptr<int64_t>(), gp, op, T, D); break;
-    case 2: moe_combine_fwd_kernel<2><<<grid, 256, 0, stream>>>(yp, pos.data_ptr<int64_t>(), gp, op, T, D); break;
-    case 4: moe_combine_fwd_kernel<4><<<grid, 256, 0, stream>>>(yp, pos.data_ptr<int64_t>(), gp, op, T, D); break;
-    default: TORCH_CHECK(false, "moe: top-k must be 1, 2 or 4");
-  }
+  DLGM_DISPATCH_16(y.scalar_type(), E, {
+    auto yp = reinterpret_cast<const E*>(y.data_ptr());
+    auto op = reinterpret_cast<E*>(out.data_ptr());
+    switch (K) {
+      case 1: moe_combine_fwd_kernel<E, 1><<<grid, 256, 0, stream>>>(yp, pos.data_ptr<int64_t>(), gp, op, T, D); break;
+      case 2: moe_combine_fwd_kernel<E, 2><<<grid, 256, 0, stream>>>(yp, pos.data_ptr<int64_t>(), gp, op, T, D); break;
+      case 4: moe_combine_fwd_kernel<E, 4><<<grid, 256, 0, stream>>>(yp, pos.data_ptr<int64_t>(), gp, op, T, D); break;
+      default: TORCH_CHECK(false, "moe: top-k must be 1, 2 or 4");
+    }
+  });
   DLGM_CHECK_HIP(hipGetLastError());
   return out;
 }
@@ -170,6 +172,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_moe_permute(const at::Tensor
   auto src = at::empty({n}, topi.options());
   const size_t lds = (size_t)(n_experts * kPermThreads + kPermThreads / 64) * sizeof(int);
   auto stream = c10::hip::getCurrentHIPStream();
+  if (lds > 64 * 1024)  // > 64 KiB of dynamic LDS (up to 160 KiB on gfx950) has to be opted into
+    DLGM_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(moe_permute_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   moe_permute_kernel<<<1, kPermThreads, lds, stream>>>(topi.data_ptr<int64_t>(), n, (int)K, (int)n_experts,
                                                       offsets.data_ptr<int>(), pos.data_ptr<int64_t>(),
                                                       src.data_ptr<int64_t>());
@@ -182,22 +187,27 @@ std::tuple<at::Tensor, at::Tensor> dlgm_moe_combine_bwd(const at::Tensor& dout, 
   const int64_t D = y.size(1);
   check(y, pos, D);
   const int64_t T = pos.size(0), K = pos.size(1);
-  TORCH_CHECK(dout.is_contiguous() && dout.scalar_type() == at::kBFloat16 && dout.numel() == T * D, "moe: bad dout");
+  TORCH_CHECK(dout.is_contiguous() && dout.scalar_type() == y.scalar_type() && dout.numel() == T * D, "moe: bad dout");
   TORCH_CHECK(gates.scalar_type() == at::kFloat && gates.is_contiguous() && gates.numel() == T * K, "moe: bad gates");
   auto dy = at::zeros_like(y);  // slots not referenced by any token (none in practice) stay zero
   auto dg = at::empty({T, K}, gates.options());
   if (T == 0) return {dy, dg};
   auto stream = c10::hip::getCurrentHIPStream();
   const dim3 grid((T + 3) / 4);
-  auto dp = reinterpret_cast<const bf16*>(dout.data_ptr());
-  auto yp = reinterpret_cast<const bf16*>(y.data_ptr());
-  auto dyp = reinterpret_cast<bf16*>(dy.data_ptr());
-  switch (K) {
-    case 1: moe_combine_bwd_kernel<1><<<grid, 256, 0, stream>>>(dp, yp, pos.data_ptr<int64_t>(), gates.data_ptr<float>(), dyp, dg.data_ptr<float>(), T, D); break;
-    case 2: moe_combine_bwd_kernel<2><<<grid, 256, 0, stream>>>(dp, yp, pos.data_ptr<int64_t>(), gates.data_ptr<float>(), dyp, dg.data_ptr<float>(), T, D); break;
-    case 4: moe_combine_bwd_kernel<4><<<grid, 256, 0, stream>>>(dp, yp, pos.data_ptr<int64_t>(), gates.data_ptr<float>(), dyp, dg.data_ptr<float>(), T, D); break;
-    default: TORCH_CHECK(false, "moe: top-k must be 1, 2 or 4");
-  }
+  DLGM_DISPATCH_16(y.scalar_type(), E, {
+    auto dp = reinterpret_cast<const E*>(dout.data_ptr());
+    auto yp = reinterpret_cast<const E*>(y.data_ptr());
+    auto dyp = reinterpret_cast<E*>(dy.data_ptr());
+    auto pp = pos.data_ptr<int64_t>();
+    auto gp = gates.data_ptr<float>();
+    auto dgp = dg.data_ptr<float>();
+    switch (K) {
+      case 1: moe_combine_bwd_kernel<E, 1><<<grid, 256, 0, stream>>>(dp, yp, pp, gp, dyp, dgp, T, D); break;
+      case 2: moe_combine_bwd_kernel<E, 2><<<grid, 256, 0, stream>>>(dp, yp, pp, gp, dyp, dgp, T, D); break;
+      case 4: moe_combine_bwd_kernel<E, 4><<<grid, 256, 0, stream>>>(dp, yp, pp, gp, dyp, dgp, T, D); break;
+      default: TORCH_CHECK(false, "moe: top-k must be 1, 2 or 4");
+    }
+  });
   DLGM_CHECK_HIP(hipGetLastError());
   return {dy, dg};
 }

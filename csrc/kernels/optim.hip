@@ -42,6 +42,11 @@ __device__ __forceinline__ void load4<bf16>(const bf16* p, float (&o)[4]) {
   bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
   o[0] = (float)v[0]; o[1] = (float)v[1]; o[2] = (float)v[2]; o[3] = (float)v[3];
 }
+template <>
+__device__ __forceinline__ void load4<f16>(const f16* p, float (&o)[4]) {
+  f16x4 v = *reinterpret_cast<const f16x4*>(p);
+  o[0] = (float)v[0]; o[1] = (float)v[1]; o[2] = (float)v[2]; o[3] = (float)v[3];
+}
 
 template <typename T>
 __global__ __launch_bounds__(kThreads) void grad_stats_partial_kernel(const T* __restrict__ g, int64_t n,
@@ -126,10 +131,10 @@ __device__ __forceinline__ float clip_coef(const float* stats, const AdamHyper& 
   return coef;
 }
 
-template <typename GT>
+template <typename GT, typename PT>
 __global__ __launch_bounds__(kThreads) void adamw_kernel(float* __restrict__ p, float* __restrict__ m,
                                                          float* __restrict__ v, const GT* __restrict__ g,
-                                                         bf16* __restrict__ p16, const float* __restrict__ stats,
+                                                         PT* __restrict__ p16, const float* __restrict__ stats,
                                                          int64_t n, AdamHyper h) {
   bool skip;
   const float gc = clip_coef(stats, h, skip);
@@ -155,7 +160,7 @@ __global__ __launch_bounds__(kThreads) void adamw_kernel(float* __restrict__ p, 
     *reinterpret_cast<f32x4*>(p + i * 4) = pp;
     *reinterpret_cast<f32x4*>(m + i * 4) = mm;
     *reinterpret_cast<f32x4*>(v + i * 4) = vv;
-    if (p16) *reinterpret_cast<bf16x4*>(p16 + i * 4) = __builtin_convertvector(pp, bf16x4);
+    if (p16) *reinterpret_cast<vec4_t<PT>*>(p16 + i * 4) = __builtin_convertvector(pp, vec4_t<PT>);
   }
   if (blockIdx.x == 0)
     for (int64_t i = nv * 4 + threadIdx.x; i < n; i += kThreads) {
@@ -163,7 +168,7 @@ __global__ __launch_bounds__(kThreads) void adamw_kernel(float* __restrict__ p, 
       m[i] = h.b1 * m[i] + (1.f - h.b1) * gj;
       v[i] = h.b2 * v[i] + (1.f - h.b2) * gj * gj;
       p[i] = p[i] * decay - step_size * m[i] / (sqrtf(v[i]) * inv_sqrt_bc2 + h.eps);
-      if (p16) p16[i] = (bf16)p[i];
+      if (p16) p16[i] = (PT)p[i];
     }
 }
 
@@ -183,13 +188,15 @@ __global__ __launch_bounds__(kThreads) void accumulate_kernel(float* __restrict_
       dst[i] = (beta == 0.f ? 0.f : dst[i] * beta) + alpha * (float)src[i];
 }
 
-__global__ __launch_bounds__(kThreads) void cast_kernel(const float* __restrict__ src, bf16* __restrict__ dst,
+template <typename PT>
+__global__ __launch_bounds__(kThreads) void cast_kernel(const float* __restrict__ src, PT* __restrict__ dst,
                                                         int64_t n) {
   const int64_t nv = n >> 2;
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kThreads)
-    *reinterpret_cast<bf16x4*>(dst + i * 4) = __builtin_convertvector(*reinterpret_cast<const f32x4*>(src + i * 4), bf16x4);
+    *reinterpret_cast<vec4_t<PT>*>(dst + i * 4) =
+        __builtin_convertvector(*reinterpret_cast<const f32x4*>(src + i * 4), vec4_t<PT>);
   if (blockIdx.x == 0)
-    for (int64_t i = nv * 4 + threadIdx.x; i < n; i += kThreads) dst[i] = (bf16)src[i];
+    for (int64_t i = nv * 4 + threadIdx.x; i < n; i += kThreads) dst[i] = (PT)src[i];
 }
 
 void check_flat(const at::Tensor& t, const char* name) {
@@ -222,11 +229,9 @@ void dlgm_grad_stats(at::TensorList grads, at::Tensor out, bool accumulate) {
     const auto& g = grads[i];
     if (g.scalar_type() == at::kFloat)
       grad_stats_partial_kernel<float><<<grids[i], kThreads, 0, stream>>>(g.data_ptr<float>(), g.numel(), pp + off);
-    else {
-      TORCH_CHECK(g.scalar_type() == at::kBFloat16, "grad_stats: grads must be fp32 or bf16");
-      grad_stats_partial_kernel<bf16><<<grids[i], kThreads, 0, stream>>>(
-          reinterpret_cast<const bf16*>(g.data_ptr()), g.numel(), pp + off);
-    }
+    else
+      DLGM_DISPATCH_16(g.scalar_type(), E, grad_stats_partial_kernel<E><<<grids[i], kThreads, 0, stream>>>(
+                                               reinterpret_cast<const E*>(g.data_ptr()), g.numel(), pp + off));
     off += grids[i];
   }
   grad_stats_final_kernel<<<1, kThreads, 0, stream>>>(pp, (int)total, out.data_ptr<float>(), accumulate);
@@ -245,11 +250,10 @@ void dlgm_adamw_step_(at::Tensor p, at::Tensor m, at::Tensor v, const at::Tensor
   TORCH_CHECK(p.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat,
               "adamw: master/state must be fp32");
   TORCH_CHECK(m.numel() == n && v.numel() == n && g.numel() == n, "adamw: size mismatch");
-  bf16* p16p = nullptr;
-  if (p16.has_value() && p16->defined()) {
-    check_flat(*p16, "param_bf16");
-    TORCH_CHECK(p16->scalar_type() == at::kBFloat16 && p16->numel() == n, "adamw: bad bf16 copy");
-    p16p = reinterpret_cast<bf16*>(p16->data_ptr());
+  const bool has16 = p16.has_value() && p16->defined();
+  if (has16) {
+    check_flat(*p16, "param_16");
+    TORCH_CHECK(DLGM_IS16(*p16) && p16->numel() == n, "adamw: bad bf16/fp16 compute copy");
   }
   const float* sp = nullptr;
   if (stats.has_value() && stats->defined()) {
@@ -261,14 +265,17 @@ void dlgm_adamw_step_(at::Tensor p, at::Tensor m, at::Tensor v, const at::Tensor
               (float)grad_scale, (float)max_norm};
   auto stream = c10::hip::getCurrentHIPStream();
   const int64_t grid = stream_grid(n / 4);
-  if (g.scalar_type() == at::kFloat)
-    adamw_kernel<float><<<grid, kThreads, 0, stream>>>(p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
-                                                       g.data_ptr<float>(), p16p, sp, n, h);
-  else {
-    TORCH_CHECK(g.scalar_type() == at::kBFloat16, "adamw: grad must be fp32 or bf16");
-    adamw_kernel<bf16><<<grid, kThreads, 0, stream>>>(p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
-                                                      reinterpret_cast<const bf16*>(g.data_ptr()), p16p, sp, n, h);
-  }
+  // the compute copy's dtype selects the instantiation (bf16 unless the engine runs the fp16 path)
+  DLGM_DISPATCH_16(has16 ? p16->scalar_type() : at::kBFloat16, PT, {
+    PT* p16p = has16 ? reinterpret_cast<PT*>(p16->data_ptr()) : nullptr;
+    if (g.scalar_type() == at::kFloat)
+      adamw_kernel<float, PT><<<grid, kThreads, 0, stream>>>(p.data_ptr<float>(), m.data_ptr<float>(),
+                                                             v.data_ptr<float>(), g.data_ptr<float>(), p16p, sp, n, h);
+    else
+      DLGM_DISPATCH_16(g.scalar_type(), GT, adamw_kernel<GT, PT><<<grid, kThreads, 0, stream>>>(
+                                                p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                                                reinterpret_cast<const GT*>(g.data_ptr()), p16p, sp, n, h));
+  });
   DLGM_CHECK_HIP(hipGetLastError());
 }
 
@@ -284,24 +291,22 @@ void dlgm_accumulate_(at::Tensor dst, const at::Tensor& src, double alpha, doubl
   if (src.scalar_type() == at::kFloat)
     accumulate_kernel<float><<<grid, kThreads, 0, stream>>>(dst.data_ptr<float>(), src.data_ptr<float>(), n,
                                                             (float)alpha, (float)beta);
-  else {
-    TORCH_CHECK(src.scalar_type() == at::kBFloat16, "accumulate: src must be fp32 or bf16");
-    accumulate_kernel<bf16><<<grid, kThreads, 0, stream>>>(dst.data_ptr<float>(),
-                                                           reinterpret_cast<const bf16*>(src.data_ptr()), n,
-                                                           (float)alpha, (float)beta);
-  }
+  else
+    DLGM_DISPATCH_16(src.scalar_type(), E, accumulate_kernel<E><<<grid, kThreads, 0, stream>>>(
+                                             dst.data_ptr<float>(), reinterpret_cast<const E*>(src.data_ptr()), n,
+                                             (float)alpha, (float)beta));
   DLGM_CHECK_HIP(hipGetLastError());
 }
 
 void dlgm_cast_f32_bf16_(at::Tensor dst, const at::Tensor& src) {
   check_flat(dst, "dst");
   check_flat(src, "src");
-  TORCH_CHECK(src.scalar_type() == at::kFloat && dst.scalar_type() == at::kBFloat16 && src.numel() == dst.numel(),
-              "cast: expects fp32 -> bf16 of equal size");
+  TORCH_CHECK(src.scalar_type() == at::kFloat && DLGM_IS16(dst) && src.numel() == dst.numel(),
+              "cast: expects fp32 -> bf16/fp16 of equal size");
   const int64_t n = src.numel();
   if (n == 0) return;
   auto stream = c10::hip::getCurrentHIPStream();
-  cast_kernel<<<stream_grid(n / 4), kThreads, 0, stream>>>(src.data_ptr<float>(),
-                                                           reinterpret_cast<bf16*>(dst.data_ptr()), n);
+  DLGM_DISPATCH_16(dst.scalar_type(), PT, cast_kernel<PT><<<stream_grid(n / 4), kThreads, 0, stream>>>(
+                                             src.data_ptr<float>(), reinterpret_cast<PT*>(dst.data_ptr()), n));
   DLGM_CHECK_HIP(hipGetLastError());
 }

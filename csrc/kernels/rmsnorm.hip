@@ -22,10 +22,10 @@ namespace {
 constexpr int kThreads = 256;  // 4 waves -> 4 rows in flight per block
 constexpr int kWaves = kThreads / 64;
 
-template <int MAXC, bool RESID>
+template <typename E, int MAXC, bool RESID>
 __global__ __launch_bounds__(kThreads) void rmsnorm_fwd_kernel(
-    const bf16* __restrict__ x, const bf16* __restrict__ r, const bf16* __restrict__ w,
-    bf16* __restrict__ y, bf16* __restrict__ h, float* __restrict__ rstd_out, int T, int D,
+    const E* __restrict__ x, const E* __restrict__ r, const E* __restrict__ w,
+    E* __restrict__ y, E* __restrict__ h, float* __restrict__ rstd_out, int T, int D,
     float eps) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * kWaves + (threadIdx.x >> 6);
@@ -44,7 +44,7 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_fwd_kernel(
         store8f(h + base + ch * 8, v[c]);
         // the normalised value must be computed from the rounded residual
         // stream so forward and backward see the same h.
-        v[c] = __builtin_convertvector(__builtin_convertvector(v[c], bf16x8), f32x8);
+        v[c] = __builtin_convertvector(__builtin_convertvector(v[c], vec8_t<E>), f32x8);
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) ss += v[c][j] * v[c][j];
@@ -69,10 +69,10 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_fwd_kernel(
 // the row is held as raw bf16 (4 VGPRs per 8 elements, widened on use), w is re-read from L1
 // instead of pinned in 64 VGPRs, and the residual-gradient row is loaded together with dy and h,
 // so a row costs ONE dependent HBM latency and 3 waves fit per SIMD (was 1-2, ~2.2 TB/s).
-template <int MAXC, bool DRES>
+template <typename E, int MAXC, bool DRES>
 __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(
-    const bf16* __restrict__ dy, const bf16* __restrict__ hin, const bf16* __restrict__ w,
-    const float* __restrict__ rstd, const bf16* __restrict__ dres, bf16* __restrict__ dx,
+    const E* __restrict__ dy, const E* __restrict__ hin, const E* __restrict__ w,
+    const float* __restrict__ rstd, const E* __restrict__ dres, E* __restrict__ dx,
     float* __restrict__ dw_part, int T, int D) {
   __shared__ __attribute__((aligned(16))) f32x8 red[kWaves][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -84,14 +84,14 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(
   for (int row = blockIdx.x * kWaves + wid; row < T; row += nw) {
     const size_t base = (size_t)row * D;
     const float rs = rstd[row];
-    bf16x8 gr[MAXC], hr[MAXC], rr[DRES ? MAXC : 1];
+    vec8_t<E> gr[MAXC], hr[MAXC], rr[DRES ? MAXC : 1];
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
       const int ch = lane + c * 64;
       if (ch < nch) {
-        gr[c] = *reinterpret_cast<const bf16x8*>(dy + base + ch * 8);
-        hr[c] = *reinterpret_cast<const bf16x8*>(hin + base + ch * 8);
-        if constexpr (DRES) rr[c] = *reinterpret_cast<const bf16x8*>(dres + base + ch * 8);
+        gr[c] = *reinterpret_cast<const vec8_t<E>*>(dy + base + ch * 8);
+        hr[c] = *reinterpret_cast<const vec8_t<E>*>(hin + base + ch * 8);
+        if constexpr (DRES) rr[c] = *reinterpret_cast<const vec8_t<E>*>(dres + base + ch * 8);
       }
     }
     float dot = 0.f;
@@ -147,10 +147,10 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(
 // no LDS reduction, and the per-thread state is tiny (~80 VGPRs -> 5-6 waves per SIMD): the row is
 // loaded once (dy, h, dres together), reduced across the block through a 2-slot LDS array (one
 // barrier per row; slot parity keeps a fast wave from overwriting a value a slow wave still reads).
-template <int CPL, bool DRES>
+template <typename E, int CPL, bool DRES>
 __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_rowblock_kernel(
-    const bf16* __restrict__ dy, const bf16* __restrict__ hin, const bf16* __restrict__ w,
-    const float* __restrict__ rstd, const bf16* __restrict__ dres, bf16* __restrict__ dx,
+    const E* __restrict__ dy, const E* __restrict__ hin, const E* __restrict__ w,
+    const float* __restrict__ rstd, const E* __restrict__ dres, E* __restrict__ dx,
     float* __restrict__ dw_part, int T, int D) {
   __shared__ float red[2][kWaves];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -165,13 +165,13 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_rowblock_kernel(
   for (int row = blockIdx.x; row < T; row += gridDim.x, ++it) {
     const size_t base = (size_t)row * D;
     const float rs = rstd[row];
-    bf16x8 gr[CPL], hr[CPL], rr[DRES ? CPL : 1];
+    vec8_t<E> gr[CPL], hr[CPL], rr[DRES ? CPL : 1];
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
       const size_t off = base + (size_t)(tid + c * kThreads) * 8;
-      gr[c] = *reinterpret_cast<const bf16x8*>(dy + off);
-      hr[c] = *reinterpret_cast<const bf16x8*>(hin + off);
-      if constexpr (DRES) rr[c] = *reinterpret_cast<const bf16x8*>(dres + off);
+      gr[c] = *reinterpret_cast<const vec8_t<E>*>(dy + off);
+      hr[c] = *reinterpret_cast<const vec8_t<E>*>(hin + off);
+      if constexpr (DRES) rr[c] = *reinterpret_cast<const vec8_t<E>*>(dres + off);
     }
     float dot = 0.f;
 #pragma unroll
@@ -255,7 +255,7 @@ int max_chunks_for(int64_t D) {
 
 void check_rows(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
-  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bf16");
+  TORCH_CHECK(DLGM_IS16(t), name, " must be bf16 or fp16");
   TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
 }
 
@@ -284,26 +284,30 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_rmsnorm_fwd(const at::Tensor
   if (T == 0) return {y, resid ? h : x, rstd};
   auto stream = c10::hip::getCurrentHIPStream();
   const dim3 grid((T + kWaves - 1) / kWaves);
-  auto xp = reinterpret_cast<const bf16*>(x.data_ptr());
-  auto rp = resid ? reinterpret_cast<const bf16*>(residual->data_ptr()) : nullptr;
-  auto wp = reinterpret_cast<const bf16*>(w.data_ptr());
-  auto yp = reinterpret_cast<bf16*>(y.data_ptr());
-  auto hp = resid ? reinterpret_cast<bf16*>(h.data_ptr()) : nullptr;
+  TORCH_CHECK(w.scalar_type() == x.scalar_type() && (!resid || residual->scalar_type() == x.scalar_type()),
+              "rmsnorm: x, residual and w must share one dtype");
 #define LAUNCH_FWD(C)                                                                        \
   if (resid)                                                                                 \
-    rmsnorm_fwd_kernel<C, true><<<grid, kThreads, 0, stream>>>(xp, rp, wp, yp, hp,           \
+    rmsnorm_fwd_kernel<E, C, true><<<grid, kThreads, 0, stream>>>(xp, rp, wp, yp, hp,        \
                                                                rstd.data_ptr<float>(), T, D, \
                                                                (float)eps);                  \
   else                                                                                       \
-    rmsnorm_fwd_kernel<C, false><<<grid, kThreads, 0, stream>>>(xp, rp, wp, yp, hp,          \
+    rmsnorm_fwd_kernel<E, C, false><<<grid, kThreads, 0, stream>>>(xp, rp, wp, yp, hp,       \
                                                                 rstd.data_ptr<float>(), T, D, \
                                                                 (float)eps);
+  DLGM_DISPATCH_16(x.scalar_type(), E, {
+  auto xp = reinterpret_cast<const E*>(x.data_ptr());
+  auto rp = resid ? reinterpret_cast<const E*>(residual->data_ptr()) : nullptr;
+  auto wp = reinterpret_cast<const E*>(w.data_ptr());
+  auto yp = reinterpret_cast<E*>(y.data_ptr());
+  auto hp = resid ? reinterpret_cast<E*>(h.data_ptr()) : nullptr;
   switch (MAXC) {
     case 2: LAUNCH_FWD(2); break;
     case 4: LAUNCH_FWD(4); break;
     case 8: LAUNCH_FWD(8); break;
     default: LAUNCH_FWD(16); break;
   }
+  });
 #undef LAUNCH_FWD
   DLGM_CHECK_HIP(hipGetLastError());
   return {y, resid ? h : x, rstd};
@@ -328,25 +332,35 @@ at::Tensor dlgm_rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at:
   if (has_dres) check_rows(*dres, "dres");
   auto dx = at::empty_like(dy);
   auto stream = c10::hip::getCurrentHIPStream();
-  auto dyp = reinterpret_cast<const bf16*>(dy.data_ptr());
-  auto hp = reinterpret_cast<const bf16*>(h.data_ptr());
-  auto wp = reinterpret_cast<const bf16*>(w.data_ptr());
-  auto drp = has_dres ? reinterpret_cast<const bf16*>(dres->data_ptr()) : nullptr;
-  auto dxp = reinterpret_cast<bf16*>(dx.data_ptr());
-  const int cpl = (D % (8 * kThreads) == 0) ? (int)(D / (8 * kThreads)) : 0;
-  int64_t nblk;
+  int64_t nblk = 0;
   at::Tensor part;
+  TORCH_CHECK(h.scalar_type() == dy.scalar_type() && w.scalar_type() == dy.scalar_type() &&
+                  (!has_dres || dres->scalar_type() == dy.scalar_type()), "rmsnorm_bwd: mixed dtypes");
+  const int cpl = (D % (8 * kThreads) == 0) ? (int)(D / (8 * kThreads)) : 0;
+#define LAUNCH_ROWBLOCK(C)                                                                                  \
+    if (has_dres)                                                                                           \
+      rmsnorm_bwd_rowblock_kernel<E, C, true><<<nblk, kThreads, 0, stream>>>(dyp, hp, wp, rstd.data_ptr<float>(), \
+                                                                        drp, dxp, part.data_ptr<float>(), T, D); \
+    else                                                                                                    \
+      rmsnorm_bwd_rowblock_kernel<E, C, false><<<nblk, kThreads, 0, stream>>>(dyp, hp, wp, rstd.data_ptr<float>(), \
+                                                                         drp, dxp, part.data_ptr<float>(), T, D);
+#define LAUNCH_BWD(C)                                                                                \
+    if (has_dres)                                                                                    \
+      rmsnorm_bwd_kernel<E, C, true><<<nblk, kThreads, 0, stream>>>(dyp, hp, wp, rstd.data_ptr<float>(),  \
+                                                                 drp, dxp, part.data_ptr<float>(), T, D); \
+    else                                                                                             \
+      rmsnorm_bwd_kernel<E, C, false><<<nblk, kThreads, 0, stream>>>(dyp, hp, wp, rstd.data_ptr<float>(), \
+                                                                  drp, dxp, part.data_ptr<float>(), T, D);
+  DLGM_DISPATCH_16(dy.scalar_type(), E, {
+  auto dyp = reinterpret_cast<const E*>(dy.data_ptr());
+  auto hp = reinterpret_cast<const E*>(h.data_ptr());
+  auto wp = reinterpret_cast<const E*>(w.data_ptr());
+  auto drp = has_dres ? reinterpret_cast<const E*>(dres->data_ptr()) : nullptr;
+  auto dxp = reinterpret_cast<E*>(dx.data_ptr());
   if (cpl == 1 || cpl == 2 || cpl == 4) {
     // block-per-row kernel: 1024 blocks (~5 resident per CU), 8 rows each at T = 8192
     nblk = std::max<int64_t>(1, std::min<int64_t>(T, 1024));
     part = at::empty({nblk, D}, dy.options().dtype(at::kFloat));
-#define LAUNCH_ROWBLOCK(C)                                                                                  \
-    if (has_dres)                                                                                           \
-      rmsnorm_bwd_rowblock_kernel<C, true><<<nblk, kThreads, 0, stream>>>(dyp, hp, wp, rstd.data_ptr<float>(), \
-                                                                        drp, dxp, part.data_ptr<float>(), T, D); \
-    else                                                                                                    \
-      rmsnorm_bwd_rowblock_kernel<C, false><<<nblk, kThreads, 0, stream>>>(dyp, hp, wp, rstd.data_ptr<float>(), \
-                                                                         drp, dxp, part.data_ptr<float>(), T, D);
     if (T > 0) {
       switch (cpl) {
         case 1: LAUNCH_ROWBLOCK(1); break;
@@ -356,26 +370,20 @@ at::Tensor dlgm_rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at:
     } else {
       part.zero_();
     }
-#undef LAUNCH_ROWBLOCK
   } else {
     // wave-per-row kernel for narrow rows: 3 waves / SIMD over 256 CUs = 768 blocks of 4 waves
     nblk = std::max<int64_t>(1, std::min<int64_t>((T + kWaves - 1) / kWaves, 768));
     part = at::empty({nblk, D}, dy.options().dtype(at::kFloat));
-#define LAUNCH_BWD(C)                                                                                \
-    if (has_dres)                                                                                    \
-      rmsnorm_bwd_kernel<C, true><<<nblk, kThreads, 0, stream>>>(dyp, hp, wp, rstd.data_ptr<float>(),  \
-                                                                 drp, dxp, part.data_ptr<float>(), T, D); \
-    else                                                                                             \
-      rmsnorm_bwd_kernel<C, false><<<nblk, kThreads, 0, stream>>>(dyp, hp, wp, rstd.data_ptr<float>(), \
-                                                                  drp, dxp, part.data_ptr<float>(), T, D);
     switch (MAXC) {
       case 2: LAUNCH_BWD(2); break;
       case 4: LAUNCH_BWD(4); break;
       case 8: LAUNCH_BWD(8); break;
       default: LAUNCH_BWD(16); break;
     }
-#undef LAUNCH_BWD
   }
+  });
+#undef LAUNCH_ROWBLOCK
+#undef LAUNCH_BWD
   DLGM_CHECK_HIP(hipGetLastError());
   // many partial rows: fold them 16 at a time in a wide first pass (fixed order: deterministic)
   constexpr int kSlice = 16;
@@ -396,9 +404,8 @@ at::Tensor dlgm_rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at:
                                                                 dw.data_ptr<float>(), rows, D,
                                                                 accumulate_dw);
   else {
-    TORCH_CHECK(dw.scalar_type() == at::kBFloat16, "rmsnorm_bwd: dw must be fp32 or bf16");
-    column_reduce_kernel<bf16><<<rgrid, kThreads, 0, stream>>>(
-        part.data_ptr<float>(), reinterpret_cast<bf16*>(dw.data_ptr()), rows, D, accumulate_dw);
+    DLGM_DISPATCH_16(dw.scalar_type(), E, column_reduce_kernel<E><<<rgrid, kThreads, 0, stream>>>(
+        part.data_ptr<float>(), reinterpret_cast<E*>(dw.data_ptr()), rows, D, accumulate_dw));
   }
   DLGM_CHECK_HIP(hipGetLastError());
   return dx;

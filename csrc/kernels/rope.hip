@@ -5,7 +5,7 @@
 // rotated, V is left alone, so no split / transpose copy is ever made -- the
 // attention kernel consumes the strided q/k/v views of the same buffer.
 //
-// Each lane rotates 8 (x_i, x_{i+hd/2}) pairs: two 16-byte bf16 loads of the
+// Each lane rotates 8 (x_i, x_{i+hd/2}) pairs: two 16-byte bf16/fp16 loads of the
 // row, two float4-pair loads of the cos/sin table (fp32, [max_pos, hd/2],
 // precomputed on the host -- no on-device trig, Appendix B "Element-wise").
 // Backward is the same kernel with the rotation inverted.
@@ -17,8 +17,8 @@ using namespace dlgm;
 
 namespace {
 
-template <bool INVERSE>
-__global__ __launch_bounds__(256) void rope_kernel(bf16* __restrict__ qkv, const float* __restrict__ cos_t,
+template <typename E, bool INVERSE>
+__global__ __launch_bounds__(256) void rope_kernel(E* __restrict__ qkv, const float* __restrict__ cos_t,
                                                    const float* __restrict__ sin_t,
                                                    const int64_t* __restrict__ pos_ids, int64_t T,
                                                    int64_t row_stride, int n_heads, int hd, int seq_len) {
@@ -32,7 +32,7 @@ __global__ __launch_bounds__(256) void rope_kernel(bf16* __restrict__ qkv, const
   const int64_t pos = pos_ids ? pos_ids[t] : (t % seq_len);
   const int half = hd >> 1;
   const int i0 = sub * 8;
-  bf16* p = qkv + t * row_stride + (int64_t)head * hd;
+  E* p = qkv + t * row_stride + (int64_t)head * hd;
   const float* cp = cos_t + pos * half + i0;
   const float* sp = sin_t + pos * half + i0;
   f32x8 a = load8f(p + i0);
@@ -51,7 +51,7 @@ __global__ __launch_bounds__(256) void rope_kernel(bf16* __restrict__ qkv, const
 void dlgm_rope_(at::Tensor qkv, const at::Tensor& cos_t, const at::Tensor& sin_t,
                 const c10::optional<at::Tensor>& pos_ids, int64_t n_rope_heads, int64_t head_dim,
                 int64_t seq_len, bool inverse) {
-  TORCH_CHECK(qkv.is_cuda() && qkv.scalar_type() == at::kBFloat16, "rope: qkv must be bf16 GPU");
+  TORCH_CHECK(qkv.is_cuda() && DLGM_IS16(qkv), "rope: qkv must be a bf16/fp16 GPU tensor");
   TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1, "rope: qkv must be [T, C] with unit inner stride");
   TORCH_CHECK(head_dim % 16 == 0, "rope: head_dim must be a multiple of 16");
   TORCH_CHECK(n_rope_heads * head_dim <= qkv.size(1), "rope: heads exceed row width");
@@ -71,13 +71,15 @@ void dlgm_rope_(at::Tensor qkv, const at::Tensor& cos_t, const at::Tensor& sin_t
   const int64_t threads = T * n_rope_heads * (head_dim / 16);
   const int64_t blocks = (threads + 255) / 256;
   auto stream = c10::hip::getCurrentHIPStream();
-  auto p = reinterpret_cast<bf16*>(qkv.data_ptr());
   const int64_t* pp = has_pos ? pos_ids->data_ptr<int64_t>() : nullptr;
-  if (inverse)
-    rope_kernel<true><<<blocks, 256, 0, stream>>>(p, cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), pp, T,
-                                                  qkv.stride(0), n_rope_heads, head_dim, seq_len);
-  else
-    rope_kernel<false><<<blocks, 256, 0, stream>>>(p, cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), pp, T,
-                                                   qkv.stride(0), n_rope_heads, head_dim, seq_len);
+  DLGM_DISPATCH_16(qkv.scalar_type(), E, {
+    auto p = reinterpret_cast<E*>(qkv.data_ptr());
+    if (inverse)
+      rope_kernel<E, true><<<blocks, 256, 0, stream>>>(p, cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), pp, T,
+                                                       qkv.stride(0), n_rope_heads, head_dim, seq_len);
+    else
+      rope_kernel<E, false><<<blocks, 256, 0, stream>>>(p, cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), pp, T,
+                                                        qkv.stride(0), n_rope_heads, head_dim, seq_len);
+  });
   DLGM_CHECK_HIP(hipGetLastError());
 }

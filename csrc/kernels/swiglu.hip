@@ -4,7 +4,7 @@
 // (gate = gu[:, :F], up = gu[:, F:]), so the activation reads one buffer.
 // Forward writes y [T, F]; backward reads dy and gu and writes dgu [T, 2F]
 // -- the gradient of the fused GEMM output -- in a single pass.
-// Pure HBM streaming: 16 B per lane per access, grid-strided, fp32 math.
+// Pure HBM streaming: 16 B per lane per access, grid-strided, fp32 math; bf16 or fp16 storage.
 #include <torch/all.h>
 #include <c10/hip/HIPStream.h>
 #include "dlgm_common.h"
@@ -13,14 +13,15 @@ using namespace dlgm;
 
 namespace {
 
-__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const bf16* __restrict__ gu, bf16* __restrict__ y,
-                                                         int64_t T, int64_t F, int64_t gu_stride) {
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const T* __restrict__ gu, T* __restrict__ y,
+                                                         int64_t T_, int64_t F, int64_t gu_stride) {
   const int64_t fch = F >> 3;
-  const int64_t total = T * fch;
+  const int64_t total = T_ * fch;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t t = i / fch, c = (i - t * fch) * 8;
-    const bf16* row = gu + t * gu_stride;
+    const T* row = gu + t * gu_stride;
     f32x8 g = load8f(row + c), u = load8f(row + F + c);
     f32x8 o;
 #pragma unroll
@@ -29,15 +30,16 @@ __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const bf16* __restrict_
   }
 }
 
-__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ gu,
-                                                         bf16* __restrict__ dgu, int64_t T, int64_t F,
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ gu,
+                                                         T* __restrict__ dgu, int64_t T_, int64_t F,
                                                          int64_t gu_stride) {
   const int64_t fch = F >> 3;
-  const int64_t total = T * fch;
+  const int64_t total = T_ * fch;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t t = i / fch, c = (i - t * fch) * 8;
-    const bf16* row = gu + t * gu_stride;
+    const T* row = gu + t * gu_stride;
     f32x8 g = load8f(row + c), u = load8f(row + F + c), d = load8f(dy + t * F + c);
     f32x8 dg, du;
 #pragma unroll
@@ -47,7 +49,7 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16* __restrict_
       du[j] = d[j] * sg;
       dg[j] = d[j] * u[j] * (s + sg * (1.f - s));
     }
-    bf16* out = dgu + t * 2 * F;
+    T* out = dgu + t * 2 * F;
     store8f(out + c, dg);
     store8f(out + F + c, du);
   }
@@ -61,32 +63,31 @@ int64_t grid_for(int64_t work) {
 }  // namespace
 
 at::Tensor dlgm_swiglu_fwd(const at::Tensor& gu) {
-  TORCH_CHECK(gu.is_cuda() && gu.scalar_type() == at::kBFloat16 && gu.dim() == 2 && gu.stride(1) == 1,
-              "swiglu: gu must be a [T, 2F] bf16 GPU tensor");
+  TORCH_CHECK(gu.is_cuda() && DLGM_IS16(gu) && gu.dim() == 2 && gu.stride(1) == 1,
+              "swiglu: gu must be a [T, 2F] bf16/fp16 GPU tensor");
   const int64_t T = gu.size(0), F = gu.size(1) / 2;
   TORCH_CHECK(gu.size(1) % 2 == 0 && F % 8 == 0 && gu.stride(0) % 8 == 0, "swiglu: F must be a multiple of 8");
   auto y = at::empty({T, F}, gu.options());
   if (T == 0) return y;
   auto stream = c10::hip::getCurrentHIPStream();
-  swiglu_fwd_kernel<<<grid_for(T * F / 8), 256, 0, stream>>>(reinterpret_cast<const bf16*>(gu.data_ptr()),
-                                                             reinterpret_cast<bf16*>(y.data_ptr()), T, F,
-                                                             gu.stride(0));
+  DLGM_DISPATCH_16(gu.scalar_type(), E, swiglu_fwd_kernel<E><<<grid_for(T * F / 8), 256, 0, stream>>>(
+      reinterpret_cast<const E*>(gu.data_ptr()), reinterpret_cast<E*>(y.data_ptr()), T, F, gu.stride(0)));
   DLGM_CHECK_HIP(hipGetLastError());
   return y;
 }
 
 at::Tensor dlgm_swiglu_bwd(const at::Tensor& dy, const at::Tensor& gu) {
-  TORCH_CHECK(gu.is_cuda() && gu.scalar_type() == at::kBFloat16 && gu.dim() == 2 && gu.stride(1) == 1,
-              "swiglu_bwd: gu must be a [T, 2F] bf16 GPU tensor");
+  TORCH_CHECK(gu.is_cuda() && DLGM_IS16(gu) && gu.dim() == 2 && gu.stride(1) == 1,
+              "swiglu_bwd: gu must be a [T, 2F] bf16/fp16 GPU tensor");
   const int64_t T = gu.size(0), F = gu.size(1) / 2;
-  TORCH_CHECK(dy.is_contiguous() && dy.scalar_type() == at::kBFloat16 && dy.numel() == T * F,
-              "swiglu_bwd: dy must be a contiguous [T, F] bf16 tensor");
+  TORCH_CHECK(dy.is_contiguous() && dy.scalar_type() == gu.scalar_type() && dy.numel() == T * F,
+              "swiglu_bwd: dy must be a contiguous [T, F] tensor of gu's dtype");
   auto dgu = at::empty({T, 2 * F}, gu.options());
   if (T == 0) return dgu;
   auto stream = c10::hip::getCurrentHIPStream();
-  swiglu_bwd_kernel<<<grid_for(T * F / 8), 256, 0, stream>>>(
-      reinterpret_cast<const bf16*>(dy.data_ptr()), reinterpret_cast<const bf16*>(gu.data_ptr()),
-      reinterpret_cast<bf16*>(dgu.data_ptr()), T, F, gu.stride(0));
+  DLGM_DISPATCH_16(gu.scalar_type(), E, swiglu_bwd_kernel<E><<<grid_for(T * F / 8), 256, 0, stream>>>(
+      reinterpret_cast<const E*>(dy.data_ptr()), reinterpret_cast<const E*>(gu.data_ptr()),
+      reinterpret_cast<E*>(dgu.data_ptr()), T, F, gu.stride(0)));
   DLGM_CHECK_HIP(hipGetLastError());
   return dgu;
 }

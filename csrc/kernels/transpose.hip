@@ -41,14 +41,15 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restr
 
 // out[C, R] (contiguous) = x[R, C]^T; x may be a row-strided view (stride(1) == 1).
 at::Tensor dlgm_transpose(const at::Tensor& x, const c10::optional<at::Tensor>& out_opt) {
-  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2, "transpose: bf16 2-D CUDA tensor");
+  // 16-bit payload moved bit-exactly: serves bf16 and fp16
+  TORCH_CHECK(x.is_cuda() && DLGM_IS16(x) && x.dim() == 2, "transpose: bf16/fp16 2-D GPU tensor");
   TORCH_CHECK(x.stride(1) == 1, "transpose: rows must be contiguous");
   const int64_t R = x.size(0), C = x.size(1);
   TORCH_CHECK(R % 8 == 0 && C % 8 == 0 && x.stride(0) % 8 == 0, "transpose: dims and row stride must be multiples of 8");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "transpose: input must be 16-byte aligned");
   at::Tensor y = out_opt.has_value() ? *out_opt : at::empty({C, R}, x.options());
-  TORCH_CHECK(y.sizes() == at::IntArrayRef({C, R}) && y.is_contiguous() && y.scalar_type() == at::kBFloat16,
-              "transpose: out must be a contiguous bf16 [C, R] tensor");
+  TORCH_CHECK(y.sizes() == at::IntArrayRef({C, R}) && y.is_contiguous() && y.scalar_type() == x.scalar_type(),
+              "transpose: out must be a contiguous [C, R] tensor of x's dtype");
   if (R == 0 || C == 0) return y;
   const int64_t tiles = ((R + 63) / 64) * ((C + 63) / 64);
   const int64_t grid = std::min<int64_t>((tiles + 3) / 4, 256 * 16);

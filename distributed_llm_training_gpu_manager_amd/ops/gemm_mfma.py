@@ -9,6 +9,7 @@ reading the routing counts on the host. CPU tensors take an fp32 reference path 
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -16,8 +17,11 @@ import torch
 from .._native import hip_ops, use_native
 
 DENSE, GROUP_M, GROUP_K = 0, 1, 2
-# the grouped weight-gradient mode is used by the models only once it has passed on the hardware
-GROUPED_WGRAD = False
+# expert GEMMs as grouped launches (DLGM_MOE_GROUPED=1) or the per-expert hipBLASLt loop (default until the
+# grouped kernel outruns hipBLASLt: Mixtral 2-layer A/B 98.4k vs 116.9k tok/s, profiles/mixtral_grouped_ab_r02.json);
+# the grouped weight-gradient mode can be switched off on its own (DLGM_MOE_GROUPED_WGRAD=0)
+GROUPED = os.environ.get("DLGM_MOE_GROUPED", "0") == "1"
+GROUPED_WGRAD = os.environ.get("DLGM_MOE_GROUPED_WGRAD", "1") != "0"
 
 
 def _ok(t: torch.Tensor) -> bool:
@@ -44,7 +48,7 @@ def supported(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> bool:
 
 def grouped_supported(x: torch.Tensor) -> bool:
     """Can the grouped kernels take rows `x` (bf16, row-major, 16-B aligned, on the GPU with the extension)?"""
-    return use_native(x) and _ok(x) and x.dim() == 2 and x.stride(1) == 1 and x.stride(0) % 8 == 0
+    return GROUPED and use_native(x) and _ok(x) and x.dim() == 2 and x.stride(1) == 1 and x.stride(0) % 8 == 0
 
 
 def mfma_mm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, acc: bool = False) -> torch.Tensor:

@@ -83,7 +83,6 @@ def test_grouped_rows_forward_uneven_and_empty_groups():
         lo += n
 
 
-@pytest.mark.skip(reason="grouped-K path under investigation (memory fault on the box)")
 def test_grouped_weight_gradient_uneven_and_empty_groups():
     g = torch.Generator(device=dev).manual_seed(3)
     sizes = [130, 0, 700, 1]
