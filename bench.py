@@ -57,6 +57,8 @@ def main() -> int:
                     help="after the timed steps, trace this many extra steps with torch.profiler")
     ap.add_argument("--profile-dir", default="gpurun_out/torch_trace")
     ap.add_argument("--no-telemetry", action="store_true", help="do not poll amdsmi during the run")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"],
+                    help="compute dtype (fp16: the DeepSpeed fp16 path with the dynamic loss scaler)")
     ap.add_argument("--comm-sweep", default="auto", choices=["auto", "on", "off"],
                     help="after the timed steps, measure RCCL busbw over xGMI (auto: when WORLD_SIZE > 1)")
     ap.add_argument("--telemetry-interval", type=float, default=2.0)
@@ -82,7 +84,7 @@ def main() -> int:
                         activation_checkpointing=args.ckpt, max_live_parameters=_knob(args.live_params),
                         max_reuse_distance=_knob(args.reuse_distance),
                         local_grad_accum={"on": True, "off": False}.get(args.local_grads, args.local_grads),
-                        hip_graphs=args.hip_graphs)
+                        hip_graphs=args.hip_graphs, fp16=args.dtype == "fp16")
     t0 = time.time()
     eng = ZeroEngine(mcfg, ecfg, env.device, comm)
     if env.device.type == "cuda":
@@ -153,7 +155,7 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": args.dtype,
             "data": "synthetic (uniform random token ids; random-init weights)",
             "config": {
                 "model": mcfg.name if not args.n_layers else f"{mcfg.name} ({mcfg.n_layers} layers)",

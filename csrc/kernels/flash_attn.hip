@@ -37,6 +37,8 @@ using namespace dlgm;
 namespace {
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+typedef __fp16 hf16x4 __attribute__((ext_vector_type(4)));  // the transpose-read builtin's f16 vector type
+typedef __attribute__((address_space(3))) hf16x4 lds_f16x4;
 
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
@@ -53,6 +55,10 @@ __device__ __forceinline__ bool uniform(bool c) { return __builtin_amdgcn_readfi
 
 __device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+// fp16 compute path (DeepSpeed "fp16" block): the same fragment maps on the f16 MFMA
+__device__ __forceinline__ f32x16 mfma32(const f16x8& a, const f16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
 // 16-byte-chunk XOR swizzles (see header). D = head dim, rows of D bf16.
@@ -75,8 +81,9 @@ __device__ __forceinline__ int swz_dual(int row, int ch) {
   else return ch ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3));
 }
 
-__device__ __forceinline__ bf16x8 lds_read_b128(const bf16* base) {
-  return *reinterpret_cast<const bf16x8*>(base);
+template <typename E>
+__device__ __forceinline__ vec8_t<E> lds_read_b128(const E* base) {
+  return *reinterpret_cast<const vec8_t<E>*>(base);
 }
 
 // x of lane i ^ 32 (the other half-wave): one v_permlane32_swap instead of an LDS bpermute round trip
@@ -90,17 +97,17 @@ __device__ __forceinline__ float swap_halves(float x) {
 // pair (k, k+1) leaves lanes h = 0 with columns 8k .. 8k+7 and lanes h = 1 with 8k+8 .. 8k+15: one
 // 16-byte store per pair instead of two 8-byte stores (the tail is store-issue bound). Both lanes of
 // a pair share the row, so the swap runs on all lanes and only the store is guarded by `valid`.
-template <int DT>
-__device__ __forceinline__ void store_rows_bf16(bf16* row, const f32x16 (&acc)[DT], float scale, int h, bool valid) {
+template <int DT, typename E>
+__device__ __forceinline__ void store_rows_bf16(E* row, const f32x16 (&acc)[DT], float scale, int h, bool valid) {
 #pragma unroll
   for (int k = 0; k < 4 * DT; k += 2) {
     const f32x16& oa = acc[k >> 2];
     const f32x16& ob = acc[(k + 1) >> 2];
     const int ja = 4 * (k & 3), jb = 4 * ((k + 1) & 3);
-    bf16x4 va = {(bf16)(oa[ja] * scale), (bf16)(oa[ja + 1] * scale), (bf16)(oa[ja + 2] * scale),
-                 (bf16)(oa[ja + 3] * scale)};
-    bf16x4 vb = {(bf16)(ob[jb] * scale), (bf16)(ob[jb + 1] * scale), (bf16)(ob[jb + 2] * scale),
-                 (bf16)(ob[jb + 3] * scale)};
+    vec4_t<E> va = {(E)(oa[ja] * scale), (E)(oa[ja + 1] * scale), (E)(oa[ja + 2] * scale),
+                    (E)(oa[ja + 3] * scale)};
+    vec4_t<E> vb = {(E)(ob[jb] * scale), (E)(ob[jb + 1] * scale), (E)(ob[jb + 2] * scale),
+                    (E)(ob[jb + 3] * scale)};
     uint2 a = __builtin_bit_cast(uint2, va), c = __builtin_bit_cast(uint2, vb);
     const auto sx = __builtin_amdgcn_permlane32_swap(a.x, c.x, false, false);
     const auto sy = __builtin_amdgcn_permlane32_swap(a.y, c.y, false, false);
@@ -111,9 +118,15 @@ __device__ __forceinline__ void store_rows_bf16(bf16* row, const f32x16 (&acc)[D
 __device__ __forceinline__ bf16x4 lds_read_tr(const bf16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(p));
 }
+__device__ __forceinline__ f16x4 lds_read_tr(const f16* p) {
+  return __builtin_bit_cast(f16x4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((lds_f16x4*)(p)));
+}
 
 __device__ __forceinline__ bf16x8 cat(bf16x4 a, bf16x4 b) {
   return (bf16x8){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+__device__ __forceinline__ f16x8 cat(f16x4 a, f16x4 b) {
+  return (f16x8){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
 typedef __attribute__((address_space(1))) const void* gptr_t;
@@ -143,7 +156,7 @@ __device__ __forceinline__ void dma16(const void* base, int nbytes, uint32_t vof
 // tile rows at or past S re-read row S-1 (so no address leaves the tensor). SWZ: 0 = row image, 1 = dual image, 2 = tr image.
 // A wave's pieces sit NW*PR rows apart (16 at D = 128, 32 at D = 64), a multiple of every swizzle's
 // row period, so they share ONE per-lane offset (1 VGPR) and differ only by a scalar soffset step.
-template <int D, int ROWS, int SWZ, int NW = 4>
+template <typename E, int D, int ROWS, int SWZ, bool TAIL, int NW = 4>
 struct TileDma {
   static constexpr int CH = D / 8, PR = 64 / CH, NP = ROWS / PR, PPW = NP / NW;
   static_assert(NP % NW == 0, "pieces must split evenly over the waves");
@@ -151,8 +164,8 @@ struct TileDma {
   uint32_t off0;
   int wave, nbytes, nrows;
   int64_t stride;
-  const bf16* base;
-  __device__ __forceinline__ TileDma(const bf16* base_, int64_t row_stride, int nrows_, int wave_, int lane)
+  const E* base;
+  __device__ __forceinline__ TileDma(const E* base_, int64_t row_stride, int nrows_, int wave_, int lane)
       : wave(wave_), nbytes((int)(((int64_t)(nrows_ - 1) * row_stride + D) * 2)), nrows(nrows_), stride(row_stride),
         base(base_) {
     const int rin = lane / CH, phys = lane % CH;
@@ -160,20 +173,23 @@ struct TileDma {
     const int logical = SWZ == 2 ? swz_tr<D>(row, phys) : SWZ == 1 ? swz_dual<D>(row, phys) : swz_row<D>(row, phys);
     off0 = (uint32_t)((row * row_stride + logical * 8) * 2);
   }
-  __device__ __forceinline__ void issue(bf16* img, int row0) const {
-    if (row0 + ROWS <= nrows) {  // whole tile in range: scalar row advance
+  __device__ __forceinline__ void issue(E* img, int row0) const {
+    if (!TAIL || row0 + ROWS <= nrows) {  // whole tile in range: scalar row advance
       const uint32_t soff = (uint32_t)(row0 * stride * 2), step = (uint32_t)(NW * PR * stride * 2);
 #pragma unroll
       for (int j = 0; j < PPW; ++j) dma16(base, nbytes, off0, soff + j * step, img + (wave + NW * j) * 512);
       return;
     }
-    // tail tile: every address stays inside the tensor -- rows at or past nrows re-read row nrows-1
-    // (finite; masked to zero weight by the kernels) and the whole offset goes through voffset
-    const int rin = wave * PR + (int)(threadIdx.x & 63) / CH;
+    if constexpr (TAIL) {
+      // tail tile (S % tile != 0 -- a separate instantiation, so the full-tile kernels keep their
+      // registers): every address stays inside the tensor -- rows at or past nrows re-read row
+      // nrows-1 (finite; masked to zero weight by the kernels), the whole offset goes through voffset
+      const int rin = wave * PR + (int)(threadIdx.x & 63) / CH;
 #pragma unroll
-    for (int j = 0; j < PPW; ++j) {
-      const int r = min(row0 + NW * PR * j + rin, nrows - 1);
-      dma16(base, nbytes, off0 + (uint32_t)((int64_t)(r - rin) * stride * 2), 0, img + (wave + NW * j) * 512);
+      for (int j = 0; j < PPW; ++j) {
+        const int r = min(row0 + NW * PR * j + rin, nrows - 1);
+        dma16(base, nbytes, off0 + (uint32_t)((int64_t)(r - rin) * stride * 2), 0, img + (wave + NW * j) * 512);
+      }
     }
   }
 };
@@ -184,11 +200,12 @@ __device__ __forceinline__ int xcd_remap(int id, int total) {
   return (id % 8) * (total / 8) + id / 8;
 }
 
+template <typename E>
 struct FwdParams {
-  const bf16* q;
-  const bf16* k;
-  const bf16* v;
-  bf16* o;
+  const E* q;
+  const E* k;
+  const E* v;
+  E* o;
   float* lse;
   int64_t q_sb, q_ss, q_sh;
   int64_t k_sb, k_ss, k_sh;
@@ -202,13 +219,13 @@ constexpr int kFwdThreads = 256;
 constexpr int kFwdBQ = 128;  // 4 waves x 32 query rows
 constexpr int kFwdBKV = 64;
 
-template <int D>
-__global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams p) {
+template <typename E, int D, bool TAIL>
+__global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams<E> p) {
   constexpr int CH = D / 8;   // 16-byte chunks per row
   constexpr int KK = D / 16;  // MFMA k-steps over the head dim
   constexpr int DT = D / 32;  // 32-wide output tiles over the head dim
   constexpr int TILE = kFwdBKV * D;
-  __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];
+  __shared__ __attribute__((aligned(16))) E smem[4 * TILE];
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5, i16 = lane & 15, g = lane >> 4;
@@ -227,18 +244,18 @@ __global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams p) 
 
   const int q0 = qt * kFwdBQ;
   const int q0w = q0 + 32 * w;
-  const bf16* qb = p.q + b * p.q_sb + hq * p.q_sh;
-  const bf16* kb = p.k + b * p.k_sb + hk * p.k_sh;
-  const bf16* vb = p.v + b * p.v_sb + hk * p.v_sh;
+  const E* qb = p.q + b * p.q_sb + hq * p.q_sh;
+  const E* kb = p.k + b * p.k_sb + hk * p.k_sh;
+  const E* vb = p.v + b * p.v_sb + hk * p.v_sh;
 
   // Q fragments (B operand of S^T = K Q^T): lane holds Q[q0w + r][16kk + 8h .. +7]
-  bf16x8 qf[KK];
+  vec8_t<E> qf[KK];
   {
     const int qrow = q0w + r;
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk)
-      qf[kk] = qrow < p.S ? *reinterpret_cast<const bf16x8*>(qb + (int64_t)qrow * p.q_ss + 16 * kk + 8 * h)
-                          : (bf16x8)((bf16)0.f);
+      qf[kk] = qrow < p.S ? *reinterpret_cast<const vec8_t<E>*>(qb + (int64_t)qrow * p.q_ss + 16 * kk + 8 * h)
+                          : (vec8_t<E>)((E)0.f);
   }
 
   const int kv_end = p.causal ? min(p.S, q0 + kFwdBQ) : p.S;
@@ -248,8 +265,8 @@ __global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams p) 
   // lane-linearly, the XOR swizzle applied to the SOURCE offset, the tile advance a scalar soffset
   // -- staging costs no VALU and no VGPR round trip; rows past S read as zero.
   const int wu = __builtin_amdgcn_readfirstlane(w);
-  const TileDma<D, kFwdBKV, 0> kdma(kb, p.k_ss, p.S, wu, lane);
-  const TileDma<D, kFwdBKV, 2> vdma(vb, p.v_ss, p.S, wu, lane);
+  const TileDma<E, D, kFwdBKV, 0, TAIL> kdma(kb, p.k_ss, p.S, wu, lane);
+  const TileDma<E, D, kFwdBKV, 2, TAIL> vdma(vb, p.v_ss, p.S, wu, lane);
   auto stage = [&](int buf, int t) {
     kdma.issue(smem + buf * TILE, t * kFwdBKV);
     vdma.issue(smem + (2 + buf) * TILE, t * kFwdBKV);
@@ -271,8 +288,8 @@ __global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams p) 
     if (t + 1 < nt) stage(buf ^ 1, t + 1);
     const int kv0 = t * kFwdBKV;
     if (p.causal && kv0 > q0w + 31) return;  // whole tile above this wave's diagonal
-    const bf16* kt = smem + buf * TILE;
-    const bf16* vt = smem + (2 + buf) * TILE;
+    const E* kt = smem + buf * TILE;
+    const E* vt = smem + (2 + buf) * TILE;
 
     // ---- S^T = K Q^T for two 32-key subtiles
     f32x16 s[2] = {(f32x16)(0.f), (f32x16)(0.f)};
@@ -281,7 +298,7 @@ __global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams p) 
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int row = 32 * u + r;
-        bf16x8 a = lds_read_b128(kt + row * D + swz_row<D>(row, 2 * kk + h) * 8);
+        vec8_t<E> a = lds_read_b128(kt + row * D + swz_row<D>(row, 2 * kk + h) * 8);
         s[u] = mfma32(a, qf[kk], s[u]);
       }
     }
@@ -316,7 +333,7 @@ __global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams p) 
       for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
     }
     const float m_use = m_run == -INFINITY ? 0.f : m_run;
-    bf16x8 pf[2][2];
+    vec8_t<E> pf[2][2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
 #pragma unroll
@@ -327,9 +344,9 @@ __global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams p) 
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
-        pf[u][s2] = (bf16x8){(bf16)s[u][8 * s2 + 0], (bf16)s[u][8 * s2 + 1], (bf16)s[u][8 * s2 + 2],
-                             (bf16)s[u][8 * s2 + 3], (bf16)s[u][8 * s2 + 4], (bf16)s[u][8 * s2 + 5],
-                             (bf16)s[u][8 * s2 + 6], (bf16)s[u][8 * s2 + 7]};
+        pf[u][s2] = (vec8_t<E>){(E)s[u][8 * s2 + 0], (E)s[u][8 * s2 + 1], (E)s[u][8 * s2 + 2],
+                             (E)s[u][8 * s2 + 3], (E)s[u][8 * s2 + 4], (E)s[u][8 * s2 + 5],
+                             (E)s[u][8 * s2 + 6], (E)s[u][8 * s2 + 7]};
     }
 
     // ---- O^T += V^T P^T  (P^T accumulator used in place as the B operand)
@@ -343,8 +360,8 @@ __global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams p) 
         for (int s2 = 0; s2 < 2; ++s2) {
           const int r1 = 32 * u + 16 * s2 + 4 * h + (i16 >> 2);
           const int r2 = r1 + 8;
-          bf16x4 a1 = lds_read_tr(vt + r1 * D + swz_tr<D>(r1, ch) * 8 + within);
-          bf16x4 a2 = lds_read_tr(vt + r2 * D + swz_tr<D>(r2, ch) * 8 + within);
+          vec4_t<E> a1 = lds_read_tr(vt + r1 * D + swz_tr<D>(r1, ch) * 8 + within);
+          vec4_t<E> a2 = lds_read_tr(vt + r2 * D + swz_tr<D>(r2, ch) * 8 + within);
           o[dt] = mfma32(cat(a1, a2), pf[u][s2], o[dt]);
         }
     }
@@ -369,8 +386,8 @@ __global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams p) 
 // delta[b, hq, q] = sum_d dO[b,q,hq,d] * O[b,q,hq,d]. A row of D bf16 is D/8 lanes x 16 B, so a
 // wave64 covers 64 / (D/8) rows at once (4 at D = 128, 8 at D = 64): every lane loads, and the row
 // sum is a shuffle over the row's lane group only.
-template <int D>
-__global__ __launch_bounds__(256) void flash_bwd_delta_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ out,
+template <typename E, int D>
+__global__ __launch_bounds__(256) void flash_bwd_delta_kernel(const E* __restrict__ dout, const E* __restrict__ out,
                                                               float* __restrict__ delta, int B, int S, int Hq,
                                                               int64_t do_ss, int64_t do_sh, int64_t do_sb) {
   constexpr int LPR = D / 8;             // lanes per row
@@ -392,18 +409,19 @@ __global__ __launch_bounds__(256) void flash_bwd_delta_kernel(const bf16* __rest
   if (ok && sub == 0) delta[((int64_t)b * Hq + hq) * S + q] = acc;
 }
 
+template <typename E>
 struct BwdParams {
-  const bf16* q;
-  const bf16* k;
-  const bf16* v;
-  const bf16* dout;
+  const E* q;
+  const E* k;
+  const E* v;
+  const E* dout;
   const float* lse;    // [B, Hq, S], natural log of sum exp(scale * s)
   const float* delta;  // [B, Hq, S]
-  bf16* dq;            // [B, S, Hq, D]
+  E* dq;            // [B, S, Hq, D]
   float* dk_part;      // [group, B, S, Hkv, D] fp32 partials (one per q head of the GQA group)
   float* dv_part;
-  bf16* dk;            // [B, S, Hkv, D] (written directly when group == 1)
-  bf16* dv;
+  E* dk;            // [B, S, Hkv, D] (written directly when group == 1)
+  E* dv;
   int64_t q_sb, q_ss, q_sh;
   int64_t k_sb, k_ss, k_sh;
   int64_t v_sb, v_ss, v_sh;
@@ -422,8 +440,8 @@ struct BwdParams {
 // Stage ROWS x D bf16 rows (row r at base + r*row_stride, r clamped to < nrows_valid) into an
 // LDS image swizzled by SWZ, using LDS-DMA pieces issued by `wave` of `nwaves`. The image is
 // lane-linear per piece; the swizzle is applied to the global SOURCE address (involution).
-template <int D, int ROWS, int SWZ, int NW = 4>  // SWZ: 0 = row image, 1 = dual image; NW waves share it
-__device__ __forceinline__ void stage_rows(bf16* img, const bf16* base, int64_t row_stride, int row0, int nvalid,
+template <typename E, int D, int ROWS, int SWZ, int NW = 4>  // SWZ: 0 = row image, 1 = dual image; NW waves share it
+__device__ __forceinline__ void stage_rows(E* img, const E* base, int64_t row_stride, int row0, int nvalid,
                                            int wave, int lane) {
   constexpr int CH = D / 8;
   constexpr int PR = 64 / CH;               // rows per 1 KiB piece
@@ -443,14 +461,14 @@ constexpr int kKvThreads = 256;
 constexpr int kKvBKV = 128;
 constexpr int kKvBQ = 32;
 
-template <int D>
-__global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams p) {
+template <typename E, int D, bool TAIL>
+__global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams<E> p) {
   constexpr int KK = D / 16;
   constexpr int DT = D / 32;
   constexpr int QT = kKvBQ * D;
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * QT + kKvBKV * D];  // [buf][Q | dO], then V rows
+  __shared__ __attribute__((aligned(16))) E smem[2 * 2 * QT + kKvBKV * D];  // [buf][Q | dO], then V rows
   __shared__ __attribute__((aligned(16))) float rc[2][64];        // [buf][lse 0..31 | delta 32..63]
-  bf16* vimg = smem + 2 * 2 * QT;  // this block's 128 V rows (row image): B operand of dP, re-read per tile
+  E* vimg = smem + 2 * 2 * QT;  // this block's 128 V rows (row image): B operand of dP, re-read per tile
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -465,22 +483,22 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
   const int k0 = kt * kKvBKV;
   const int kw0 = k0 + 32 * w;
   const int key = kw0 + r;
-  const bf16* kb = p.k + b * p.k_sb + hk * p.k_sh;
-  const bf16* vb = p.v + b * p.v_sb + hk * p.v_sh;
-  const bf16* qb = p.q + b * p.q_sb + hq * p.q_sh;
-  const bf16* dob = p.dout + b * p.do_sb + hq * p.do_sh;
+  const E* kb = p.k + b * p.k_sb + hk * p.k_sh;
+  const E* vb = p.v + b * p.v_sb + hk * p.v_sh;
+  const E* qb = p.q + b * p.q_sb + hq * p.q_sh;
+  const E* dob = p.dout + b * p.do_sb + hq * p.do_sh;
   const float* lseb = p.lse + ((int64_t)b * p.Hq + hq) * p.S;
   const float* dlb = p.delta + ((int64_t)b * p.Hq + hq) * p.S;
 
   // K^T B-operand fragments of this wave's 32 keys stay in registers for the whole block; the V
   // rows go to LDS once (registers are the binding constraint at 2 waves / SIMD)
-  bf16x8 kf[KK];
+  vec8_t<E> kf[KK];
 #pragma unroll
   for (int kk = 0; kk < KK; ++kk) {
     const bool ok = key < p.S;
-    kf[kk] = ok ? *reinterpret_cast<const bf16x8*>(kb + (int64_t)key * p.k_ss + 16 * kk + 8 * h) : (bf16x8)((bf16)0.f);
+    kf[kk] = ok ? *reinterpret_cast<const vec8_t<E>*>(kb + (int64_t)key * p.k_ss + 16 * kk + 8 * h) : (vec8_t<E>)((E)0.f);
   }
-  stage_rows<D, kKvBKV, 0>(vimg, vb, p.v_ss, k0, p.S, w, lane);
+  stage_rows<E, D, kKvBKV, 0>(vimg, vb, p.v_ss, k0, p.S, w, lane);
   f32x16 dkt[DT], dvt[DT];  // dK^T, dV^T : [d][key]
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) {
@@ -490,10 +508,10 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
   const int nqt = (p.S + kKvBQ - 1) / kKvBQ;
   const int t0 = p.causal ? k0 / kKvBQ : 0;
 
-  const TileDma<D, kKvBQ, 1> qdma(qb, p.q_ss, p.S, w, lane), dodma(dob, p.do_ss, p.S, w, lane);
+  const TileDma<E, D, kKvBQ, 1, TAIL> qdma(qb, p.q_ss, p.S, w, lane), dodma(dob, p.do_ss, p.S, w, lane);
   auto stage = [&](int buf, int t) {
     const int q0 = t * kKvBQ;
-    bf16* img = smem + buf * 2 * QT;
+    E* img = smem + buf * 2 * QT;
     qdma.issue(img, q0);
     dodma.issue(img + QT, q0);
     if (w == 0) {
@@ -512,8 +530,8 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
     const int q0 = t * kKvBQ;
     const bool active = uniform(!(p.causal && q0 + kKvBQ - 1 < kw0));
     if (active) {
-      const bf16* qi = smem + buf * 2 * QT;
-      const bf16* di = qi + QT;
+      const E* qi = smem + buf * 2 * QT;
+      const E* di = qi + QT;
       f32x16 sacc, dpacc;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -523,14 +541,14 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
       }
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
-        bf16x8 a = lds_read_b128(qi + r * D + swz_dual<D>(r, 2 * kk + h) * 8);
+        vec8_t<E> a = lds_read_b128(qi + r * D + swz_dual<D>(r, 2 * kk + h) * 8);
         sacc = mfma32(a, kf[kk], sacc);
       }
       const int vrow = 32 * w + r;
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
-        bf16x8 a = lds_read_b128(di + r * D + swz_dual<D>(r, 2 * kk + h) * 8);
-        bf16x8 vv = lds_read_b128(vimg + vrow * D + swz_row<D>(vrow, 2 * kk + h) * 8);
+        vec8_t<E> a = lds_read_b128(di + r * D + swz_dual<D>(r, 2 * kk + h) * 8);
+        vec8_t<E> vv = lds_read_b128(vimg + vrow * D + swz_row<D>(vrow, 2 * kk + h) * 8);
         dpacc = mfma32(a, vv, dpacc);
       }
       // dS = P (dP - delta); the softmax scale is applied once to dK at the end
@@ -545,15 +563,15 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
         sacc[i] = pv;
         dpacc[i] *= pv;
       }
-      bf16x8 pfr[2], dsf[2];
+      vec8_t<E> pfr[2], dsf[2];
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        pfr[s2] = (bf16x8){(bf16)sacc[8 * s2 + 0], (bf16)sacc[8 * s2 + 1], (bf16)sacc[8 * s2 + 2],
-                           (bf16)sacc[8 * s2 + 3], (bf16)sacc[8 * s2 + 4], (bf16)sacc[8 * s2 + 5],
-                           (bf16)sacc[8 * s2 + 6], (bf16)sacc[8 * s2 + 7]};
-        dsf[s2] = (bf16x8){(bf16)dpacc[8 * s2 + 0], (bf16)dpacc[8 * s2 + 1], (bf16)dpacc[8 * s2 + 2],
-                           (bf16)dpacc[8 * s2 + 3], (bf16)dpacc[8 * s2 + 4], (bf16)dpacc[8 * s2 + 5],
-                           (bf16)dpacc[8 * s2 + 6], (bf16)dpacc[8 * s2 + 7]};
+        pfr[s2] = (vec8_t<E>){(E)sacc[8 * s2 + 0], (E)sacc[8 * s2 + 1], (E)sacc[8 * s2 + 2],
+                           (E)sacc[8 * s2 + 3], (E)sacc[8 * s2 + 4], (E)sacc[8 * s2 + 5],
+                           (E)sacc[8 * s2 + 6], (E)sacc[8 * s2 + 7]};
+        dsf[s2] = (vec8_t<E>){(E)dpacc[8 * s2 + 0], (E)dpacc[8 * s2 + 1], (E)dpacc[8 * s2 + 2],
+                           (E)dpacc[8 * s2 + 3], (E)dpacc[8 * s2 + 4], (E)dpacc[8 * s2 + 5],
+                           (E)dpacc[8 * s2 + 6], (E)dpacc[8 * s2 + 7]};
       }
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
@@ -563,10 +581,10 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
         for (int s2 = 0; s2 < 2; ++s2) {
           const int r1 = 16 * s2 + 4 * h + (i16 >> 2);
           const int r2 = r1 + 8;
-          bf16x8 a_do = cat(lds_read_tr(di + r1 * D + swz_dual<D>(r1, ch) * 8 + within),
+          vec8_t<E> a_do = cat(lds_read_tr(di + r1 * D + swz_dual<D>(r1, ch) * 8 + within),
                             lds_read_tr(di + r2 * D + swz_dual<D>(r2, ch) * 8 + within));
           dvt[dt] = mfma32(a_do, pfr[s2], dvt[dt]);
-          bf16x8 a_q = cat(lds_read_tr(qi + r1 * D + swz_dual<D>(r1, ch) * 8 + within),
+          vec8_t<E> a_q = cat(lds_read_tr(qi + r1 * D + swz_dual<D>(r1, ch) * 8 + within),
                            lds_read_tr(qi + r2 * D + swz_dual<D>(r2, ch) * 8 + within));
           dkt[dt] = mfma32(a_q, dsf[s2], dkt[dt]);
         }
@@ -604,7 +622,8 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
 }
 
 // Sum the per-q-head fp32 partials of the GQA group (fixed order: deterministic) -> bf16.
-__global__ __launch_bounds__(256) void gqa_reduce_kernel(const float* __restrict__ part, bf16* __restrict__ out,
+template <typename E>
+__global__ __launch_bounds__(256) void gqa_reduce_kernel(const float* __restrict__ part, E* __restrict__ out,
                                                          int group, int64_t n, int row_len, int64_t out_stride) {
   const int64_t nv = n >> 3;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
@@ -627,12 +646,12 @@ constexpr int kDqThreads = 256;
 constexpr int kDqBQ = 128;
 constexpr int kDqBKV = 64;
 
-template <int D>
-__global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams p) {
+template <typename E, int D, bool TAIL>
+__global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams<E> p) {
   constexpr int KK = D / 16;
   constexpr int DT = D / 32;
   constexpr int TILE = kDqBKV * D;
-  __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];  // [buf][K | V]
+  __shared__ __attribute__((aligned(16))) E smem[4 * TILE];  // [buf][K | V]
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -650,17 +669,17 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams p
   const int q0 = qt * kDqBQ;
   const int q0w = q0 + 32 * w;
   const int qcol = q0w + r;
-  const bf16* qb = p.q + b * p.q_sb + hq * p.q_sh;
-  const bf16* dob = p.dout + b * p.do_sb + hq * p.do_sh;
-  const bf16* kb = p.k + b * p.k_sb + hk * p.k_sh;
-  const bf16* vb = p.v + b * p.v_sb + hk * p.v_sh;
+  const E* qb = p.q + b * p.q_sb + hq * p.q_sh;
+  const E* dob = p.dout + b * p.do_sb + hq * p.do_sh;
+  const E* kb = p.k + b * p.k_sb + hk * p.k_sh;
+  const E* vb = p.v + b * p.v_sb + hk * p.v_sh;
 
-  bf16x8 qf[KK], dof[KK];
+  vec8_t<E> qf[KK], dof[KK];
 #pragma unroll
   for (int kk = 0; kk < KK; ++kk) {
     const bool ok = qcol < p.S;
-    qf[kk] = ok ? *reinterpret_cast<const bf16x8*>(qb + (int64_t)qcol * p.q_ss + 16 * kk + 8 * h) : (bf16x8)((bf16)0.f);
-    dof[kk] = ok ? *reinterpret_cast<const bf16x8*>(dob + (int64_t)qcol * p.do_ss + 16 * kk + 8 * h) : (bf16x8)((bf16)0.f);
+    qf[kk] = ok ? *reinterpret_cast<const vec8_t<E>*>(qb + (int64_t)qcol * p.q_ss + 16 * kk + 8 * h) : (vec8_t<E>)((E)0.f);
+    dof[kk] = ok ? *reinterpret_cast<const vec8_t<E>*>(dob + (int64_t)qcol * p.do_ss + 16 * kk + 8 * h) : (vec8_t<E>)((E)0.f);
   }
   const int64_t rowc = ((int64_t)b * p.Hq + hq) * p.S;
   const float lse2 = qcol < p.S ? p.lse[rowc + qcol] * kLog2e : INFINITY;
@@ -672,10 +691,10 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams p
 
   const int kv_end = p.causal ? min(p.S, q0 + kDqBQ) : p.S;
   const int nt = (kv_end + kDqBKV - 1) / kDqBKV;
-  const TileDma<D, kDqBKV, 1> kdma(kb, p.k_ss, p.S, w, lane);
-  const TileDma<D, kDqBKV, 0> vdma(vb, p.v_ss, p.S, w, lane);
+  const TileDma<E, D, kDqBKV, 1, TAIL> kdma(kb, p.k_ss, p.S, w, lane);
+  const TileDma<E, D, kDqBKV, 0, TAIL> vdma(vb, p.v_ss, p.S, w, lane);
   auto stage = [&](int buf, int t) {
-    bf16* img = smem + buf * 2 * TILE;
+    E* img = smem + buf * 2 * TILE;
     kdma.issue(img, t * kDqBKV);
     vdma.issue(img + TILE, t * kDqBKV);
   };
@@ -687,8 +706,8 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams p
     if (t + 1 < nt) stage(buf ^ 1, t + 1);
     const int kv0 = t * kDqBKV;
     if (!(p.causal && kv0 > q0w + 31)) {
-      const bf16* kt = smem + buf * 2 * TILE;
-      const bf16* vt = kt + TILE;
+      const E* kt = smem + buf * 2 * TILE;
+      const E* vt = kt + TILE;
       f32x16 s[2] = {(f32x16)(0.f), (f32x16)(0.f)};
       f32x16 dp[2] = {(f32x16)(-dl), (f32x16)(-dl)};
 #pragma unroll
@@ -696,13 +715,13 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams p
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           const int row = 32 * u + r;
-          bf16x8 a = lds_read_b128(kt + row * D + swz_dual<D>(row, 2 * kk + h) * 8);
+          vec8_t<E> a = lds_read_b128(kt + row * D + swz_dual<D>(row, 2 * kk + h) * 8);
           s[u] = mfma32(a, qf[kk], s[u]);
-          bf16x8 c = lds_read_b128(vt + row * D + swz_row<D>(row, 2 * kk + h) * 8);
+          vec8_t<E> c = lds_read_b128(vt + row * D + swz_row<D>(row, 2 * kk + h) * 8);
           dp[u] = mfma32(c, dof[kk], dp[u]);
         }
       }
-      bf16x8 dsf[2][2];
+      vec8_t<E> dsf[2][2];
       const bool need_mask = uniform((p.causal && kv0 + kDqBKV - 1 > q0w) || kv0 + kDqBKV > p.S);
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -717,9 +736,9 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams p
         }
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2)
-          dsf[u][s2] = (bf16x8){(bf16)s[u][8 * s2 + 0], (bf16)s[u][8 * s2 + 1], (bf16)s[u][8 * s2 + 2],
-                                (bf16)s[u][8 * s2 + 3], (bf16)s[u][8 * s2 + 4], (bf16)s[u][8 * s2 + 5],
-                                (bf16)s[u][8 * s2 + 6], (bf16)s[u][8 * s2 + 7]};
+          dsf[u][s2] = (vec8_t<E>){(E)s[u][8 * s2 + 0], (E)s[u][8 * s2 + 1], (E)s[u][8 * s2 + 2],
+                                (E)s[u][8 * s2 + 3], (E)s[u][8 * s2 + 4], (E)s[u][8 * s2 + 5],
+                                (E)s[u][8 * s2 + 6], (E)s[u][8 * s2 + 7]};
       }
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
@@ -731,7 +750,7 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams p
           for (int s2 = 0; s2 < 2; ++s2) {
             const int r1 = 32 * u + 16 * s2 + 4 * h + (i16 >> 2);
             const int r2 = r1 + 8;
-            bf16x8 a = cat(lds_read_tr(kt + r1 * D + swz_dual<D>(r1, ch) * 8 + within),
+            vec8_t<E> a = cat(lds_read_tr(kt + r1 * D + swz_dual<D>(r1, ch) * 8 + within),
                            lds_read_tr(kt + r2 * D + swz_dual<D>(r2, ch) * 8 + within));
             dqt[dt] = mfma32(a, dsf[u][s2], dqt[dt]);
           }
@@ -747,7 +766,7 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams p
 }
 
 void check_qkv(const at::Tensor& t, const char* name) {
-  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16, name, " must be a bf16 GPU tensor");
+  TORCH_CHECK(t.is_cuda() && DLGM_IS16(t), name, " must be a bf16/fp16 GPU tensor");
   TORCH_CHECK(t.dim() == 4 && t.stride(3) == 1, name, " must be [B, S, H, D] with unit stride on D");
   TORCH_CHECK(t.stride(0) % 8 == 0 && t.stride(1) % 8 == 0 && t.stride(2) % 8 == 0,
               name, " strides must keep 16-byte alignment");
@@ -771,17 +790,24 @@ std::tuple<at::Tensor, at::Tensor> dlgm_flash_attn_fwd(const at::Tensor& q, cons
   auto out = at::empty({B, S, Hq, D}, q.options());
   auto lse = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
   if (B == 0 || S == 0) return {out, lse};
-  FwdParams p{reinterpret_cast<const bf16*>(q.data_ptr()), reinterpret_cast<const bf16*>(k.data_ptr()),
-              reinterpret_cast<const bf16*>(v.data_ptr()), reinterpret_cast<bf16*>(out.data_ptr()),
-              lse.data_ptr<float>(), q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
-              v.stride(0), v.stride(1), v.stride(2), B, S, Hq, Hkv, (float)(softmax_scale * kLog2e), causal};
+  TORCH_CHECK(k.scalar_type() == q.scalar_type() && v.scalar_type() == q.scalar_type(), "flash_attn: mixed dtypes");
   const int nqt = (S + kFwdBQ - 1) / kFwdBQ;
   const int64_t blocks = (int64_t)nqt * B * Hq;
   auto stream = c10::hip::getCurrentHIPStream();
-  if (D == 128)
-    flash_fwd_kernel<128><<<blocks, kFwdThreads, 0, stream>>>(p);
-  else
-    flash_fwd_kernel<64><<<blocks, kFwdThreads, 0, stream>>>(p);
+  DLGM_DISPATCH_16(q.scalar_type(), E, {
+    FwdParams<E> p{reinterpret_cast<const E*>(q.data_ptr()), reinterpret_cast<const E*>(k.data_ptr()),
+                   reinterpret_cast<const E*>(v.data_ptr()), reinterpret_cast<E*>(out.data_ptr()),
+                   lse.data_ptr<float>(), q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
+                   v.stride(0), v.stride(1), v.stride(2), B, S, Hq, Hkv, (float)(softmax_scale * kLog2e), causal};
+    const bool tail = S % 128 != 0;  // a partial K/V tile exists: the clamped-staging instantiation
+    if (D == 128) {
+      if (tail) flash_fwd_kernel<E, 128, true><<<blocks, kFwdThreads, 0, stream>>>(p);
+      else flash_fwd_kernel<E, 128, false><<<blocks, kFwdThreads, 0, stream>>>(p);
+    } else {
+      if (tail) flash_fwd_kernel<E, 64, true><<<blocks, kFwdThreads, 0, stream>>>(p);
+      else flash_fwd_kernel<E, 64, false><<<blocks, kFwdThreads, 0, stream>>>(p);
+    }
+  });
   DLGM_CHECK_HIP(hipGetLastError());
   return {out, lse};
 }
@@ -810,8 +836,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
     // caller's inverse RoPE and dW/dX GEMMs read it without a concatenation pass
     const int64_t C = (int64_t)(Hq + 2 * Hkv) * D;
     const at::Tensor& f = *dqkv;
-    TORCH_CHECK(f.is_cuda() && f.scalar_type() == at::kBFloat16 && f.is_contiguous() && f.numel() == (int64_t)B * S * C,
-                "flash_attn_bwd: dqkv must be a contiguous bf16 [B*S, (Hq+2Hkv)*D] tensor");
+    TORCH_CHECK(f.is_cuda() && f.scalar_type() == q.scalar_type() && f.is_contiguous() &&
+                    f.numel() == (int64_t)B * S * C,
+                "flash_attn_bwd: dqkv must be a contiguous [B*S, (Hq+2Hkv)*D] tensor of q's dtype");
     auto f3 = f.view({B, S, C});
     dq = f3.narrow(2, 0, (int64_t)Hq * D).unflatten(2, {Hq, D});
     dk = f3.narrow(2, (int64_t)Hq * D, (int64_t)Hkv * D).unflatten(2, {Hkv, D});
@@ -831,42 +858,57 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
   }
   auto stream = c10::hip::getCurrentHIPStream();
   const int64_t rows = (int64_t)B * S * Hq;
-  auto dop = reinterpret_cast<const bf16*>(dout.data_ptr());
-  if (D == 128)
-    flash_bwd_delta_kernel<128><<<(rows + 15) / 16, 256, 0, stream>>>(dop, reinterpret_cast<const bf16*>(out.data_ptr()),
-                                                                       delta.data_ptr<float>(), B, S, Hq, dout.stride(1),
-                                                                       dout.stride(2), dout.stride(0));
-  else
-    flash_bwd_delta_kernel<64><<<(rows + 31) / 32, 256, 0, stream>>>(dop, reinterpret_cast<const bf16*>(out.data_ptr()),
-                                                                      delta.data_ptr<float>(), B, S, Hq, dout.stride(1),
-                                                                      dout.stride(2), dout.stride(0));
-  DLGM_CHECK_HIP(hipGetLastError());
-  BwdParams p{reinterpret_cast<const bf16*>(q.data_ptr()), reinterpret_cast<const bf16*>(k.data_ptr()),
-              reinterpret_cast<const bf16*>(v.data_ptr()), dop, lse.data_ptr<float>(), delta.data_ptr<float>(),
-              reinterpret_cast<bf16*>(dq.data_ptr()), group > 1 ? dk_part.data_ptr<float>() : nullptr,
-              group > 1 ? dv_part.data_ptr<float>() : nullptr, reinterpret_cast<bf16*>(dk.data_ptr()),
-              reinterpret_cast<bf16*>(dv.data_ptr()), q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1),
-              k.stride(2), v.stride(0), v.stride(1), v.stride(2), dout.stride(0), dout.stride(1), dout.stride(2), dq_ss,
-              dkv_ss, B, S, Hq, Hkv, (float)softmax_scale, (float)(softmax_scale * kLog2e),
-              (float)(-1.0 / softmax_scale), causal};
+  TORCH_CHECK(k.scalar_type() == q.scalar_type() && v.scalar_type() == q.scalar_type() &&
+                  dout.scalar_type() == q.scalar_type() && out.scalar_type() == q.scalar_type(),
+              "flash_attn_bwd: mixed dtypes");
   const int64_t kv_blocks = (int64_t)B * Hq * ((S + kKvBKV - 1) / kKvBKV);
   const int64_t dq_blocks = (int64_t)B * Hq * ((S + kDqBQ - 1) / kDqBQ);
-  if (D == 128) {
-    flash_bwd_dkdv_kernel<128><<<kv_blocks, kKvThreads, 0, stream>>>(p);
-    flash_bwd_dq_kernel<128><<<dq_blocks, kDqThreads, 0, stream>>>(p);
-  } else {
-    flash_bwd_dkdv_kernel<64><<<kv_blocks, kKvThreads, 0, stream>>>(p);
-    flash_bwd_dq_kernel<64><<<dq_blocks, kDqThreads, 0, stream>>>(p);
-  }
-  DLGM_CHECK_HIP(hipGetLastError());
-  if (group > 1) {
-    const int64_t n = (int64_t)B * S * Hkv * D;
-    const int64_t grid = std::min<int64_t>((n / 8 + 255) / 256, 4096);
-    gqa_reduce_kernel<<<grid, 256, 0, stream>>>(dk_part.data_ptr<float>(), reinterpret_cast<bf16*>(dk.data_ptr()),
-                                                group, n, Hkv * D, dkv_ss);
-    gqa_reduce_kernel<<<grid, 256, 0, stream>>>(dv_part.data_ptr<float>(), reinterpret_cast<bf16*>(dv.data_ptr()),
-                                                group, n, Hkv * D, dkv_ss);
+  DLGM_DISPATCH_16(q.scalar_type(), E, {
+    auto dop = reinterpret_cast<const E*>(dout.data_ptr());
+    auto outp = reinterpret_cast<const E*>(out.data_ptr());
+    if (D == 128)
+      flash_bwd_delta_kernel<E, 128><<<(rows + 15) / 16, 256, 0, stream>>>(dop, outp, delta.data_ptr<float>(), B, S, Hq,
+                                                                          dout.stride(1), dout.stride(2), dout.stride(0));
+    else
+      flash_bwd_delta_kernel<E, 64><<<(rows + 31) / 32, 256, 0, stream>>>(dop, outp, delta.data_ptr<float>(), B, S, Hq,
+                                                                         dout.stride(1), dout.stride(2), dout.stride(0));
     DLGM_CHECK_HIP(hipGetLastError());
-  }
+    BwdParams<E> p{reinterpret_cast<const E*>(q.data_ptr()), reinterpret_cast<const E*>(k.data_ptr()),
+                   reinterpret_cast<const E*>(v.data_ptr()), dop, lse.data_ptr<float>(), delta.data_ptr<float>(),
+                   reinterpret_cast<E*>(dq.data_ptr()), group > 1 ? dk_part.data_ptr<float>() : nullptr,
+                   group > 1 ? dv_part.data_ptr<float>() : nullptr, reinterpret_cast<E*>(dk.data_ptr()),
+                   reinterpret_cast<E*>(dv.data_ptr()), q.stride(0), q.stride(1), q.stride(2), k.stride(0),
+                   k.stride(1), k.stride(2), v.stride(0), v.stride(1), v.stride(2), dout.stride(0), dout.stride(1),
+                   dout.stride(2), dq_ss, dkv_ss, B, S, Hq, Hkv, (float)softmax_scale,
+                   (float)(softmax_scale * kLog2e), (float)(-1.0 / softmax_scale), causal};
+    const bool tail = S % 128 != 0;
+    if (D == 128) {
+      if (tail) {
+        flash_bwd_dkdv_kernel<E, 128, true><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+        flash_bwd_dq_kernel<E, 128, true><<<dq_blocks, kDqThreads, 0, stream>>>(p);
+      } else {
+        flash_bwd_dkdv_kernel<E, 128, false><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+        flash_bwd_dq_kernel<E, 128, false><<<dq_blocks, kDqThreads, 0, stream>>>(p);
+      }
+    } else {
+      if (tail) {
+        flash_bwd_dkdv_kernel<E, 64, true><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+        flash_bwd_dq_kernel<E, 64, true><<<dq_blocks, kDqThreads, 0, stream>>>(p);
+      } else {
+        flash_bwd_dkdv_kernel<E, 64, false><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+        flash_bwd_dq_kernel<E, 64, false><<<dq_blocks, kDqThreads, 0, stream>>>(p);
+      }
+    }
+    DLGM_CHECK_HIP(hipGetLastError());
+    if (group > 1) {
+      const int64_t n = (int64_t)B * S * Hkv * D;
+      const int64_t grid = std::min<int64_t>((n / 8 + 255) / 256, 4096);
+      gqa_reduce_kernel<E><<<grid, 256, 0, stream>>>(dk_part.data_ptr<float>(), reinterpret_cast<E*>(dk.data_ptr()),
+                                                     group, n, Hkv * D, dkv_ss);
+      gqa_reduce_kernel<E><<<grid, 256, 0, stream>>>(dv_part.data_ptr<float>(), reinterpret_cast<E*>(dv.data_ptr()),
+                                                     group, n, Hkv * D, dkv_ss);
+      DLGM_CHECK_HIP(hipGetLastError());
+    }
+  });
   return {dq, dk, dv};
 }

@@ -39,8 +39,8 @@ namespace {
 
 constexpr size_t kWorkspace = 128ull << 20;  // stream-K / split-K solutions need scratch
 
-// problem key: shape, operand layouts (op + leading dim), output dtype, beta != 0
-using Key = std::tuple<int64_t, int64_t, int64_t, int, int64_t, int, int64_t, int64_t, int, bool>;
+// problem key: shape, operand layouts (op + leading dim), output dtype, beta != 0, operand dtype (bf16 / fp16)
+using Key = std::tuple<int64_t, int64_t, int64_t, int, int64_t, int, int64_t, int64_t, int, bool, int>;
 
 struct Problem {
   hipblasLtMatmulDesc_t desc = nullptr;
@@ -77,13 +77,14 @@ Operand as_lt(const at::Tensor& t) {  // t [R, C] row-major or a transposed view
 hipDataType dt(const at::Tensor& t) {
   if (t.scalar_type() == at::kFloat) return HIP_R_32F;
   if (t.scalar_type() == at::kBFloat16) return HIP_R_16BF;
+  if (t.scalar_type() == at::kHalf) return HIP_R_16F;
   TORCH_CHECK(false, "gemm_lt: unsupported dtype ", t.scalar_type());
 }
 
 Problem& problem(State& S, const at::Tensor& out, const at::Tensor& a, const at::Tensor& b, bool beta_nz) {
   const Operand A = as_lt(b), B = as_lt(a);  // hipBLASLt A = b, B = a
   const int64_t M = out.size(1), N = out.size(0), K = a.size(1);
-  Key key{M, N, K, (int)A.op, A.ld, (int)B.op, B.ld, out.stride(0), (int)dt(out), beta_nz};
+  Key key{M, N, K, (int)A.op, A.ld, (int)B.op, B.ld, out.stride(0), (int)dt(out), beta_nz, (int)dt(a)};
   auto it = S.problems.find(key);
   if (it != S.problems.end()) return it->second;
   Problem p;
@@ -107,7 +108,8 @@ void check_args(const at::Tensor& out, const at::Tensor& a, const at::Tensor& b)
   TORCH_CHECK(out.is_cuda() && a.is_cuda() && b.is_cuda(), "gemm_lt: CUDA tensors expected");
   TORCH_CHECK(out.dim() == 2 && a.dim() == 2 && b.dim() == 2, "gemm_lt: 2-D operands");
   TORCH_CHECK(a.size(1) == b.size(0) && out.size(0) == a.size(0) && out.size(1) == b.size(1), "gemm_lt: shape mismatch");
-  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16, "gemm_lt: bf16 operands");
+  TORCH_CHECK((a.scalar_type() == at::kBFloat16 || a.scalar_type() == at::kHalf) && b.scalar_type() == a.scalar_type(),
+              "gemm_lt: bf16 or fp16 operands of one dtype");
   TORCH_CHECK(out.stride(1) == 1, "gemm_lt: row-major output");
 }
 
@@ -203,7 +205,7 @@ at::Tensor dlgm_gemm_lt_tune(const at::Tensor& out, const at::Tensor& a, const a
     LT_CHECK(hipblasLtMatmulDescGetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &va, sizeof(va), &sz));
     LT_CHECK(hipblasLtMatmulDescGetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &vb, sizeof(vb), &sz));
     if (hipblaslt_ext::getAllAlgos(S.handle, hipblaslt_ext::GemmType::HIPBLASLT_GEMM, (hipblasOperation_t)va,
-                                   (hipblasOperation_t)vb, HIP_R_16BF, HIP_R_16BF, dt(out), dt(out),
+                                   (hipblasOperation_t)vb, dt(b), dt(a), dt(out), dt(out),
                                    HIPBLAS_COMPUTE_32F, all) == HIPBLAS_STATUS_SUCCESS)
       for (auto& r : all) add(r.algo);
   }

@@ -226,7 +226,9 @@ class AsyncCheckpointer:
     def _views(self, snap: torch.Tensor) -> Dict[str, torch.Tensor]:
         n = self.n
         f = snap[:12 * n].view(torch.float32).view(3, n)
-        return {"master": f[0], "exp_avg": f[1], "exp_avg_sq": f[2], "bf16": snap[12 * n:14 * n].view(torch.bfloat16)}
+        # "bf16": the 16-bit compute copy (fp16 when the engine runs the fp16 path)
+        return {"master": f[0], "exp_avg": f[1], "exp_avg_sq": f[2],
+                "bf16": snap[12 * n:14 * n].view(self.engine.p16_shard.dtype)}
 
     # ------------------------------------------------------------------ save
     def save(self, step: int, client_state: Optional[Dict[str, Any]] = None, blocking: bool = False) -> str:
@@ -377,7 +379,7 @@ class AsyncCheckpointer:
             self._stream_slot(w, name, v[name])
         files[optim_file(self.rank)] = w.close(fsync=True)
         model = {"module": {}, "buffer_names": [], "param_shapes": meta["param_shapes"],
-                 "bf16_param_shard": Slot("bf16", torch.bfloat16, (self.n,)), "ds_version": DS_VERSION,
+                 "bf16_param_shard": Slot("bf16", eng.p16_shard.dtype, (self.n,)), "ds_version": DS_VERSION,
                  "global_steps": step, "dp_world_size": eng.W, "mp_world_size": 1, "dlgm_layout": lay}
         path = os.path.join(tmp, model_file(self.rank))
         w = PtWriter(path, model)

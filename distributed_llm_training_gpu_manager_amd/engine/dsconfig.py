@@ -24,8 +24,6 @@ def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, **overri
     sp = sch.get("params", {})
     fp16 = ds.get("fp16", {}).get("enabled", False)
     bf16 = ds.get("bf16", {}).get("enabled", False)
-    if fp16 and not bf16:
-        notes.append("fp16 requested: MI355X engine computes in bf16 and keeps the dynamic loss scaler")
     comm = ds.get("communication_data_type", "bf16")
     comm_dtype = {"fp32": torch.float32, "float32": torch.float32}.get(comm, torch.bfloat16)
     if comm in ("fp16", "float16"):

@@ -125,7 +125,7 @@ class Trainer:
         else:
             self.ecfg, self.notes = EngineConfig(zero_stage=args.zero_stage, micro_batch_size=args.micro_batch,
                                                  seq_len=args.seq_len, grad_accum=args.grad_accum, lr=args.lr,
-                                                 seed=args.seed), []
+                                                 seed=args.seed, fp16=getattr(args, "fp16", False)), []
         if args.lr_scale != 1.0:
             self.ecfg.lr *= args.lr_scale
         if getattr(args, "expert_parallel", 0):
@@ -362,6 +362,8 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--device", default="auto")
     ap.add_argument("--zero-stage", type=int, default=3)
+    ap.add_argument("--fp16", action="store_true",
+                    help="fp16 compute with the dynamic loss scaler (without a DeepSpeed config; else its fp16 block)")
     ap.add_argument("--micro-batch", type=int, default=1)
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--lr", type=float, default=3e-4)

@@ -110,7 +110,7 @@ def init_param(spec: ParamSpec, out: torch.Tensor, gen: torch.Generator, seed: i
 def _store_grad(dst: torch.Tensor, src: torch.Tensor, acc: bool) -> None:
     """dst (+)= src. fp32 targets on the GPU take the HIP accumulate kernel (one pass, bf16 or fp32 source:
     torch's mixed-dtype add runs ~3x slower and the cast-then-add pair costs two passes)."""
-    if (dst.is_cuda and dst.dtype == torch.float32 and src.dtype in (torch.bfloat16, torch.float32)
+    if (dst.is_cuda and dst.dtype == torch.float32 and src.dtype in (torch.bfloat16, torch.float16, torch.float32)
             and dst.is_contiguous() and src.is_contiguous() and dst.data_ptr() % 16 == 0 and src.data_ptr() % 16 == 0):
         from ..ops.optim import accumulate_
         accumulate_(dst, src.reshape(dst.shape), 1.0, 1.0 if acc else 0.0)

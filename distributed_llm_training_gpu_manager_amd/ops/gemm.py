@@ -41,7 +41,8 @@ def _plan(a: torch.Tensor, b: torch.Tensor) -> str:
 
 
 def _plannable(a: torch.Tensor, b: torch.Tensor) -> bool:
-    return (a.is_cuda and a.dtype == torch.bfloat16 and a.dim() == 2 and a.stride(0) == 1 and a.stride(1) != 1
+    return (a.is_cuda and a.dtype in (torch.bfloat16, torch.float16) and a.dim() == 2 and a.stride(0) == 1
+            and a.stride(1) != 1
             and b.stride(-1) == 1 and a.shape[0] % 8 == 0 and a.shape[1] % 8 == 0 and b.shape[1] % 8 == 0)
 
 
@@ -64,8 +65,16 @@ def grad_mm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, acc: bool) -> t
     """
     if out.is_cuda and _plannable(a, b):
         a, b = apply_plan(a, b, _plan(a, b))
-    if out.is_cuda and lt_enabled() and lt_mm(out, a, b, acc):
-        return out
+    if out.is_cuda and lt_enabled():
+        if a.dtype == torch.bfloat16 and lt_mm(out, a, b, acc):  # tuned per-problem solution (bf16 table)
+            return out
+        if a.dtype == torch.float16 and out.dtype == torch.float32:
+            # fp16 -> fp32 accumulate straight through hipBLASLt with a solution timed on first use: the
+            # library's first heuristic pick for these problems is a 32x32 macro-tile kernel that ran
+            # ~10 ms per dW GEMM on MI355X (profiles/rocprof_kernel_stats_fp16_heuristic_r02.csv)
+            beta = 1.0 if acc else 0.0
+            hip_ops().gemm_lt(out, a, b, beta, _f16_solution(out, a, b, beta))
+            return out
     if out.dtype == a.dtype:
         if acc:
             return torch.addmm(out, a, b, beta=1.0, out=out)
@@ -120,6 +129,20 @@ def lt_mm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, acc: bool) -> boo
     return True
 
 
+_F16_PICK: dict = {}
+
+
+def _f16_solution(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, beta: float) -> int:
+    """Fastest of hipBLASLt's top heuristic candidates for this fp16 problem, timed once per process."""
+    key = _lt_key(out, a, b, beta)
+    idx = _F16_PICK.get(key)
+    if idx is None:
+        res = hip_ops().gemm_lt_tune(out, a, b, beta, 24, False, 2)
+        idx = int(res[0, 0]) if res.shape[0] else -1
+        _F16_PICK[key] = idx
+    return idx
+
+
 def mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     """a @ b for the forward / input-gradient GEMMs: tuned hipBLASLt solution when one is recorded."""
     if a.is_cuda and a.dtype == torch.bfloat16 and lt_enabled():
@@ -138,7 +161,7 @@ def grad_copy(out: torch.Tensor, src: torch.Tensor, acc: bool) -> None:
 
 def transpose(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Contiguous x^T for a 2-D bf16 tensor (register-blocked HIP kernel on the GPU)."""
-    if use_native(x) and x.dtype == torch.bfloat16 and x.shape[0] % 8 == 0 and x.shape[1] % 8 == 0 \
+    if use_native(x) and x.dtype in (torch.bfloat16, torch.float16) and x.shape[0] % 8 == 0 and x.shape[1] % 8 == 0 \
             and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0:
         return hip_ops().transpose(x, out)
     y = x.t().contiguous()

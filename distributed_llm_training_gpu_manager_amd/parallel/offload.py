@@ -41,8 +41,9 @@ CHUNK_ELEMS = 32 << 20  # 128 MiB of fp32 gradient per staging slot
 class HostOffloadOptimizer:
     def __init__(self, numel: int, device: torch.device, kind: str = "cpu", nvme_path: Optional[str] = None,
                  rank: int = 0, chunk_elems: int = CHUNK_ELEMS, buffer_count: int = 4, aio_threads: int = 8,
-                 aio_block_size: int = 8 << 20):
+                 aio_block_size: int = 8 << 20, dtype: torch.dtype = torch.bfloat16):
         assert kind in ("cpu", "nvme"), kind
+        self.dtype = dtype  # the compute copy: bf16 (AdamW writes it in the host update) or fp16
         if _host.lib() is None:
             raise RuntimeError("optimizer offload needs the host runtime (_dlgm_host.so); run build()")
         self.n, self.device, self.kind = numel, device, kind
@@ -66,7 +67,7 @@ class HostOffloadOptimizer:
         if self.cuda:
             self.stream = torch.cuda.Stream(device)
             self.gslot = [torch.empty(self.chunk, dtype=torch.float32, pin_memory=True) for _ in range(2)]
-            self.pslot = [torch.empty(self.chunk, dtype=torch.bfloat16, pin_memory=True) for _ in range(2)]
+            self.pslot = [torch.empty(self.chunk, dtype=dtype, pin_memory=True) for _ in range(2)]
 
     def _mmap(self, root: str, rank: int, name: str) -> torch.Tensor:
         path = os.path.join(root, f"zero_offload_r{rank}.{name}.f32")
@@ -83,7 +84,7 @@ class HostOffloadOptimizer:
         """p16_shard <- bf16(master) (initialisation / restore)."""
         for off in range(0, self.n, self.chunk):
             ln = min(self.chunk, self.n - off)
-            p16_shard.narrow(0, off, ln).copy_(self.master.narrow(0, off, ln).to(torch.bfloat16))
+            p16_shard.narrow(0, off, ln).copy_(self.master.narrow(0, off, ln).to(p16_shard.dtype))
 
     # ------------------------------------------------------------------ step
     def step(self, grad_shard: torch.Tensor, p16_shard: torch.Tensor, *, lr: float, beta1: float, beta2: float,
@@ -122,14 +123,23 @@ class HostOffloadOptimizer:
             slot = i % 2
             if h2d[slot] is not None:
                 h2d[slot].synchronize()  # the H2D of chunk i-2 has drained this bf16 staging slot
-            _host.cpu_adamw_(self.master.narrow(0, off, ln), self.exp_avg.narrow(0, off, ln),
-                             self.exp_avg_sq.narrow(0, off, ln), self.gslot[slot][:ln], self.pslot[slot][:ln], *hyper)
+            self._host_update(self.master.narrow(0, off, ln), self.exp_avg.narrow(0, off, ln),
+                              self.exp_avg_sq.narrow(0, off, ln), self.gslot[slot][:ln], self.pslot[slot][:ln], hyper)
             with torch.cuda.stream(s):
                 p16_shard.narrow(0, off, ln).copy_(self.pslot[slot][:ln], non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(s)
             h2d[slot] = ev
         cur.wait_stream(s)  # compute resumes on the updated bf16 params
+
+    @staticmethod
+    def _host_update(master, m, v, g, p16, hyper) -> None:
+        """AVX2 AdamW on one chunk; the runtime writes a bf16 compute copy itself, an fp16 one is cast here."""
+        if p16 is None or p16.dtype == torch.bfloat16:
+            _host.cpu_adamw_(master, m, v, g, p16, *hyper)
+        else:
+            _host.cpu_adamw_(master, m, v, g, None, *hyper)
+            p16.copy_(master)
 
     def _step_swapped(self, grad_shard: torch.Tensor, p16_shard: torch.Tensor, hyper) -> None:
         """NVMe: state chunks stream file -> ring slot -> AdamW -> file, reads running buffer_count-2
@@ -190,7 +200,7 @@ class HostOffloadOptimizer:
             else:
                 g = grad_shard.narrow(0, off, ln)
                 p16 = p16_shard.narrow(0, off, ln) if p16_shard.dtype == torch.bfloat16 else None
-            _host.cpu_adamw_(st[0, :ln], st[1, :ln], st[2, :ln], g, p16, *hyper)
+            self._host_update(st[0, :ln], st[1, :ln], st[2, :ln], g, p16, hyper)
             writes[i] = [aio.write(h, st[k, :ln], off * 4) for k, h in enumerate(self.fh)]
             if cuda:
                 with torch.cuda.stream(s):

@@ -298,8 +298,9 @@ class ZeroEngine:
             g.gfull_off = goff
             goff += g.numel if g.P > 1 else 0
         self.gfull_total = goff
-        # MI355X compute dtype is bf16 (fp16 requests keep the loss-scaler path but compute in bf16)
-        self.dtype = torch.bfloat16
+        # compute dtype: bf16, or fp16 for the DeepSpeed "fp16" block -- every HIP kernel has an f16
+        # instantiation (f16 MFMA in attention) and the dynamic loss scaler guards the fp16 range
+        self.dtype = torch.float16 if cfg.fp16 else torch.bfloat16
         self.is_cuda = device.type == "cuda"
         self.tuned_gemm_files: List[str] = []
         if self.is_cuda and cfg.tuned_gemms:
@@ -395,7 +396,8 @@ class ZeroEngine:
             self.offload = HostOffloadOptimizer(n, dev, self.cfg.offload_optimizer, self.cfg.nvme_path, self.rank,
                                                 buffer_count=self.cfg.offload_buffer_count,
                                                 aio_threads=self.cfg.aio_threads,
-                                                aio_block_size=self.cfg.aio_block_size)
+                                                aio_block_size=self.cfg.aio_block_size,
+                                                dtype=torch.float16 if self.cfg.fp16 else torch.bfloat16)
             self.master, self.exp_avg, self.exp_avg_sq = (self.offload.master, self.offload.exp_avg,
                                                           self.offload.exp_avg_sq)
         else:
@@ -473,10 +475,8 @@ class ZeroEngine:
             self.offload.push_params(self.p16_shard)
         elif self.param_host:
             self._p16_to_host()
-        elif self.dtype == torch.bfloat16:
-            ops.cast_f32_bf16_(self.p16_shard, self.master)
         else:
-            self.p16_shard.copy_(self.master)
+            ops.cast_f32_bf16_(self.p16_shard, self.master)  # bf16 or fp16 compute copy
 
     def _p16_to_host(self) -> None:
         """offload_param with the optimizer on the device: bf16(master) chunk by chunk into a device scratch,
@@ -898,14 +898,12 @@ class ZeroEngine:
             self._offload_step(lr, inv_scale)
         else:
             ops.adamw_step_(self.master, self.exp_avg, self.exp_avg_sq, self.grad_shard,
-                            self.p16_shard if self.dtype == torch.bfloat16 and not self.param_host else None,
+                            None if self.param_host else self.p16_shard,
                             self.stats, lr=lr,
                             beta1=cfg.betas[0], beta2=cfg.betas[1], eps=cfg.eps, weight_decay=cfg.weight_decay,
                             step=self.step_count, grad_scale=inv_scale, max_norm=cfg.grad_clip)
             if self.param_host:
                 self._p16_to_host()
-            elif self.dtype != torch.bfloat16:
-                self.p16_shard.copy_(self.master)
         self._pver += 1  # the compute copy changes below: transposed caches are stale
         if self.stage == 3:
             self._live.clear()  # (micro_step(last=True) already dropped them; direct callers may not have)

@@ -71,6 +71,15 @@ def test_mixtral_manual_backward_matches_autograd_gpu():
     _check("cuda", "mixtral-tiny", tol=1e-1)
 
 
+@pytest.mark.gpu
+def test_mixtral_grouped_expert_gemms_match_autograd_gpu(monkeypatch):
+    """Experts as grouped MFMA launches (device offsets from moe_permute, no host read of the counts)."""
+    from distributed_llm_training_gpu_manager_amd.ops import gemm_mfma as gm
+    monkeypatch.setattr(gm, "GROUPED", True)
+    monkeypatch.setattr(gm, "GROUPED_WGRAD", True)
+    _check("cuda", "mixtral-tiny", tol=1e-1)
+
+
 @pytest.mark.parametrize("aux", [0.0, 0.02])
 def test_moe_block_exact_in_fp32(aux):
     """The hand-written MoE forward/backward (router top-2, dispatch, experts, combine, aux loss)
