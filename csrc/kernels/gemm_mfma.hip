@@ -79,63 +79,82 @@ __device__ __forceinline__ void dma16(const void* base, uint32_t nbytes, uint32_
                                            (lptr_t)lds, 16, voff, soff, 0, 0);
 }
 
-// Staging plan of one operand tile (256 rows/cols x 64 k): the per-lane byte offset is loop-invariant,
-// each wave issues 4 pieces that differ by a scalar step (the swizzle period divides the piece step).
-template <bool KMAJ>
-struct Stager {
-  uint32_t voff;
-  uint32_t step;
+// 16 zero bytes in global memory: the source of the k rows past a partial K tile (grouped-K group ends)
+__device__ __attribute__((aligned(16))) bf16 g_zero16[8];
+
+// Half-tile staging plan of one operand. OP 0 = A (halves split the M rows by quadrant: half h holds rows
+// wr*128 + h*64 + [0, 64) of both wave rows), OP 1 = B (half h holds columns wc*64 + h*32 + [0, 32) of all four
+// wave columns), so a wave's quadrant (mq, nq) reads exactly A half mq and B half nq. Half images:
+//   K-contiguous: [128 rows][64 k], 128-B rows, chunk c at c ^ ((row>>1)&7)       (ds_read_b128 fragments)
+//   MN-contiguous: [64 k][128 cols], 256-B rows, chunk c at c ^ swz_mn(k)          (ds_read_b64_tr_b16 pairs)
+// 16 pieces of 1 KiB per half; wave w moves pieces w and w+8, whose source offsets differ by a constant
+// (the swizzle period divides the piece step), as do the two halves: one VGPR offset per operand.
+template <bool KMAJ, int OP>
+struct HalfStager {
+  uint32_t voff, piece2, hstep;
   int wave;
-  __device__ __forceinline__ Stager(int64_t ld, int wave_, int lane) : wave(wave_) {
-    if constexpr (KMAJ) {  // piece j = rows 8j .. 8j+7 (128 B each); this wave: j = wave + 8 i
-      const int row = 8 * wave + (lane >> 3), phys = lane & 7;
-      const int c = phys ^ swz_k(row);
-      voff = (uint32_t)((row * ld + c * 8) * 2);
-      step = (uint32_t)(64 * ld * 2);
-    } else {  // piece j = k rows 2j, 2j+1 (512 B each); this wave: j = wave + 8 i
-      const int row = 2 * wave + (lane >> 5), phys = lane & 31;
-      const int c = phys ^ swz_mn(row);
-      voff = (uint32_t)((row * ld + c * 8) * 2);
-      step = (uint32_t)(16 * ld * 2);
+  __device__ __forceinline__ HalfStager(int64_t ld, int wave_, int lane) : wave(wave_) {
+    if constexpr (KMAJ) {
+      const int hr = 8 * wave + (lane >> 3), c = (lane & 7) ^ swz_k(hr);
+      const int grow = OP == 0 ? (hr >> 6) * 128 + (hr & 63) : (hr >> 5) * 64 + (hr & 31);
+      voff = (uint32_t)((grow * ld + c * 8) * 2);
+      piece2 = (uint32_t)(128 * ld * 2);  // half-row + 64 -> tile row + 128 (both operands)
+      hstep = (uint32_t)((OP == 0 ? 64 : 32) * ld * 2);
+    } else {
+      const int k = 4 * wave + (lane >> 4), c = (lane & 15) ^ swz_mn(k);
+      const int lc = c * 8;
+      const int gcol = OP == 0 ? (lc >> 6) * 128 + (lc & 63) : (lc >> 5) * 64 + (lc & 31);
+      voff = (uint32_t)((k * ld + gcol) * 2);
+      piece2 = (uint32_t)(32 * ld * 2);  // k + 32
+      hstep = (uint32_t)((OP == 0 ? 64 : 32) * 2);
     }
   }
-  // `base` = first element of the tile (row 0 / k row 0), `nbytes` bounds the valid region from base.
-  // The piece step goes into the VGPR offset (a raw buffer's range check covers voffset only), and on
-  // a partial tile (`nvalid` < rows of the image) rows past the end are clamped onto the last valid row,
-  // so no lane ever addresses memory outside the operand whatever the range check does; the duplicated
-  // rows are finite and are either masked out of the reduction (k rows, read_frag) or feed output
-  // rows that are never stored (m / n rows).
-  __device__ __forceinline__ void issue(char* img, const bf16* base, uint32_t nbytes, int64_t ld, int nvalid) const {
-    constexpr int ROWS = KMAJ ? 256 : 64;
-    // last line of defence: a lane whose 16 B would end past `nbytes` reads the tile's first chunk instead
+  // Stage half `h` of the tile at `base` (row / k-row 0 of the tile; `nbytes` bounds the valid region from
+  // base) into `img`. `nvalid` < the image's rows (256 tile rows K-contiguous, 64 k-rows MN-contiguous): a
+  // partial tile, whose rows past the end are clamped onto the last valid one (no address leaves the
+  // operand; the copies are masked out of the reduction or feed output rows that are never stored).
+  template <bool PART>  // PART: partial tiles can occur in this instantiation
+  __device__ __forceinline__ void issue(char* img, const bf16* base, uint32_t nbytes, int64_t ld, int h,
+                                        int nvalid) const {
     auto guard = [nbytes](uint32_t vo) { return vo + 16 <= nbytes ? vo : 0u; };
-    if (__builtin_amdgcn_readfirstlane(nvalid) >= ROWS) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) dma16(base, nbytes, guard(voff + i * step), 0, img + (wave + 8 * i) * 1024);
+    constexpr int ROWS = KMAJ ? 256 : 64;
+    const uint32_t v0 = voff + h * hstep;
+    if (!PART || __builtin_amdgcn_readfirstlane(nvalid) >= ROWS) {
+      dma16(base, nbytes, guard(v0), 0, img + wave * 1024);
+      dma16(base, nbytes, guard(v0 + piece2), 0, img + (wave + 8) * 1024);
       return;
     }
+    if constexpr (!PART) return;
+    // partial tile: the same offsets, each lane's row moved onto the last valid one (negative deltas wrap)
     const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int row, c;
+    for (int j = 0; j < 2; ++j) {
+      int row;  // the tile row (K-contiguous) or k-row (MN-contiguous) this lane's 16 B come from
       if constexpr (KMAJ) {
-        row = 8 * wave + 64 * i + (lane >> 3);
-        c = (lane & 7) ^ swz_k(row);
+        const int hr = 8 * (wave + 8 * j) + (lane >> 3);
+        row = OP == 0 ? (hr >> 6) * 128 + h * 64 + (hr & 63) : (hr >> 5) * 64 + h * 32 + (hr & 31);
       } else {
-        row = 2 * wave + 16 * i + (lane >> 5);
-        c = (lane & 31) ^ swz_mn(row);
+        row = 4 * (wave + 8 * j) + (lane >> 4);
       }
-      const int src = row < nvalid ? row : nvalid - 1;
-      dma16(base, nbytes, guard((uint32_t)((src * ld + c * 8) * 2)), 0, img + (wave + 8 * i) * 1024);
+      if constexpr (KMAJ) {  // rows past the end feed output rows that are never stored: clamp them
+        const int src = row < nvalid ? row : nvalid - 1;
+        dma16(base, nbytes, guard(v0 + j * piece2 + (uint32_t)((int64_t)(src - row) * ld * 2)), 0,
+              img + (wave + 8 * j) * 1024);
+      } else {  // k rows past the end must contribute zero: those lanes copy from a zero chunk instead
+        if (row < nvalid)
+          dma16(base, nbytes, guard(v0 + j * piece2), 0, img + (wave + 8 * j) * 1024);
+        else
+          dma16(g_zero16, 16, 0, 0, img + (wave + 8 * j) * 1024);
+      }
     }
   }
 };
 
-// 16x16x32 fragment (lane: row/col l&15, k = 8(l>>4) + j) of the operand image, k-substep s.
-// `kv` < BK: a partial K tile of an MN image -- elements with k >= kv are zeroed (their LDS rows
-// hold a clamped copy of the last valid row).
-template <bool KMAJ>
-__device__ __forceinline__ bf16x8 read_frag(const char* img, int r0, int s, int lane, int kv) {
+// 16x16x32 fragment (lane: row l&15, k = 8(l>>4) + j) of a HALF image, k-substep s, rows r0.. of the half.
+// (MASK: zero the elements with k >= kv in registers -- unused: partial K tiles are zero-filled in LDS by
+// the staging, which keeps the grouped-K kernel free of spills.)
+template <bool KMAJ, bool MASK>
+__device__ __forceinline__ bf16x8 frag(const char* img, int r0, int s, int lane, int kv) {
   const int i = lane & 15, g = lane >> 4;
   if constexpr (KMAJ) {
     const int r = r0 + i, c = 4 * s + g;
@@ -145,9 +164,9 @@ __device__ __forceinline__ bf16x8 read_frag(const char* img, int r0, int s, int 
     const int ch = (r0 >> 3) + (p >> 1);
     const int k1 = 32 * s + 8 * g + q;
     const int x = swz_mn(k1);  // k1 and k1 + 4 share it
-    const char* a = img + k1 * 512 + ((ch ^ x) << 4) + (p & 1) * 8;
-    bf16x8 v = cat4(lds_tr(a), lds_tr(a + 4 * 512));
-    if (__builtin_amdgcn_readfirstlane(kv) < BK) {
+    const char* a = img + k1 * 256 + ((ch ^ x) << 4) + (p & 1) * 8;
+    bf16x8 v = cat4(lds_tr(a), lds_tr(a + 4 * 256));
+    if (MASK && __builtin_amdgcn_readfirstlane(kv) < BK) {
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         if (32 * s + 8 * g + j >= kv) v[j] = (bf16)0.f;
@@ -161,9 +180,27 @@ __device__ __forceinline__ int xcd_remap(int id, int total) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + id / 8;
 }
 
+__device__ __forceinline__ void raw_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// One K-tile of the main loop = 4 phases; each phase: this phase's LDS fragment reads, one half-tile of
+// LDS-DMA for a later K-tile, a counted vmcnt, barrier, 16 MFMAs (one 64x32 output quadrant x K=64),
+// barrier. The two wave rows run one barrier apart (wave row 1 takes an extra barrier up front), so on
+// every SIMD one wave issues its reads / DMA while the other runs MFMAs. Read / restage rules
+// (cdna_hip_programming.md §5 '8-phase template'): a half-tile is read one phase after the wait that retires
+// it, and restaged at least two phases after its last read:
+//   phase 1 reads A half 0 + B half 0 (K-tile k) and stages B half 1 of k+1 (other buffer),
+//   phase 2 reads B half 1 and stages A half 1 of k+1,
+//   phase 3 reads A half 1 and stages A half 0 of k+2 (this buffer: last read in phase 1),
+//   phase 4 reads nothing (every fragment is in registers) and stages B half 0 of k+2.
+// With that order four half-tiles are always in flight: vmcnt(8) (2 DMA instructions per half-tile) before
+// each phase's first barrier retires exactly what the next phase reads, until the stages run out (then 0).
 template <int MODE, bool AK, bool BKM, int EPI>
 __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
-  __shared__ __attribute__((aligned(1024))) char smem[4 * TILE_BYTES];  // [buf][A | B]
+  __shared__ __attribute__((aligned(1024))) char smem[4 * TILE_BYTES];  // [buf][A | B][half][16 KiB]
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = w >> 2, wc = w & 3;
@@ -175,9 +212,19 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
   int m_lo = 0, m_hi = p.M;  // valid rows of A / C for this block
   int k_lo = 0, k_hi = p.K;  // reduction range
   constexpr int CES = EPI == kStoreBf16 ? 2 : 4;
+  // tile order: GM output rows x all columns per group, walked down the GM rows first, so the ~32 blocks
+  // resident on one XCD (consecutive ids after the XCD remap) cover a GM x (32/GM) patch: per K-step they
+  // read GM A tiles + 32/GM B tiles instead of 1-2 A + ~30 B tiles (half the L2 misses, measured)
+  constexpr int GM = 4;
+  auto grouped_tile = [&](int lin, int tiles_m, int& om, int& on) {
+    const int per = GM * p.tiles_n;
+    const int g = lin / per, rem = lin - g * per;
+    const int gm = min(GM, tiles_m - g * GM);
+    on = rem / gm;
+    om = g * GM + (rem - on * gm);
+  };
   if constexpr (MODE == kDense) {
-    tm = id / p.tiles_n;
-    tn = id - tm * p.tiles_n;
+    grouped_tile(id, p.tiles_m, tm, tn);
   } else if constexpr (MODE == kGroupM) {
     tn = id % p.tiles_n;
     int j = id / p.tiles_n;
@@ -197,9 +244,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
   } else {  // grouped-K
     const int per = p.tiles_m * p.tiles_n;
     grp = id / per;
-    const int rem = id - grp * per;
-    tm = rem / p.tiles_n;
-    tn = rem - tm * p.tiles_n;
+    grouped_tile(id - grp * per, p.tiles_m, tm, tn);
     k_lo = p.offsets[grp];
     k_hi = p.offsets[grp + 1];
   }
@@ -218,60 +263,102 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4)(0.f);
 
   const int nk = (k_hi - k_lo + BK - 1) / BK;
+  // partial tiles: K (grouped-K group ends), M rows (K-contiguous A: grouped-M group ends / M % 256 != 0)
+  constexpr bool PK = MODE == kGroupK, PM = AK;
   if (nk > 0) {
-    const Stager<AK> sa(p.lda, w, lane);
-    const Stager<BKM> sb(p.ldb, w, lane);
-    // A tile t: AK -> rows m0.., k from k_lo + 64t ; !AK -> k rows, columns m0..
-    auto stage = [&](int buf, int t) {
+    const HalfStager<AK, 0> sa(p.lda, w, lane);
+    const HalfStager<BKM, 1> sb(p.ldb, w, lane);
+    auto region = [&](int buf, int op, int h) { return smem + buf * 2 * TILE_BYTES + op * TILE_BYTES + h * (TILE_BYTES / 2); };
+    // stage half h of operand op for K-tile t (skipped past the end); returns whether anything was issued
+    auto stage = [&](int op, int h, int t) -> bool {
+      if (t >= nk) return false;
       const int k0 = k_lo + t * BK;
-      char* img = smem + buf * 2 * TILE_BYTES;
       const int kv = min(BK, k_hi - k0);
-      if constexpr (AK) {
-        const bf16* base = A + (int64_t)m0 * p.lda + k0;
-        sa.issue(img, base, (uint32_t)(((int64_t)(rows_valid - 1) * p.lda + BK) * 2), p.lda, rows_valid);
+      char* img = region(t & 1, op, h);
+      if (op == 0) {
+        if constexpr (AK)
+          sa.template issue<PM>(img, A + (int64_t)m0 * p.lda + k0, (uint32_t)(((int64_t)(rows_valid - 1) * p.lda + BK) * 2), p.lda,
+                   h, rows_valid);
+        else
+          sa.template issue<PK>(img, A + (int64_t)k0 * p.lda + m0, (uint32_t)(((int64_t)(kv - 1) * p.lda + BM) * 2), p.lda, h, kv);
       } else {
-        const bf16* base = A + (int64_t)k0 * p.lda + m0;
-        sa.issue(img, base, (uint32_t)(((int64_t)(kv - 1) * p.lda + BM) * 2), p.lda, kv);
+        if constexpr (BKM)
+          sb.template issue<false>(img, B + (int64_t)n0 * p.ldb + k0, (uint32_t)(((int64_t)(BN - 1) * p.ldb + BK) * 2), p.ldb, h, BN);
+        else
+          sb.template issue<PK>(img, B + (int64_t)k0 * p.ldb + n0, (uint32_t)(((int64_t)(kv - 1) * p.ldb + BN) * 2), p.ldb, h, kv);
       }
-      if constexpr (BKM) {
-        const bf16* base = B + (int64_t)n0 * p.ldb + k0;
-        sb.issue(img + TILE_BYTES, base, (uint32_t)(((int64_t)(BN - 1) * p.ldb + BK) * 2), p.ldb, BN);
-      } else {
-        const bf16* base = B + (int64_t)k0 * p.ldb + n0;
-        sb.issue(img + TILE_BYTES, base, (uint32_t)(((int64_t)(kv - 1) * p.ldb + BN) * 2), p.ldb, kv);
-      }
+      return true;
     };
-    auto tile = [&](auto bufc, int t) {
-      constexpr int buf = decltype(bufc)::value;
-      const char* aimg = smem + buf * 2 * TILE_BYTES;
-      const char* bimg = aimg + TILE_BYTES;
-      const int kv = min(BK, k_hi - (k_lo + t * BK));
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        bf16x8 bfr[4];
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) bfr[ni] = read_frag<BKM>(bimg, wc * 64 + 16 * ni, s, lane, kv);
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi) {
-          const bf16x8 afr = read_frag<AK>(aimg, wr * 128 + 16 * mi, s, lane, kv);
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = mfma16(bfr[ni], afr, acc[mi][ni]);
-        }
-      }
-    };
-    stage(0, 0);
-    for (int t = 0; t < nk; t += 2) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (t + 1 < nk) stage(1, t + 1);
-      tile(std::integral_constant<int, 0>{}, t);
-      if (t + 1 < nk) {
+    auto wait = [](bool all_issued) {
+      if (all_issued)
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (t + 2 < nk) stage(0, t + 2);
-        tile(std::integral_constant<int, 1>{}, t + 1);
+    };
+    bf16x8 af[4][2], bq0[2][2], bq1[2][2];
+    auto mma = [&](int mq, int nq) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[4 * mq + i][2 * nq + j] = mfma16(nq ? bq1[j][s2] : bq0[j][s2], af[i][s2], acc[4 * mq + i][2 * nq + j]);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    auto phase_end = [&](bool issued, int mq, int nq) {
+      wait(issued);
+      raw_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      mma(mq, nq);
+      raw_barrier();
+    };
+    auto ktile = [&](auto bufc, int t) {
+      constexpr int buf = decltype(bufc)::value;
+      const int kv = min(BK, k_hi - (k_lo + t * BK));
+      const char* a0 = region(buf, 0, 0);
+      const char* a1 = region(buf, 0, 1);
+      const char* b0 = region(buf, 1, 0);
+      const char* b1 = region(buf, 1, 1);
+      // phase 1: A half 0 + B half 0 -> quadrant (0, 0)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bq0[j][s2] = frag<BKM, false>(b0, wc * 32 + 16 * j, s2, lane, kv);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i][s2] = frag<AK, false>(a0, wr * 64 + 16 * i, s2, lane, kv);
       }
+      phase_end(stage(1, 1, t + 1), 0, 0);
+      // phase 2: B half 1 -> quadrant (0, 1)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bq1[j][s2] = frag<BKM, false>(b1, wc * 32 + 16 * j, s2, lane, kv);
+      phase_end(stage(0, 1, t + 1), 0, 1);
+      // phase 3: A half 1 -> quadrant (1, 1)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i][s2] = frag<AK, false>(a1, wr * 64 + 16 * i, s2, lane, kv);
+      phase_end(stage(0, 0, t + 2), 1, 1);
+      // phase 4: registers only -> quadrant (1, 0)
+      phase_end(stage(1, 0, t + 2), 1, 0);
+    };
+    // prologue: the six half-tiles the loop expects in flight (in the loop's stage order)
+    stage(0, 0, 0);
+    stage(1, 0, 0);
+    stage(1, 1, 0);
+    stage(0, 1, 0);
+    stage(0, 0, 1);
+    wait(stage(1, 0, 1));
+    raw_barrier();
+    if (wr == 1) raw_barrier();  // wave row 1 runs one barrier behind
+    for (int t = 0; t < nk; t += 2) {
+      ktile(std::integral_constant<int, 0>{}, t);
+      if (t + 1 < nk) ktile(std::integral_constant<int, 1>{}, t + 1);
     }
+    if (wr == 0) raw_barrier();  // equal barrier counts for both wave rows
   }
 
   // ---- epilogue: lane holds C[m][n .. n+3] (m = column of D^T, n = 4 rows of D^T)

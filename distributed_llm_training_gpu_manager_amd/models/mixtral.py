@@ -79,12 +79,12 @@ class MixtralBlock(LlamaBlock):
         ctx.aux.setdefault("moe_aux", []).append(float(E) * (f * probs.mean(0)).sum())
         return out, (probs, topi, gates, pos, f, x_local, dctx, exp_saved, y_sorted)
 
-    def _grouped(self, x: torch.Tensor) -> bool:
+    def _grouped(self, x: torch.Tensor, wgrad: bool = False) -> bool:
         """Expert GEMMs as single grouped MFMA launches (csrc/kernels/gemm_mfma.hip) with the device
-        offsets: no host read of the routing counts, no per-expert launches."""
+        offsets: no host read of the routing counts, no per-expert launches (wgrad: the dW GEMMs only)."""
         c = self.cfg
-        return gm.grouped_supported(x) and (2 * c.ffn_dim) % 256 == 0 and c.d_model % 256 == 0 \
-            and c.ffn_dim % 64 == 0 and c.d_model % 64 == 0
+        return gm.grouped_supported(x, wgrad) and (2 * c.ffn_dim) % 256 == 0 and c.d_model % 256 == 0 \
+            and c.ffn_dim % 256 == 0 and c.d_model % 64 == 0
 
     def _experts_fwd(self, p: Params, x: torch.Tensor, dctx):
         c = self.cfg
@@ -114,7 +114,7 @@ class MixtralBlock(LlamaBlock):
 
     def _experts_bwd(self, p: Params, g: Params, x: torch.Tensor, dy: torch.Tensor, saved, acc: bool):
         gu_all, a_all, dctx = saved
-        if self._grouped(x) and gm.GROUPED_WGRAD:
+        if self._grouped(x):
             offs = dctx.local_offsets
             dy = dy.contiguous()
             da_all = gm.grouped_mm(dy, p["w_down"], offs, transpose_w=False)
@@ -124,26 +124,35 @@ class MixtralBlock(LlamaBlock):
             gm.grouped_wgrad(g["w_gate_up"], dgu_all, x, offs, acc)
             return gm.grouped_mm(dgu_all, p["w_gate_up"], offs, transpose_w=False)
         counts = dctx.counts()
+        # weight gradients as grouped launches (reduction over each expert's token rows, device offsets)
+        gw = self._grouped(x, wgrad=True) and dctx.local_offsets is not None
+        dy = dy.contiguous() if gw else dy
         dx = torch.empty_like(x)
         da_all = torch.empty_like(a_all)
+        if gw:
+            gm.grouped_wgrad(g["w_down"], dy, a_all, dctx.local_offsets, acc)
         off = 0
         for e, n in enumerate(counts):
             if n == 0:
-                if not acc:
+                if not acc and not gw:
                     g["w_down"][e].zero_()
                     g["w_gate_up"][e].zero_()
                 continue
             dye = dy.narrow(0, off, n)
-            grad_mm(g["w_down"][e], dye.t(), a_all.narrow(0, off, n), acc)
+            if not gw:
+                grad_mm(g["w_down"][e], dye.t(), a_all.narrow(0, off, n), acc)
             torch.mm(dye, p["w_down"][e], out=da_all.narrow(0, off, n))
             off += n
         dgu_all = ops.swiglu_bwd(da_all, gu_all)  # one launch over every expert's rows
         del da_all
+        if gw:
+            gm.grouped_wgrad(g["w_gate_up"], dgu_all, x, dctx.local_offsets, acc)
         off = 0
         for e, n in enumerate(counts):
             if n:
                 dgu = dgu_all.narrow(0, off, n)
-                grad_mm(g["w_gate_up"][e], dgu.t(), x.narrow(0, off, n), acc)
+                if not gw:
+                    grad_mm(g["w_gate_up"][e], dgu.t(), x.narrow(0, off, n), acc)
                 torch.mm(dgu, p["w_gate_up"][e], out=dx.narrow(0, off, n))
             off += n
         return dx

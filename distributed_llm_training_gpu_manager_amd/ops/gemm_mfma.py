@@ -17,12 +17,15 @@ import torch
 from .._native import hip_ops, use_native
 
 DENSE, GROUP_M, GROUP_K = 0, 1, 2
-# expert GEMMs as grouped launches (DLGM_MOE_GROUPED=1) or the per-expert hipBLASLt loop (default until the
-# grouped kernel outruns hipBLASLt: Mixtral 2-layer A/B 98.4k vs 116.9k tok/s, profiles/mixtral_grouped_ab_r02.json);
-# the grouped weight-gradient mode can be switched off on its own (DLGM_MOE_GROUPED_WGRAD=0)
-GROUPED = os.environ.get("DLGM_MOE_GROUPED", "0") == "1"
-GROUPED_WGRAD = os.environ.get("DLGM_MOE_GROUPED_WGRAD", "1") != "0"
-
+# Expert GEMM strategy (DLGM_MOE_GROUPED): "1" every expert GEMM as one grouped MFMA launch (device offsets,
+# no host read of the routing counts); "wgrad" only the weight gradients grouped (dX / forward per expert
+# through hipBLASLt, which needs the counts on the host once per layer); "0" the per-expert hipBLASLt loop.
+# Default "0": on Mixtral-8x7B (2 layers, seq 4096, GA 4, one MI355X) the loop measured 117.8k tok/s, the
+# grouped dW 111.0k and all-grouped 107.5k (profiles/mixtral_grouped_ab_r02.json): the grouped kernel's
+# 256x256x64 8-phase pipeline reaches 0.9-1.3 PF/s, below hipBLASLt's per-expert solutions.
+_MODE = os.environ.get("DLGM_MOE_GROUPED", "0")
+GROUPED = _MODE == "1"
+GROUPED_WGRAD = _MODE in ("1", "wgrad") and os.environ.get("DLGM_MOE_GROUPED_WGRAD", "1") != "0"
 
 def _ok(t: torch.Tensor) -> bool:
     return t.dtype == torch.bfloat16 and t.data_ptr() % 16 == 0
@@ -46,9 +49,11 @@ def supported(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> bool:
             and out.stride(-1) == 1 and out.stride(0) % 4 == 0 and out.dtype in (torch.float32, torch.bfloat16))
 
 
-def grouped_supported(x: torch.Tensor) -> bool:
-    """Can the grouped kernels take rows `x` (bf16, row-major, 16-B aligned, on the GPU with the extension)?"""
-    return GROUPED and use_native(x) and _ok(x) and x.dim() == 2 and x.stride(1) == 1 and x.stride(0) % 8 == 0
+def grouped_supported(x: torch.Tensor, wgrad: bool = False) -> bool:
+    """Can the grouped kernels take rows `x` (bf16, row-major, 16-B aligned, on the GPU with the extension)?
+    wgrad: asking for the weight-gradient GEMMs only (GROUPED_WGRAD), else for all expert GEMMs (GROUPED)."""
+    on = GROUPED_WGRAD if wgrad else GROUPED
+    return on and use_native(x) and _ok(x) and x.dim() == 2 and x.stride(1) == 1 and x.stride(0) % 8 == 0
 
 
 def mfma_mm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, acc: bool = False) -> torch.Tensor:

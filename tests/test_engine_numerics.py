@@ -72,11 +72,13 @@ def test_mixtral_manual_backward_matches_autograd_gpu():
 
 
 @pytest.mark.gpu
-def test_mixtral_grouped_expert_gemms_match_autograd_gpu(monkeypatch):
-    """Experts as grouped MFMA launches (device offsets from moe_permute, no host read of the counts)."""
+@pytest.mark.parametrize("grouped,wgrad", [(True, True), (False, True), (False, False)])
+def test_mixtral_expert_gemm_modes_match_autograd_gpu(monkeypatch, grouped, wgrad):
+    """Experts as grouped MFMA launches (device offsets from moe_permute, no host read of the counts), the
+    grouped weight gradients only, and the per-expert hipBLASLt loop."""
     from distributed_llm_training_gpu_manager_amd.ops import gemm_mfma as gm
-    monkeypatch.setattr(gm, "GROUPED", True)
-    monkeypatch.setattr(gm, "GROUPED_WGRAD", True)
+    monkeypatch.setattr(gm, "GROUPED", grouped)
+    monkeypatch.setattr(gm, "GROUPED_WGRAD", wgrad)
     _check("cuda", "mixtral-tiny", tol=1e-1)
 
 

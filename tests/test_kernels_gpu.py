@@ -351,3 +351,40 @@ def test_router_topk(E, K):
     assert rel_err(p, p_ref) < 1e-5
     assert torch.equal(i.cpu(), i_ref)
     assert rel_err(g, g_ref) < 1e-5
+
+
+@pytest.mark.parametrize("S", [4096, 8192])
+def test_flash_attention_headline_shape_vs_fp32(S):
+    """The headline shape (Llama-3-8B: Hq=32, Hkv=8, D=128, causal) at S=4096 and 8192: heaviest-first order,
+    XCD remap and deferred rescale on full-length rows, against an fp32 reference built on the GPU per head."""
+    torch.manual_seed(0)
+    B, Hq, Hkv, D = 1, 32, 8, 128
+    g = Hq // Hkv
+    q = torch.randn(B, S, Hq, D, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16)
+    do = torch.randn(B, S, Hq, D, device=DEV, dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    o, lse = ops.flash_attn_fwd(q, k, v, scale, True)
+    dq, dk, dv = ops.flash_attn_bwd(do, q, k, v, o, lse, scale, True)
+    mask = torch.ones(S, S, dtype=torch.bool, device=DEV).triu(1)
+    dk_ref = torch.zeros(S, Hkv, D, device=DEV)
+    dv_ref = torch.zeros(S, Hkv, D, device=DEV)
+    worst = {"o": 0.0, "lse": 0.0, "dq": 0.0}
+    for h in range(Hq):
+        qh = q[0, :, h].float().requires_grad_(True)
+        kh = k[0, :, h // g].float().requires_grad_(True)
+        vh = v[0, :, h // g].float().requires_grad_(True)
+        s = (qh @ kh.t()) * scale
+        s = s.masked_fill(mask, float("-inf"))
+        lse_ref = torch.logsumexp(s, -1)
+        oh = torch.softmax(s, -1) @ vh
+        oh.backward(do[0, :, h].float())
+        worst["o"] = max(worst["o"], rel_err(o[0, :, h], oh.detach()))
+        worst["lse"] = max(worst["lse"], rel_err(lse[0, h], lse_ref.detach()))
+        worst["dq"] = max(worst["dq"], rel_err(dq[0, :, h], qh.grad))
+        dk_ref[:, h // g] += kh.grad
+        dv_ref[:, h // g] += vh.grad
+        del s, oh
+    assert worst["o"] < 2e-2 and worst["lse"] < 1e-3 and worst["dq"] < 3e-2, worst
+    assert rel_err(dk[0], dk_ref) < 3e-2 and rel_err(dv[0], dv_ref) < 3e-2

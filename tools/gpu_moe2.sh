@@ -1,0 +1,8 @@
+#!/bin/bash
+set -o pipefail
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 300 python -u -m pytest tests/test_engine_numerics.py -x -v --timeout 120 --timeout-method thread -k "mixtral" > gpurun_out/moe2_test.log 2>&1 &&
+for m in wgrad 0 1; do
+DLGM_MOE_GROUPED=$m timeout -k 10 400 python -u bench.py --model mixtral-8x7b --n-layers 2 --seq 4096 --ga 4 --steps 6 --warmup 2 --no-telemetry > gpurun_out/bench_mixtral_$m.json 2> gpurun_out/bench_mixtral_$m.err || exit 1
+done
