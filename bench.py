@@ -61,6 +61,7 @@ def main() -> int:
                     help="compute dtype (fp16: the DeepSpeed fp16 path with the dynamic loss scaler)")
     ap.add_argument("--comm-sweep", default="auto", choices=["auto", "on", "off"],
                     help="after the timed steps, measure RCCL busbw over xGMI (auto: when WORLD_SIZE > 1)")
+    ap.add_argument("--comm-sweep-timeout", type=float, default=120.0)
     ap.add_argument("--telemetry-interval", type=float, default=2.0)
     ap.add_argument("--n-layers", type=int, default=0,
                     help="override the preset's layer count (kernel profiling of big models on one GPU only; "
@@ -131,11 +132,6 @@ def main() -> int:
             for i in range(args.profile_steps):
                 eng.train_step(steps_data[args.warmup + args.steps + i])
 
-    comm_rows = None
-    if args.comm_sweep == "on" or (args.comm_sweep == "auto" and env.world > 1):
-        # outside the timed region: the xGMI bus-bandwidth curve of this node at this world size
-        from distributed_llm_training_gpu_manager_amd.utils.commbench import sweep
-        comm_rows = sweep(comm, env.device, sizes_mb=(16, 64, 256) if env.device.type == "cuda" else (1,))
 
     tokens_per_step_gpu = args.mbs * args.seq * args.ga
     total_tokens = tokens_per_step_gpu * env.world * args.steps
@@ -143,6 +139,7 @@ def main() -> int:
     flops_tok = mcfg.flops_per_token(args.seq, recompute=args.ckpt)
     tflops_gpu = tps / env.world * flops_tok / 1e12
     loss = float(m["loss"])
+    out = None
     if env.rank == 0:
         out = {
             "metric": METRIC,
@@ -182,9 +179,29 @@ def main() -> int:
                 "zero3_resident_gathered_params": eng.live_plan.resident_params,
                 "mem": {k: round(v, 1) for k, v in eng.memory_report().items()},
                 "telemetry": telem,
-                "comm_busbw": comm_rows,
+                "comm_busbw": None,
             },
         }
+    if args.comm_sweep == "on" or (args.comm_sweep == "auto" and env.world > 1):
+        # outside the timed region: the xGMI bus-bandwidth curve of this node at this world size (ring
+        # collectives and the direct mesh all-gather). A watchdog on every rank prints the result line
+        # without the curve and ends the process if the sweep stalls, so the measurement is never lost.
+        import threading
+        from distributed_llm_training_gpu_manager_amd.utils.commbench import sweep
+
+        def _stalled():
+            if out is not None:
+                out["extra"]["comm_busbw"] = "sweep timed out"
+                print(json.dumps(out), flush=True)
+            os._exit(0)
+        dog = threading.Timer(args.comm_sweep_timeout, _stalled)
+        dog.daemon = True
+        dog.start()
+        rows = sweep(comm, env.device, sizes_mb=(16, 64, 256) if env.device.type == "cuda" else (1,))
+        dog.cancel()
+        if out is not None:
+            out["extra"]["comm_busbw"] = rows
+    if out is not None:
         print(json.dumps(out), flush=True)
     if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()

@@ -82,6 +82,8 @@ def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, **overri
         cfg.local_grad_accum = mi["local_grad_accum"]
     if "hip_graphs" in mi:
         cfg.hip_graphs = bool(mi["hip_graphs"])
+    if "mesh_allgather" in mi:
+        cfg.mesh_allgather = bool(mi["mesh_allgather"])
     if mi.get("comm_dtype"):
         cfg.comm_dtype = {"fp32": torch.float32, "float32": torch.float32}.get(mi["comm_dtype"], torch.bfloat16)
     for k, v in overrides.items():

@@ -105,6 +105,9 @@ class EngineConfig:
     # the bf16 parameter partition lives in pinned host memory; each gather stages the shard H2D on a side
     # stream and all-gathers from there ("nvme" is served from host memory too)
     offload_param: str = "none"
+    # parameter all-gathers as direct mesh exchanges (batched point-to-point over every xGMI link at once)
+    # instead of RCCL's ring all-gather; opt-in, A/B'd by the bench's post-timing sweep (utils/commbench.py)
+    mesh_allgather: bool = False
     nvme_path: Optional[str] = None
     # ZeRO-2/3 gradients: True = accumulate fp32 locally and reduce-scatter once per optimizer step;
     # False = reduce-scatter every micro-batch (DeepSpeed); "hbm" = True when GA > 1 and the full fp32
@@ -517,6 +520,11 @@ class ZeroEngine:
             return buf, g.gcomm.all_gather(buf, stage, async_op=True)
 
     # ------------------------------------------------------------------ params
+    def _all_gather(self, g: FlatGroup, out: torch.Tensor, shard: torch.Tensor) -> Handle:
+        if self.cfg.mesh_allgather:
+            return g.gcomm.all_gather_mesh(out, shard, async_op=True)
+        return g.gcomm.all_gather(out, shard, async_op=True)
+
     def _shard16(self, g: FlatGroup) -> torch.Tensor:
         return self.p16_shard.narrow(0, g.shard_off, g.shard_numel)
 
@@ -533,7 +541,7 @@ class ZeroEngine:
             self._live[gi] = (self._shard16(g), DONE)
         else:
             buf = torch.empty(g.numel, dtype=self.dtype, device=self.device)
-            self._live[gi] = (buf, g.gcomm.all_gather(buf, self._shard16(g), async_op=True))
+            self._live[gi] = (buf, self._all_gather(g, buf, self._shard16(g)))
 
     def _issue_gathers(self, gis) -> None:
         for gi in gis:
@@ -835,7 +843,7 @@ class ZeroEngine:
         """Recompute the bf16 compute copies from the fp32 master (after restore / external edits)."""
         self._p16_from_master()
         if self.stage in (1, 2):
-            hs = [g.gcomm.all_gather(self.p16_full.narrow(0, g.full_off, g.numel), self._shard16(g), async_op=True)
+            hs = [self._all_gather(g, self.p16_full.narrow(0, g.full_off, g.numel), self._shard16(g))
                   for g in self.groups]
             for h in hs:
                 h.wait()
@@ -910,8 +918,7 @@ class ZeroEngine:
         if self.stage in (1, 2):
             hs = []
             for g in self.groups:
-                hs.append(g.gcomm.all_gather(self.p16_full.narrow(0, g.full_off, g.numel), self._shard16(g),
-                                             async_op=True))
+                hs.append(self._all_gather(g, self.p16_full.narrow(0, g.full_off, g.numel), self._shard16(g)))
             for h in hs:
                 h.wait()
         if self.scaler is not None:

@@ -13,7 +13,7 @@ import torch
 
 from ..parallel.comm import Comm
 
-FACTOR = {"all_gather": lambda w: (w - 1) / w, "reduce_scatter": lambda w: (w - 1) / w,
+FACTOR = {"all_gather": lambda w: (w - 1) / w, "mesh_all_gather": lambda w: (w - 1) / w, "reduce_scatter": lambda w: (w - 1) / w,
           "all_to_all": lambda w: (w - 1) / w, "all_reduce": lambda w: 2 * (w - 1) / w}
 
 
@@ -25,6 +25,10 @@ def run(op: str, comm: Comm, nbytes: int, device, dtype, iters: int, warmup: int
         inp = torch.randn(n // W, device=device).to(dtype)
         out = torch.empty(n, device=device, dtype=dtype)
         fn = lambda: comm.all_gather(out, inp, async_op=False)  # noqa: E731
+    elif op == "mesh_all_gather":
+        inp = torch.randn(n // W, device=device).to(dtype)
+        out = torch.empty(n, device=device, dtype=dtype)
+        fn = lambda: comm.all_gather_mesh(out, inp, async_op=True)  # noqa: E731
     elif op == "reduce_scatter":
         inp = torch.randn(n, device=device).to(dtype)
         out = torch.empty(n // W, device=device, dtype=dtype)
@@ -54,7 +58,8 @@ def run(op: str, comm: Comm, nbytes: int, device, dtype, iters: int, warmup: int
 
 
 
-def sweep(comm: Comm, device, ops: Sequence[str] = ("all_gather", "reduce_scatter", "all_reduce", "all_to_all"),
+def sweep(comm: Comm, device,
+          ops: Sequence[str] = ("all_gather", "mesh_all_gather", "reduce_scatter", "all_reduce", "all_to_all"),
           sizes_mb: Sequence[float] = (16, 64, 256), dtype=torch.bfloat16, iters: int = 5,
           warmup: int = 2) -> List[Dict]:
     rows = []

@@ -59,4 +59,4 @@ def test_bench_torchrun_two_ranks():
     _check(out, 2, 2, 1)
     assert out["extra"]["zero3_allgathers_per_step"] > 0  # partitioned: the residency plan gathers once per unit
     ops = {r["op"] for r in out["extra"]["comm_busbw"]}  # the post-timing RCCL/xGMI sweep (gloo here)
-    assert ops == {"all_gather", "reduce_scatter", "all_reduce", "all_to_all"}
+    assert ops == {"all_gather", "mesh_all_gather", "reduce_scatter", "all_reduce", "all_to_all"}
