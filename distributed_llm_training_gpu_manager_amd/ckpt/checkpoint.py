@@ -451,6 +451,7 @@ class AsyncCheckpointer:
         when all ranks hold the same newest step, else the disk tags newest first; a candidate that fails
         on any rank is rolled back on all of them (recorded in ``self.rollbacks``)."""
         self.rollbacks = []
+        self.restore_stats: Dict[str, Any] = {}
         agree = _Agree(self.engine)
         auto = tag in ("auto", "latest")
         disk = list(reversed(complete_tags(self.save_dir))) if auto else [tag]
@@ -465,12 +466,19 @@ class AsyncCheckpointer:
         for kind, t in cands:
             err = ""
             cs: Optional[Dict[str, Any]] = None
+            t0 = time.time()
             try:
                 cs = self._load_shm() if kind == "shm" else self._load_tag(t, verify)
             except (CorruptCheckpoint, FileNotFoundError, OSError, KeyError, ValueError, RuntimeError) as e:
                 err = f"{type(e).__name__}: {e}"
+            t1 = time.time()
             if agree.min(0.0 if err else 1.0) > 0:
+                t2 = time.time()
                 self.engine.sync_params_from_master()
+                if self.cuda:
+                    torch.cuda.synchronize(self.dev)
+                self.restore_stats.update(read_s=round(t1 - t0, 2), agree_s=round(t2 - t1, 2),
+                                          params_s=round(time.time() - t2, 2))
                 self.restored_from = f"{kind}:{t}"
                 return cs
             self.rollbacks.append(f"{kind}:{t}: {err or 'failed on another rank'}")
@@ -493,7 +501,10 @@ class AsyncCheckpointer:
         end = 12 * n  # the bf16 copy after the fp32 state is recomputed from the master, not read
         piece = max(_host.CHUNK, self.ring_elems * 4)
         check = m["algo"] == _host.algo()
+        ta = time.time()
         slots = [torch.empty(piece, dtype=torch.uint8, pin_memory=self.cuda) for _ in range(2)]
+        self.restore_stats["pin_s"] = round(time.time() - ta, 2)
+        waited = [0.0, 0.0]  # [main thread waiting for a read, waiting for an H2D]
         evs: List[Any] = [None, None]
         jobs = [(k, off, min(piece, end - off)) for k, off in enumerate(range(0, end, piece))]
         q: "queue.Queue" = queue.Queue(maxsize=1)
@@ -509,7 +520,9 @@ class AsyncCheckpointer:
         th = threading.Thread(target=reader, daemon=True)
         th.start()
         for _ in jobs:
+            tw = time.time()
             item = q.get()
+            waited[0] += time.time() - tw
             if isinstance(item, Exception):
                 raise item
             k, off, ln, crcs = item
@@ -524,9 +537,13 @@ class AsyncCheckpointer:
             if self.cuda:
                 ev = torch.cuda.Event()
                 ev.record()
+                tw = time.time()
                 ev.synchronize()
+                waited[1] += time.time() - tw
             free[k % 2].release()
         th.join()
+        self.restore_stats.update(wait_read_s=round(waited[0], 2), wait_h2d_s=round(waited[1], 2),
+                                  pieces=len(jobs), piece_MiB=piece >> 20, GiB=round(end / 2 ** 30, 1))
         if check and end % _host.CHUNK:  # the chunk straddling the fp32/bf16 boundary: verify it whole
             tail = torch.empty(min(_host.CHUNK, m["bytes"] - (end // _host.CHUNK) * _host.CHUNK), dtype=torch.uint8)
             c = read_slot(self.shm_src_path, tail, (end // _host.CHUNK) * _host.CHUNK)

@@ -253,7 +253,8 @@ class Trainer:
             if cs is not None:
                 start = int(cs.get("step", self.engine.step_count))
                 self._say(f"resumed from step {start} in {time.time() - t0:.2f}s via {self.ckpt.restored_from} "
-                          f"(rollbacks: {getattr(self.ckpt, 'rollbacks', [])})")
+                          f"(rollbacks: {getattr(self.ckpt, 'rollbacks', [])}; "
+                          f"restore {json.dumps(getattr(self.ckpt, 'restore_stats', {}))})")
                 self.monitor.reset()
         if self.ckpt is not None:
             self.ckpt.prepare_async()  # snapshot buffer allocated / page-locked while the first steps run

@@ -65,12 +65,14 @@ def drill_sigkill(a, work):
     log = open(job.log_path).read()
     resumed = re.findall(r"resumed from step (\d+) in ([0-9.]+)s", log)
     via = re.findall(r"resumed from step \d+ in [0-9.]+s via (\S+)", log)
+    stats = [json.loads(x) for x in re.findall(r"restore (\{.*?\})\)", log)]
     hist = {}
     if os.path.exists(os.path.join(work, "kill.json")):
         hist = json.load(open(os.path.join(work, "kill.json"))).get("ckpt", [])
     return {"drill": "sigkill", "status": job.status, "exit_codes": job.exit_codes, "restarts": job.restarts,
             "mttr_s": [round(x, 2) for x in job.mttr_s], "resume_load_s": [float(s) for _, s in resumed],
-            "resumed_from_step": [int(s) for s, _ in resumed], "restored_from": via, "events": job.events,
+            "resumed_from_step": [int(s) for s, _ in resumed], "restored_from": via, "restore_breakdown": stats,
+            "events": job.events,
             "ckpt_after_resume": hist,
             "tail": log[-800:]}
 
@@ -83,7 +85,8 @@ def drill_spot(a, work):
     rc2, out2, dt2 = run(train_argv(a, ["--steps", str(a.k + 1), "--save-dir", ck, "--resume", "auto"]), a.timeout)
     res = re.findall(r"resumed from step (\d+) in ([0-9.]+)s", out2)
     via = re.findall(r"resumed from step \d+ in [0-9.]+s via (\S+)", out2)
-    return {"drill": "spot", "exit_code_preempted": rc, "emergency_ckpt": em, "restore_exit": rc2,
+    stats = re.findall(r"restore (\{.*?\})\)", out2)
+    return {"drill": "spot", "restore_breakdown": [json.loads(x) for x in stats], "exit_code_preempted": rc, "emergency_ckpt": em, "restore_exit": rc2,
             "restore": res, "restored_from": via, "restore_process_wall_s": round(dt2, 2),
             "tail": (out[-300:], out2[-300:])}
 
