@@ -62,6 +62,8 @@ def main() -> int:
     ap.add_argument("--comm-sweep", default="auto", choices=["auto", "on", "off"],
                     help="after the timed steps, measure RCCL busbw over xGMI (auto: when WORLD_SIZE > 1)")
     ap.add_argument("--comm-sweep-timeout", type=float, default=120.0)
+    ap.add_argument("--defer-expert-wgrad", default="auto", choices=["auto", "on", "off"],
+                    help="MoE: expert dW once per step over the concatenated micro-batches")
     ap.add_argument("--telemetry-interval", type=float, default=2.0)
     ap.add_argument("--n-layers", type=int, default=0,
                     help="override the preset's layer count (kernel profiling of big models on one GPU only; "
@@ -85,7 +87,8 @@ def main() -> int:
                         activation_checkpointing=args.ckpt, max_live_parameters=_knob(args.live_params),
                         max_reuse_distance=_knob(args.reuse_distance),
                         local_grad_accum={"on": True, "off": False}.get(args.local_grads, args.local_grads),
-                        hip_graphs=args.hip_graphs, fp16=args.dtype == "fp16")
+                        hip_graphs=args.hip_graphs, fp16=args.dtype == "fp16",
+                        defer_expert_wgrad={"on": True, "off": False}.get(args.defer_expert_wgrad, "auto"))
     t0 = time.time()
     eng = ZeroEngine(mcfg, ecfg, env.device, comm)
     if env.device.type == "cuda":

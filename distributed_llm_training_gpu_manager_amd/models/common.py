@@ -58,6 +58,11 @@ class StepContext:
     sp_group: Any = None  # sequence-parallel Comm (parallel/sp.py): seq_len is then the LOCAL chunk
     aux: Dict[str, Any] = field(default_factory=dict)
     grad_acc: bool = False  # backward ADDS into the gradient views (later micro-batch / tied second visit)
+    micro_index: int = 0  # position of this micro-batch in the optimizer step
+    last_micro: bool = True
+    # units may keep weight-gradient operands across the step's micro-batches and run ONE GEMM with the
+    # micro-batches concatenated along K at the last one (their gradients go straight to fp32 targets)
+    defer_wgrad: bool = False
 
     @property
     def tokens(self) -> int:

@@ -112,7 +112,7 @@ class MixtralBlock(LlamaBlock):
             off += n
         return y, (gu_all, a_all, dctx)
 
-    def _experts_bwd(self, p: Params, g: Params, x: torch.Tensor, dy: torch.Tensor, saved, acc: bool):
+    def _experts_bwd(self, p: Params, g: Params, x: torch.Tensor, dy: torch.Tensor, saved, acc: bool, ctx=None):
         gu_all, a_all, dctx = saved
         if self._grouped(x):
             offs = dctx.local_offsets
@@ -124,6 +124,8 @@ class MixtralBlock(LlamaBlock):
             gm.grouped_wgrad(g["w_gate_up"], dgu_all, x, offs, acc)
             return gm.grouped_mm(dgu_all, p["w_gate_up"], offs, transpose_w=False)
         counts = dctx.counts()
+        if ctx is not None and ctx.defer_wgrad:
+            return self._experts_bwd_deferred(p, g, x, dy, saved, counts, ctx)
         # weight gradients as grouped launches (reduction over each expert's token rows, device offsets)
         gw = self._grouped(x, wgrad=True) and dctx.local_offsets is not None
         dy = dy.contiguous() if gw else dy
@@ -157,6 +159,59 @@ class MixtralBlock(LlamaBlock):
             off += n
         return dx
 
+    def _experts_bwd_deferred(self, p: Params, g: Params, x: torch.Tensor, dy: torch.Tensor, saved, counts,
+                              ctx) -> torch.Tensor:
+        """Input gradients now, weight gradients once per step: this micro-batch's (dY, A, dGU, X) rows are
+        kept and, at the step's last micro-batch (or when the stash budget is reached), every expert's dW is
+        ONE GEMM over its rows of all kept micro-batches (K = their token count). Per-expert dW at ~1k
+        tokens is bound by the fp32 read-modify-write of the gradient (0.7 GB per expert); concatenating the
+        micro-batches pays it once per step (reference: DeepSpeed accumulates per micro-batch)."""
+        gu_all, a_all, _ = saved
+        if ctx.micro_index == 0:
+            self._wstash, self._wflushed, self._wbytes = [], False, 0
+        dx = torch.empty_like(x)
+        da_all = torch.empty_like(a_all)
+        off = 0
+        for e, n in enumerate(counts):
+            if n:
+                torch.mm(dy.narrow(0, off, n), p["w_down"][e], out=da_all.narrow(0, off, n))
+            off += n
+        dgu_all = ops.swiglu_bwd(da_all, gu_all)
+        del da_all
+        off = 0
+        for e, n in enumerate(counts):
+            if n:
+                torch.mm(dgu_all.narrow(0, off, n), p["w_gate_up"][e], out=dx.narrow(0, off, n))
+            off += n
+        self._wstash.append((dy, a_all, dgu_all, x, list(counts)))
+        self._wbytes += sum(t.numel() * t.element_size() for t in (dy, a_all, dgu_all, x))
+        budget = getattr(ctx, "defer_budget_bytes", 48 << 30)
+        if ctx.last_micro or self._wbytes > budget:
+            self._flush_wgrad(g)
+        return dx
+
+    def _flush_wgrad(self, g: Params) -> None:
+        stash, acc = self._wstash, self._wflushed
+        for e in range(self.E_local):
+            parts = []
+            for dy, a, dgu, x, cnt in stash:
+                lo, n = sum(cnt[:e]), cnt[e]
+                if n:
+                    parts.append((dy.narrow(0, lo, n), a.narrow(0, lo, n), dgu.narrow(0, lo, n), x.narrow(0, lo, n)))
+            if not parts:
+                if not acc:
+                    g["w_down"][e].zero_()
+                    g["w_gate_up"][e].zero_()
+                continue
+            cat = (lambda i: parts[0][i]) if len(parts) == 1 else (lambda i: torch.cat([q[i] for q in parts]))
+            dye, ae = cat(0), cat(1)
+            grad_mm(g["w_down"][e], dye.t(), ae, acc)
+            del dye, ae
+            dgue, xe = cat(2), cat(3)
+            grad_mm(g["w_gate_up"][e], dgue.t(), xe, acc)
+            del dgue, xe
+        self._wstash, self._wflushed, self._wbytes = [], True, 0
+
     def moe_backward(self, p: Params, g: Params, hn2: torch.Tensor, saved, dout: torch.Tensor, ctx: StepContext):
         c = self.cfg
         probs, topi, gates, pos, f, x_local, dctx, exp_saved, y_sorted = saved
@@ -164,7 +219,7 @@ class MixtralBlock(LlamaBlock):
         disp = self.dispatcher(ctx)
         dy_sorted, dgates = moe_combine_bwd(dout.contiguous(), y_sorted, pos, gates)
         dy_local = disp.redispatch(dy_sorted, dctx)
-        dx_local = self._experts_bwd(p, g, x_local, dy_local, exp_saved, ctx.grad_acc)
+        dx_local = self._experts_bwd(p, g, x_local, dy_local, exp_saved, ctx.grad_acc, ctx)
         dx_sorted = disp.combine(dx_local, dctx)
         dhn2 = moe_combine(dx_sorted, pos, None)  # adjoint of the dispatch gather: sum the K slots per token
         dtop = gates * (dgates - (gates * dgates).sum(-1, keepdim=True))

@@ -108,6 +108,12 @@ class EngineConfig:
     # parameter all-gathers as direct mesh exchanges (batched point-to-point over every xGMI link at once)
     # instead of RCCL's ring all-gather; opt-in, A/B'd by the bench's post-timing sweep (utils/commbench.py)
     mesh_allgather: bool = False
+    # expert weight gradients: keep each micro-batch's (dY, X) per expert and run one dW GEMM per expert over
+    # the concatenated micro-batches at the last one (K = GA x tokens: the fp32 gradient is read and written
+    # once per step instead of once per micro-batch). Only with direct fp32 gradient targets; "auto" = on
+    # when grad_accum > 1. Stashed operands are capped by defer_wgrad_budget_gb (flushed early above it).
+    defer_expert_wgrad: Any = "auto"
+    defer_wgrad_budget_gb: float = 48.0
     nvme_path: Optional[str] = None
     # ZeRO-2/3 gradients: True = accumulate fp32 locally and reduce-scatter once per optimizer step;
     # False = reduce-scatter every micro-batch (DeepSpeed); "hbm" = True when GA > 1 and the full fp32
@@ -751,6 +757,12 @@ class ZeroEngine:
 
     def micro_step(self, ids: torch.Tensor, labels: torch.Tensor, first: bool, last: bool) -> torch.Tensor:
         ctx = self._context(ids, labels)
+        self._micro = 0 if first else getattr(self, "_micro", 0) + 1
+        ctx.micro_index, ctx.last_micro = self._micro, last
+        dw = self.cfg.defer_expert_wgrad
+        ctx.defer_wgrad = bool((dw == "auto" and self.cfg.grad_accum > 1) or dw is True) and all(
+            self._direct_target(g) is not None for g in self.groups if g.kind == "expert")
+        ctx.defer_budget_bytes = int(self.cfg.defer_wgrad_budget_gb * (1 << 30))
         n = len(self.stages)
         saved: List[Any] = [None] * n
         x: Any = None

@@ -252,3 +252,24 @@ def test_packed_qkv_attention_matches_fp32_reference(device, hq, hkv, d):
     assert float((out.float().cpu() - ref).abs().max()) < 3e-2
     err = float((x.grad.float().cpu() - r.grad).abs().max() / r.grad.abs().max())
     assert err < 3e-2, err
+
+
+@pytest.mark.parametrize("budget_gb", [48.0, 1e-6])
+def test_mixtral_deferred_expert_wgrad_matches_per_micro_batch(budget_gb):
+    """Expert dW over the step's concatenated micro-batches (and, with a tiny stash budget, flushed every
+    micro-batch) equals the per-micro-batch accumulation."""
+    mc = get_config("mixtral-tiny", router_aux_coef=0.0)
+    g = torch.Generator().manual_seed(5)
+    mbs = [(t[:, :-1], t[:, 1:]) for t in (torch.randint(0, mc.vocab_size, (2, 33), generator=g) for _ in range(3))]
+    grads = {}
+    for defer in (False, True):
+        ec = EngineConfig(zero_stage=3, micro_batch_size=2, seq_len=32, grad_accum=3, lr=1e-3,
+                          scheduler="constant", init_device="cpu", grad_clip=0.0, defer_expert_wgrad=defer,
+                          defer_wgrad_budget_gb=budget_gb)
+        eng = ZeroEngine(mc, ec, torch.device("cpu"))
+        for i, (ids, lab) in enumerate(mbs):
+            eng.micro_step(ids, lab, first=i == 0, last=i == 2)
+        grads[defer] = _engine_grads(eng)
+    for k, v in grads[False].items():
+        err = float((grads[True][k] - v).abs().max() / v.abs().max().clamp_min(1e-8))
+        assert err < 1e-5, (k, err)
