@@ -180,18 +180,52 @@ class LlamaHead(Unit):
         return [ParamSpec("norm", (c.d_model,), init="ones", weight_decay=False),
                 ParamSpec("lm_head", (c.vocab_size, c.d_model), std=c.init_std, tcache=True)]
 
+    # [T, V] 16-bit logits above this many bytes are never materialised whole: the forward computes the loss
+    # chunk by chunk (CE without gradient) and the backward recomputes each chunk's logits, turns them into
+    # dlogits in place and runs that chunk's dX / dW GEMMs (one extra logits GEMM for micro-batches whose
+    # logits alone would take more than the budget, e.g. mbs 4 x 8192 tokens x 128k vocab = 8.4 GB)
+    logits_budget_bytes = 6 << 30
+    chunk_tokens = 8192
+
+    def _chunked(self, T: int) -> bool:
+        return T * self.cfg.vocab_size * 2 > self.logits_budget_bytes and T > self.chunk_tokens
+
     def forward(self, p: Params, x_pair, ctx: StepContext):
         c = self.cfg
         xa, xb = _as_pair(x_pair)
         hn, x, rstd = ops.rmsnorm_fwd(xa, p["norm"], c.norm_eps, residual=xb)
-        logits = mm(hn, p["lm_head"].t())
         labels = ctx.labels.reshape(-1)
+        T = hn.shape[0]
+        if self._chunked(T):
+            loss = torch.zeros((), dtype=torch.float32, device=hn.device)
+            for lo in range(0, T, self.chunk_tokens):
+                n = min(self.chunk_tokens, T - lo)
+                logits = mm(hn.narrow(0, lo, n), p["lm_head"].t())
+                rows, _ = ops.cross_entropy_fwd_bwd_(logits, labels.narrow(0, lo, n), ctx.grad_scale,
+                                                    compute_grad=False)
+                loss += rows.sum()
+                del logits
+            return loss, (x, rstd, hn, None)
+        logits = mm(hn, p["lm_head"].t())
         loss_rows, _ = ops.cross_entropy_fwd_bwd_(logits, labels, ctx.grad_scale)
         # logits now hold d(loss)/d(logits); keep them for backward
         return loss_rows.sum(), (x, rstd, hn, logits)
 
     def backward(self, p: Params, g: Params, saved, dy, ctx: StepContext):
         x, rstd, hn, dlogits = saved
+        if dlogits is None:  # chunked head: recompute each chunk's logits -> dlogits -> its dW / dX share
+            labels = ctx.labels.reshape(-1)
+            T = hn.shape[0]
+            dhn = torch.empty_like(hn)
+            for i, lo in enumerate(range(0, T, self.chunk_tokens)):
+                n = min(self.chunk_tokens, T - lo)
+                hc = hn.narrow(0, lo, n)
+                dl = mm(hc, p["lm_head"].t())
+                ops.cross_entropy_fwd_bwd_(dl, labels.narrow(0, lo, n), ctx.grad_scale)
+                grad_mm(g["lm_head"], dl.t(), hc, ctx.grad_acc or i > 0)
+                dhn.narrow(0, lo, n).copy_(dx_mm(dl, p, "lm_head"))
+                del dl
+            return ops.rmsnorm_bwd(dhn, x, p["norm"], rstd, g["norm"], accumulate_dw=ctx.grad_acc)
         grad_mm(g["lm_head"], dlogits.t(), hn, ctx.grad_acc)
         dhn = dx_mm(dlogits, p, "lm_head")
         return ops.rmsnorm_bwd(dhn, x, p["norm"], rstd, g["norm"], accumulate_dw=ctx.grad_acc)

@@ -273,3 +273,33 @@ def test_mixtral_deferred_expert_wgrad_matches_per_micro_batch(budget_gb):
     for k, v in grads[False].items():
         err = float((grads[True][k] - v).abs().max() / v.abs().max().clamp_min(1e-8))
         assert err < 1e-5, (k, err)
+
+
+def test_llama_head_chunked_logits_match_whole(monkeypatch):
+    """A micro-batch whose [T, V] logits exceed the budget runs the LM head + cross-entropy in token chunks
+    (loss in the forward, logits recomputed per chunk in the backward): same loss and gradients."""
+    from distributed_llm_training_gpu_manager_amd.models.llama import LlamaHead
+    mc = get_config("llama-tiny")
+    g = torch.Generator().manual_seed(7)
+    mbs = [(t[:, :-1], t[:, 1:]) for t in (torch.randint(0, mc.vocab_size, (2, 65), generator=g) for _ in range(2))]
+    res = {}
+    for chunked in (False, True):
+        monkeypatch.setattr(LlamaHead, "logits_budget_bytes", 1 if chunked else 6 << 30)
+        monkeypatch.setattr(LlamaHead, "chunk_tokens", 48)  # 128 tokens -> chunks of 48, 48, 32
+        ec = EngineConfig(zero_stage=3, micro_batch_size=2, seq_len=64, grad_accum=2, lr=1e-3,
+                          scheduler="constant", init_device="cpu", grad_clip=0.0)
+        eng = ZeroEngine(mc, ec, torch.device("cpu"))
+        loss = sum(float(eng.micro_step(ids, lab, first=i == 0, last=i == 1)) for i, (ids, lab) in enumerate(mbs))
+        res[chunked] = (loss, _engine_grads(eng))
+    assert abs(res[True][0] - res[False][0]) < 1e-4 * abs(res[False][0])
+    for k, v in res[False][1].items():
+        err = float((res[True][1][k] - v).abs().max() / v.abs().max().clamp_min(1e-8))
+        assert err < 1e-4, (k, err)
+
+
+@pytest.mark.gpu
+def test_llama_chunked_head_matches_autograd_gpu(monkeypatch):
+    from distributed_llm_training_gpu_manager_amd.models.llama import LlamaHead
+    monkeypatch.setattr(LlamaHead, "logits_budget_bytes", 1)
+    monkeypatch.setattr(LlamaHead, "chunk_tokens", 48)
+    _check("cuda")
