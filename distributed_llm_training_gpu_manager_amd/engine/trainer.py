@@ -164,6 +164,7 @@ class Trainer:
         signal.signal(signal.SIGUSR1, self._on_preempt)
         signal.signal(signal.SIGTERM, self._on_preempt)
         self.log: List[Dict[str, Any]] = []
+        self.read_behind = 0  # step reports read while the next step was already queued
 
     def _on_preempt(self, signum, frame) -> None:
         self.preempt = True
@@ -282,6 +283,7 @@ class Trainer:
             last = step
             # step t-1's outcome, read while step t runs on the device
             if prev is not None:
+                self.read_behind += 1  # read with a later step already queued behind it
                 stop = self._decide(self._report(*prev), step)
                 prev = None
                 if stop is not None:

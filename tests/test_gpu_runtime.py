@@ -85,8 +85,10 @@ def test_trainer_runs_ahead_and_nan_latch_keeps_pre_nan_state(tmp_path):
 
     ok = _trainer(tmp_path, "--steps", "8")
     assert ok.run() == 0
-    # the report of step t-1 was read while step t was still queued/running on the GPU
-    assert ok.trap.waited >= 4, ok.trap.waited
+    # every report but the last was read with the next step already queued (the host never drains the GPU
+    # to decide), and at least some of those reads found their step still running on the device
+    assert ok.read_behind == 7, ok.read_behind
+    assert ok.trap.waited >= 1, ok.trap.waited
     ref = _trainer(tmp_path, "--steps", "2")
     assert ref.run() == 0
     bad = _trainer(tmp_path, "--steps", "8", "--inject-nan-step", "3")
