@@ -114,6 +114,7 @@ def plan_rank(m: ModelConfig, *, world: int, zero_stage: int = 3, micro_batch: i
               local_grad_accum="hbm", local_grad_hbm_fraction: float = 0.15, max_live_parameters="hbm",
               max_reuse_distance="hbm", live_hbm_fraction: float = 0.12, prefetch_bucket_size: float = 5e8,
               transposed_weight_cache: bool = True, tcache_hbm_fraction: float = 0.08,
+              defer_expert_wgrad="auto", defer_wgrad_budget_gb: float = 48.0,
               offload_optimizer: str = "none", offload_param: str = "none",
               hbm_bytes: float = MI355X_HBM, headroom: float = 0.10) -> RankPlan:
     from .residency import ResidencyPlan, resolve_limit
@@ -157,6 +158,14 @@ def plan_rank(m: ModelConfig, *, world: int, zero_stage: int = 3, micro_batch: i
         big = max(g.numel for g in groups if g.P > 1)
         parts["grad_reduce_scratch"] = 2.0 * 2 * big * (1 + 1.0 / world)
     parts.update(_activation_bytes(m, micro_batch * seq_len, seq_len, activation_checkpointing, ep))
+    direct = zero_stage in (0, 1) or local or world == 1
+    if m.n_experts and grad_accum > 1 and direct and defer_expert_wgrad in ("auto", True):
+        # deferred expert dW (models/mixtral.py): (dY, A, dGU, X) rows of earlier micro-batches, capped
+        # + the flush transients (the current micro-batch's rows held to the flush, the per-expert
+        # concatenations): 0.45 of one micro-batch's stash, calibrated on the Mixtral EP=8 shadow rank
+        R = micro_batch * seq_len * m.top_k
+        per = 2.0 * R * (2 * m.d_model + 3 * m.ffn_dim) * m.n_layers
+        parts["moe_wgrad_stash"] = min((grad_accum - 1) * per, defer_wgrad_budget_gb * GiB) + 0.45 * per
     st = [tuple(gi) if isinstance(gi, (tuple, list)) else (gi,) for _, gi in stages]
     gathered = [zero_stage == 3 and g.P > 1 for g in groups]
     stage_sz = [sum(groups[gi].numel for gi in s if gathered[gi]) for s in st]
