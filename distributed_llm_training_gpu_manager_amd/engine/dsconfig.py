@@ -13,11 +13,16 @@ import torch
 from ..parallel.zero import EngineConfig
 
 
-def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, **overrides) -> Tuple[EngineConfig, List[str]]:
+def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, model_cfg=None, world: int = 1,
+                          **overrides) -> Tuple[EngineConfig, List[str]]:
+    """``model_cfg`` / ``world``: needed only to resolve ``"train_micro_batch_size_per_gpu": "auto"`` (or
+    the ``mi355x.auto_micro_batch`` switch) through the per-rank HBM planner."""
     if isinstance(ds, str):
         with open(ds) as f:
             ds = json.load(f)
     notes: List[str] = []
+    mi = ds.get("mi355x") or {}
+    auto_mbs = ds.get("train_micro_batch_size_per_gpu") == "auto" or bool(mi.get("auto_micro_batch", False))
     zo = ds.get("zero_optimization", {})
     opt = ds.get("optimizer", {}).get("params", {})
     sch = ds.get("scheduler", {})
@@ -37,7 +42,7 @@ def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, **overri
     act = ds.get("activation_checkpointing")
     cfg = EngineConfig(
         zero_stage=int(zo.get("stage", 0)),
-        micro_batch_size=int(ds.get("train_micro_batch_size_per_gpu", 1)),
+        micro_batch_size=1 if auto_mbs else int(ds.get("train_micro_batch_size_per_gpu", 1)),
         seq_len=seq_len,
         grad_accum=int(ds.get("gradient_accumulation_steps", 1)),
         lr=float(opt.get("lr", sp.get("warmup_max_lr", 3e-5))),
@@ -75,7 +80,6 @@ def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, **overri
         offload_param=off_p,
     )
     # engine knobs without a DeepSpeed key travel in the "mi355x" block (launcher.config.MI355XOptions)
-    mi = ds.get("mi355x") or {}
     cfg.expert_parallel_size = int(mi.get("expert_parallel_size", cfg.expert_parallel_size))
     cfg.sequence_parallel_size = int(mi.get("sequence_parallel_size", cfg.sequence_parallel_size))
     if "local_grad_accum" in mi:
@@ -86,6 +90,34 @@ def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, **overri
         cfg.mesh_allgather = bool(mi["mesh_allgather"])
     if mi.get("comm_dtype"):
         cfg.comm_dtype = {"fp32": torch.float32, "float32": torch.float32}.get(mi["comm_dtype"], torch.bfloat16)
+    if auto_mbs:
+        _auto_micro_batch(cfg, ds, model_cfg, world, notes)
     for k, v in overrides.items():
         setattr(cfg, k, v)
     return cfg, notes
+
+
+def _auto_micro_batch(cfg: EngineConfig, ds: Dict[str, Any], model_cfg, world: int, notes: List[str]) -> None:
+    """Resolve the micro-batch (and gradient accumulation, activation checkpointing) from the planner,
+    keeping the global batch: ``train_batch_size`` if given, else the configured mbs x GA x world."""
+    if model_cfg is None:
+        notes.append("train_micro_batch_size_per_gpu=auto needs the model: micro-batch 1")
+        return
+    from ..parallel.planner import auto_micro_batch
+
+    mbs = ds.get("train_micro_batch_size_per_gpu")
+    mbs = int(mbs) if isinstance(mbs, (int, float)) else 1
+    sp = max(1, cfg.sequence_parallel_size)
+    dp = max(1, world // sp)
+    gb = ds.get("train_batch_size")
+    gb = int(gb) if isinstance(gb, (int, float)) else mbs * cfg.grad_accum * dp
+    ch = auto_micro_batch(model_cfg, world=world, data_parallel=dp, seq_len=cfg.seq_len // sp, global_batch=gb,
+                          zero_stage=cfg.zero_stage,
+                          ep_size=cfg.expert_parallel_size, offload_optimizer=cfg.offload_optimizer,
+                          offload_param=cfg.offload_param, force_checkpointing=cfg.activation_checkpointing,
+                          allow_checkpointing=True)
+    cfg.micro_batch_size, cfg.grad_accum = ch.micro_batch, ch.grad_accum
+    cfg.activation_checkpointing = ch.activation_checkpointing
+    notes.append(f"auto micro-batch: {ch.micro_batch} x GA {ch.grad_accum} x {dp} ranks = {gb} sequences/step, "
+                 f"checkpointing {'on' if ch.activation_checkpointing else 'off'}, planned "
+                 f"{ch.plan.total / 2**30:.1f} GiB/rank (headroom {ch.plan.headroom:.0%})")

@@ -119,13 +119,18 @@ class Trainer:
             over["n_layers"] = args.n_layers  # drills on a box: the named architecture, fewer blocks
         self.mcfg = get_config(args.model, **over)
         if args.deepspeed_config:
-            self.ecfg, self.notes = engine_config_from_ds(args.deepspeed_config, args.seq_len, seed=args.seed)
+            self.ecfg, self.notes = engine_config_from_ds(args.deepspeed_config, args.seq_len, seed=args.seed,
+                                                          model_cfg=self.mcfg, world=self.env.world)
             with open(args.deepspeed_config) as f:
                 self._ds_elastic = bool(json.load(f).get("elasticity", {}).get("enabled", False))
         else:
             self.ecfg, self.notes = EngineConfig(zero_stage=args.zero_stage, micro_batch_size=args.micro_batch,
                                                  seq_len=args.seq_len, grad_accum=args.grad_accum, lr=args.lr,
                                                  seed=args.seed, fp16=getattr(args, "fp16", False)), []
+        if getattr(args, "auto_micro_batch", False) and not args.deepspeed_config:
+            from .dsconfig import _auto_micro_batch
+            _auto_micro_batch(self.ecfg, {"train_micro_batch_size_per_gpu": args.micro_batch}, self.mcfg,
+                              self.env.world, self.notes)
         if args.lr_scale != 1.0:
             self.ecfg.lr *= args.lr_scale
         if getattr(args, "expert_parallel", 0):
@@ -369,6 +374,8 @@ def parse_args(argv=None) -> argparse.Namespace:
                     help="fp16 compute with the dynamic loss scaler (without a DeepSpeed config; else its fp16 block)")
     ap.add_argument("--micro-batch", type=int, default=1)
     ap.add_argument("--grad-accum", type=int, default=1)
+    ap.add_argument("--auto-micro-batch", action="store_true",
+                    help="size the micro-batch to the per-rank HBM plan (keeps micro-batch x grad-accum x world)")
     ap.add_argument("--lr", type=float, default=3e-4)
     ap.add_argument("--lr-scale", type=float, default=1.0)
     ap.add_argument("--seed", type=int, default=1234)

@@ -59,6 +59,8 @@ class MI355XOptions(BaseModel):
         default="hbm", description="ZeRO-2/3: fp32 grads accumulate locally, one reduce-scatter per step ('hbm': if they fit)")
     hip_graphs: bool = Field(default=False, description="replay the micro-batch loop as one captured HIP graph "
                              "(single rank, dense models)")
+    auto_micro_batch: bool = Field(default=False, description="size the micro-batch (and GA, activation "
+                                   "checkpointing) to the per-rank HBM plan, keeping the global batch")
 
 
 class DeepSpeedConfig(BaseModel):

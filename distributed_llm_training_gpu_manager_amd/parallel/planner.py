@@ -206,6 +206,56 @@ def plan_rank(m: ModelConfig, *, world: int, zero_stage: int = 3, micro_batch: i
     return plan
 
 
+@dataclass
+class MicroBatchChoice:
+    micro_batch: int
+    grad_accum: int
+    activation_checkpointing: bool
+    plan: RankPlan
+    tried: List[Dict[str, object]] = field(default_factory=list)
+
+    def summary(self) -> Dict[str, object]:
+        return {"micro_batch": self.micro_batch, "grad_accum": self.grad_accum,
+                "activation_checkpointing": self.activation_checkpointing,
+                "total_GiB": round(self.plan.total / GiB, 2), "headroom": round(self.plan.headroom, 4),
+                "tried": self.tried}
+
+
+def auto_micro_batch(m: ModelConfig, *, world: int, seq_len: int, global_batch: Optional[int] = None,
+                     grad_accum: int = 8, max_micro: int = 64, allow_checkpointing: bool = True,
+                     force_checkpointing: bool = False, min_headroom: float = 0.10,
+                     data_parallel: Optional[int] = None, **plan_kw) -> MicroBatchChoice:
+    """Micro-batch auto-sizing from the per-rank HBM plan (the reference's launcher docstring claims
+    "automatic micro-batch sizing", ``ai_engine/deepspeed_launcher.py:7-8``, and never implements it --
+    SURVEY A23).
+
+    Largest micro-batch (sequences per rank per micro-step) whose plan keeps ``min_headroom`` of the
+    GPU free, preferring no activation checkpointing (recompute costs ~1/3 of the forward) over a larger
+    micro-batch with it. With ``global_batch`` (sequences per optimizer step over the data-parallel
+    ranks; EP and ZeRO shard inside the same world) only micro-batches that divide it are tried and the
+    gradient accumulation follows; without it the tokens per step are kept: GA = grad_accum / mbs.
+    ``data_parallel``: ranks that draw different sequences (world / sequence-parallel size; default world);
+    ``seq_len`` is then the per-rank chunk."""
+    dp = data_parallel or world
+    if global_batch is not None:
+        base = global_batch
+    else:
+        base = grad_accum * dp  # the sequences per step of (mbs 1, grad_accum)
+    cands = [b for b in range(min(max_micro, max(1, base // dp)), 0, -1) if base % (b * dp) == 0]
+    modes = [True] if force_checkpointing else ([False, True] if allow_checkpointing else [False])
+    tried: List[Dict[str, object]] = []
+    for ckpt in modes:
+        for b in cands:
+            ga = base // (b * dp)
+            p = plan_rank(m, world=world, micro_batch=b, seq_len=seq_len, grad_accum=ga,
+                          activation_checkpointing=ckpt, **plan_kw)
+            tried.append({"micro_batch": b, "checkpointing": ckpt, "total_GiB": round(p.total / GiB, 1)})
+            if p.fits(min_headroom):
+                return MicroBatchChoice(b, ga, ckpt, p, tried)
+    raise ValueError(f"{m.name} at world {world}, seq {seq_len}: no micro-batch fits with "
+                     f"{min_headroom:.0%} HBM headroom (even with checkpointing); consider offload_optimizer/param")
+
+
 def baseline_configs() -> Dict[str, RankPlan]:
     """BASELINE.json configs 2-5 as the MI355X presets run them (launcher.config.presets)."""
     from ..models import get_config
@@ -235,9 +285,15 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--ga", type=int, default=8)
     ap.add_argument("--ckpt", action="store_true")
     ap.add_argument("--ep", type=int, default=1)
+    ap.add_argument("--auto-mbs", action="store_true", help="size the micro-batch to the plan (keeps mbs x GA)")
     a = ap.parse_args(argv)
     if not a.model:
         print(json.dumps({k: v.summary() for k, v in baseline_configs().items()}, indent=1))
+        return 0
+    if a.auto_mbs:
+        ch = auto_micro_batch(get_config(a.model), world=a.world, seq_len=a.seq, global_batch=a.mbs * a.ga * a.world,
+                              zero_stage=a.zero, ep_size=a.ep, force_checkpointing=a.ckpt)
+        print(json.dumps(ch.summary(), indent=1))
         return 0
     p = plan_rank(get_config(a.model), world=a.world, zero_stage=a.zero, micro_batch=a.mbs, seq_len=a.seq,
                   grad_accum=a.ga, activation_checkpointing=a.ckpt, ep_size=a.ep)

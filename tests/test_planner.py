@@ -124,3 +124,36 @@ def test_shadow_engine_expert_parallel_one_expert_per_rank():
     t = torch.randint(0, m.vocab_size, (2, 33), generator=torch.Generator().manual_seed(1))
     out = eng.train_step([(t[:, :-1], t[:, 1:])])
     assert torch.isfinite(out["loss"])
+
+
+def test_auto_micro_batch_keeps_global_batch_and_fits():
+    from distributed_llm_training_gpu_manager_amd.parallel.planner import auto_micro_batch
+    m = get_config("llama3-8b")
+    ch = auto_micro_batch(m, world=8, seq_len=8192, global_batch=64)
+    assert ch.micro_batch * ch.grad_accum * 8 == 64
+    assert ch.plan.fits(0.10) and not ch.activation_checkpointing
+    # the next larger divisor did not fit (that is why it was not taken)
+    bigger = [t for t in ch.tried if t["micro_batch"] > ch.micro_batch]
+    assert bigger and all(t["total_GiB"] * GiB > 0.9 * MI355X_HBM for t in bigger)
+    # 70B at W=8 only fits with recompute: the planner turns checkpointing on rather than failing
+    ch70 = auto_micro_batch(get_config("llama3-70b"), world=8, seq_len=8192, global_batch=128)
+    assert ch70.activation_checkpointing and ch70.plan.fits(0.10)
+    with pytest.raises(ValueError):
+        auto_micro_batch(get_config("llama3-70b"), world=1, seq_len=8192, global_batch=8)
+
+
+def test_dsconfig_auto_micro_batch():
+    from distributed_llm_training_gpu_manager_amd.engine.dsconfig import engine_config_from_ds
+    ds = {"train_micro_batch_size_per_gpu": "auto", "train_batch_size": 64, "gradient_accumulation_steps": 8,
+          "zero_optimization": {"stage": 3}, "bf16": {"enabled": True}}
+    cfg, notes = engine_config_from_ds(ds, 8192, model_cfg=get_config("llama3-8b"), world=8)
+    assert cfg.micro_batch_size * cfg.grad_accum * 8 == 64 and cfg.micro_batch_size > 1
+    assert any("auto micro-batch" in n for n in notes)
+    # the mi355x switch keeps the configured global batch (mbs x GA x world)
+    ds2 = {"train_micro_batch_size_per_gpu": 1, "gradient_accumulation_steps": 8, "zero_optimization": {"stage": 3},
+           "mi355x": {"auto_micro_batch": True}}
+    cfg2, _ = engine_config_from_ds(ds2, 8192, model_cfg=get_config("llama3-8b"), world=1)
+    assert cfg2.micro_batch_size * cfg2.grad_accum == 8
+    # without the model the request degrades to micro-batch 1 with a note
+    cfg3, notes3 = engine_config_from_ds(ds, 8192)
+    assert cfg3.micro_batch_size == 1 and any("needs the model" in n for n in notes3)
