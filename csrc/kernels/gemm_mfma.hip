@@ -368,17 +368,24 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
     const int mrow = wr * 128 + 16 * mi + i;  // row within the block tile
     if (mrow >= rows_valid) continue;
     const int64_t m = m0 + mrow;
+    if constexpr (EPI == kAccF32) {  // the row group's four reads in flight before the adds
+      f32x4 old[4];
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+        old[ni] = *reinterpret_cast<const f32x4*>(C + (m * p.ldc + n0 + wc * 64 + 16 * ni + 4 * g) * 4);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+        *reinterpret_cast<f32x4*>(C + (m * p.ldc + n0 + wc * 64 + 16 * ni + 4 * g) * 4) = old[ni] + acc[mi][ni];
+      continue;
+    }
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) {
       const int n = n0 + wc * 64 + 16 * ni + 4 * g;
       if constexpr (EPI == kStoreBf16) {
         bf16x4 v = {(bf16)acc[mi][ni][0], (bf16)acc[mi][ni][1], (bf16)acc[mi][ni][2], (bf16)acc[mi][ni][3]};
         *reinterpret_cast<bf16x4*>(C + (m * p.ldc + n) * 2) = v;
-      } else if constexpr (EPI == kStoreF32) {
-        *reinterpret_cast<f32x4*>(C + (m * p.ldc + n) * 4) = acc[mi][ni];
       } else {
-        f32x4* dst = reinterpret_cast<f32x4*>(C + (m * p.ldc + n) * 4);
-        *dst = *dst + acc[mi][ni];
+        *reinterpret_cast<f32x4*>(C + (m * p.ldc + n) * 4) = acc[mi][ni];
       }
     }
   }

@@ -57,6 +57,10 @@ def grouped_supported(x: torch.Tensor, wgrad: bool = False) -> bool:
 
 
 def mfma_mm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, acc: bool = False) -> torch.Tensor:
+    # (a 4-wave, 128x128-per-wave variant of the dense kernel measured 20-30 % slower than these 8 waves on
+    # the Llama-3-8B GEMMs -- one barrier per K-tile with one wave per SIMD exposes the DMA and barrier
+    # latency, and its 384 live fragment/accumulator registers spill VGPRs into AGPRs;
+    # profiles/gemm_mfma_4wave_experiment_r02.log -- and was removed)
     if use_native(out):
         hip_ops().gemm_mfma(out, a, b, acc, None, DENSE, a.shape[0], b.shape[1], a.shape[1], 1, 0)
         return out

@@ -25,9 +25,11 @@ def _rel(x, ref):
 @pytest.mark.parametrize("a_rowmajor", [True, False])
 @pytest.mark.parametrize("b_rowmajor", [True, False])
 @pytest.mark.parametrize("epi", ["bf16", "f32", "acc"])
-def test_dense_layouts_and_epilogues(a_rowmajor, b_rowmajor, epi):
+@pytest.mark.parametrize("K", [64, 128, 320])
+def test_dense_layouts_and_epilogues(a_rowmajor, b_rowmajor, epi, K):
+    """K 64 / 128 / 320 = one, two (no steady state) and five K-tiles."""
     g = torch.Generator(device=dev).manual_seed(0)
-    M, K, N = 512, 320, 768
+    M, N = 512, 768
     a = _op((M, K), a_rowmajor, g)
     b = _op((K, N), b_rowmajor, g)
     ref = a.float() @ b.float()

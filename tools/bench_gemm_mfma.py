@@ -55,11 +55,16 @@ def main():
         for k, v in ts.items():
             v.sort()
             r[k] = {"ms": round(v[len(v) // 2], 3), "TFLOPs": round(fl / (v[len(v) // 2] * 1e-3) / 1e12, 1)}
-        # numerics of the dW arm against fp32
+        # numerics of the dW / forward arms against fp32
+        ref = dy.float().t() @ x.float()
         w.zero_()
         gm.mfma_mm(w, dy.t(), x, acc=True)
-        ref = dy.float().t() @ x.float()
         r["dW_rel_err"] = float((w - ref).abs().max() / ref.abs().max())
+        del ref
+        fref = x.float() @ W.float().t()
+        o = gm.mfma_mm(torch.empty(T, O, device=dev, dtype=torch.bfloat16), x, W.t())
+        r["fwd_rel_err"] = float((o.float() - fref).abs().max() / fref.abs().max())
+        del fref, o
         res[name] = r
         print(name, json.dumps(r), flush=True)
         del dy, x, w, W
