@@ -14,19 +14,23 @@
 //  * V^T operands come from the row-major V tile through ds_read_b64_tr_b16
 //    (hardware transpose read); K is read with ds_read_b128. Both LDS images are
 //    XOR-swizzled on 16-byte chunks so every read is bank-conflict free.
-//  * K/V tiles are register-staged with the async-STAGE split: global loads for
-//    tile t+1 are issued before the MFMAs of tile t and written to the other LDS
-//    buffer after the next barrier (one barrier per KV tile).
+//  * K/V (forward, dQ) and Q/dO (dK/dV) tiles arrive by LDS-DMA (buffer_load ... lds,
+//    TileDma): 16 B per lane landing lane-linearly, the swizzle applied to the source
+//    offset, the tile advance a scalar soffset; tile t+1 is in flight while tile t's
+//    MFMAs run (one barrier per tile).
 //  * Work ordering: causal blocks are launched heaviest-first, and blocks that
 //    share one (batch, kv-head) -- i.e. the same K/V stream -- are grouped on one
 //    XCD (blockIdx % 8 labels an XCD) so the K/V re-reads of the GQA group hit L2.
-//  * Backward (FA2 structure, one workgroup per 128 keys of one (batch, kv head),
-//    looping over the q heads of the GQA group and the query tiles): K and V of the
-//    wave's 32 keys live in registers, dK^T/dV^T accumulate in registers (no
-//    cross-workgroup sum), S and dP are computed with the key on the lane so they
-//    feed dV^T / dK^T directly as accumulator-operands, -LSE and -delta are loaded
-//    as the initial accumulators, and dQ is summed across key blocks with fp32
-//    atomics shaped as 128-byte row segments.
+//  * Backward = three deterministic passes, no atomics (an atomic-dQ single pass would move
+//    2.15 GB of fp32 adds per Llama-3-8B layer at S = 8192, >= 1.65 ms at the chip-wide
+//    float-atomic rate):
+//      delta = rowsum(dO * O);
+//      dK/dV: one workgroup per (b, q head, 128 keys), the wave's 32 keys on the MFMA lanes,
+//        K in registers, V in LDS, S^T / dP^T computed with the key on the lane so they feed
+//        dV^T / dK^T as accumulator operands; fp32 per-q-head partials, summed over the GQA
+//        group by gqa_reduce into the packed dqkv;
+//      dQ: one workgroup per (b, q head, 128 queries), the forward's structure, dS^T used in
+//        place as the B operand of dQ^T += K^T dS^T.
 #include <torch/all.h>
 #include <c10/hip/HIPStream.h>
 #include <cstdlib>
