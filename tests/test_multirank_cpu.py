@@ -140,7 +140,14 @@ def _block_last_expert():
         logits[:, -1] = float("-inf")
         return orig(logits, k)
     rt._blocked = True
+    rt._orig = orig
     ops.router_topk = rt
+
+
+def _unblock_last_expert():
+    from distributed_llm_training_gpu_manager_amd import ops
+    if getattr(ops.router_topk, "_blocked", False):
+        ops.router_topk = ops.router_topk._orig
 
 
 def _ep_worker(rank, world, port, model, stage, out):
@@ -180,10 +187,13 @@ def test_mixtral_expert_parallel_matches_single(tmp_path, world, model):
     got = torch.load(out, weights_only=True)
     assert got["zero_token_expert"], "the last expert must receive no tokens"
     _block_last_expert()
-    eng = ZeroEngine(_model(model), _cfg(3, world, seq_len=8, micro_batch_size=1), torch.device("cpu"))
-    for i, t in enumerate(_data(model, 1, world, seq=8, mbs=1)[0]):
-        eng.micro_step(t[:, :-1], t[:, 1:], first=i == 0, last=i == world - 1)
-    ref = eng.full_grads()
+    try:
+        eng = ZeroEngine(_model(model), _cfg(3, world, seq_len=8, micro_batch_size=1), torch.device("cpu"))
+        for i, t in enumerate(_data(model, 1, world, seq=8, mbs=1)[0]):
+            eng.micro_step(t[:, :-1], t[:, 1:], first=i == 0, last=i == world - 1)
+        ref = eng.full_grads()
+    finally:
+        _unblock_last_expert()  # the patch must not leak into later tests of this process
     assert set(got["grads"]) == set(ref)
     for k, v in ref.items():
         err = float((got["grads"][k] - v).abs().max() / v.abs().max().clamp_min(1e-8))
@@ -222,6 +232,7 @@ def _defer_worker(rank, world, port, model, dw, out):
 def test_mixtral_deferred_expert_wgrad_expert_parallel_world4(tmp_path):
     """Deferred expert dW (one GEMM per expert over the step's micro-batches, models/mixtral.py) under EP=4
     with GA 3: same gradients and parameters as per-micro-batch dW and as single-process training."""
+    _unblock_last_expert()
     got = {}
     for dw in (True, False):
         out = str(tmp_path / f"defer_{dw}.pt")
