@@ -55,6 +55,9 @@ from .ptzip import PtWriter, Slot, read_slot
 STATE = ("master", "exp_avg", "exp_avg_sq")
 TAG_RE = re.compile(r"^global_step(\d+)$")
 MODEL0 = "mp_rank_00_model_states.pt"
+# the shm snapshot is page-locked in pieces of REG_CHUNK bytes with REG_PAUSE_S between them (_register_chunked)
+REG_CHUNK = int(os.environ.get("DLGM_CKPT_REG_MB", "1024")) << 20
+REG_PAUSE_S = float(os.environ.get("DLGM_CKPT_REG_PAUSE_MS", "5")) / 1000.0
 DS_VERSION = "0.13.1+dlgm-mi355x"  # the DeepSpeed release the reference pins (requirements.txt:6)
 
 
@@ -154,6 +157,10 @@ class AsyncCheckpointer:
         self.mode = self._pick_mode(mode, shm)
         self._snap: Optional[torch.Tensor] = None  # uint8 [14 n]: fp32 master | exp_avg | exp_avg_sq | bf16 params
         self._pinned_shm = False
+        self._reg: List[Tuple[int, int]] = []  # page-locked pieces of the shm snapshot (address, bytes)
+        self._reg_hurry = threading.Event()
+        self._reg_stop = threading.Event()
+        self._unreg = None
         self._ring: List[torch.Tensor] = []
         self._stream = torch.cuda.Stream(self.dev) if self.cuda else None
         self._capture_ev = None
@@ -205,20 +212,80 @@ class AsyncCheckpointer:
                 os.ftruncate(fd, nb)
             finally:
                 os.close(fd)
-            self._snap = torch.from_file(self.shm_path, shared=True, size=nb, dtype=torch.uint8)
+            snap = torch.from_file(self.shm_path, shared=True, size=nb, dtype=torch.uint8)
             if self.cuda:
-                rc = torch.cuda.cudart().cudaHostRegister(self._snap.data_ptr(), nb, 0)
-                self._pinned_shm = int(rc) == 0
+                self._pinned_shm = self._register_chunked(snap.data_ptr(), nb)
+            self._snap = snap
         elif self.mode == "device":
             self._snap = torch.empty(nb, dtype=torch.uint8, device=self.dev)
             self._ring = [torch.empty(self.ring_elems, dtype=torch.float32, pin_memory=True) for _ in range(2)]
         else:
             self._snap = torch.empty(nb, dtype=torch.uint8, pin_memory=self.cuda)
 
+    @staticmethod
+    def _hip_register_fns():
+        """(register, unregister) through ctypes on the HIP runtime torch already loaded: a ctypes foreign call
+        releases the GIL, so page-locking ~100 GB on a background thread does not stall the training loop's
+        Python thread (torch.cuda.cudart() holds the GIL for the whole call)."""
+        import ctypes
+        try:
+            lib = ctypes.CDLL("libamdhip64.so")
+        except OSError:
+            return None
+        reg, unreg = lib.hipHostRegister, lib.hipHostUnregister
+        reg.restype, reg.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
+        unreg.restype, unreg.argtypes = ctypes.c_int, [ctypes.c_void_p]
+        return (lambda p_, n_: int(reg(p_, n_, 0))), (lambda p_: int(unreg(p_)))
+
+    def _register_chunked(self, ptr: int, nb: int) -> bool:
+        """Page-lock the mapped snapshot file in REG_CHUNK pieces with a pause between them. One
+        hipHostRegister of the whole ~112 GB file holds the HIP runtime for ~6 s and every kernel launch of
+        the training thread waits meanwhile (measured on MI355X: the first step after a restore took 6.4 s
+        instead of 0.9 s); pieces with a short pause let the training thread launch between them, and a
+        save that needs the buffer sets _reg_hurry to finish without pauses. Device copies into the snapshot
+        are split at the piece boundaries (_copy_to_snap)."""
+        fns = self._hip_register_fns()
+        if fns is None:
+            cr = torch.cuda.cudart()
+            fns = (lambda p_, n_: int(cr.cudaHostRegister(p_, n_, 0))), (lambda p_: int(cr.cudaHostUnregister(p_)))
+        self._unreg = fns[1]
+        self._reg = []
+        off = 0
+        while off < nb:
+            if self._reg_stop.is_set():  # close() while page-locking: it unregisters what is in self._reg
+                return False
+            ln = min(REG_CHUNK, nb - off)
+            if fns[0](ptr + off, ln) != 0:
+                for p_, _ in self._reg:
+                    fns[1](p_)
+                self._reg = []
+                return False
+            self._reg.append((ptr + off, ln))
+            off += ln
+            if REG_PAUSE_S > 0 and off < nb and not self._reg_hurry.is_set():
+                time.sleep(REG_PAUSE_S)
+        return True
+
+    def _copy_to_snap(self, dst: torch.Tensor, src: torch.Tensor) -> None:
+        """dst (a flat view of the snapshot) <- src, asynchronously, never crossing a page-locked piece."""
+        if not self._reg:
+            dst.copy_(src, non_blocking=True)
+            return
+        es, n = dst.element_size(), dst.numel()
+        base = dst.data_ptr() - self._snap.data_ptr()
+        i = 0
+        while i < n:
+            b = base + i * es
+            m = min(n - i, ((b // REG_CHUNK + 1) * REG_CHUNK - b) // es)
+            dst[i:i + m].copy_(src[i:i + m], non_blocking=True)
+            i += m
+
     def prepare_async(self) -> None:
         """Allocate (and page-lock) the snapshot buffer on a background thread while training runs, so the
         first save -- often an emergency one on a spot notice -- does not pay for 14 B/param of fresh host
         pages. Call it after any restore: the shm tier's file is the one a restore reads."""
+        if os.environ.get("DLGM_CKPT_PREPARE", "1") == "0":
+            return
         if self.active and self._snap is None and self._prep is None:
             self._prep = threading.Thread(target=self._alloc_snapshot, daemon=True, name="ckpt-prepare")
             self._prep.start()
@@ -241,6 +308,7 @@ class AsyncCheckpointer:
             self.wait()
         save_id = f"{step}.{self._restart}.{self._saves}"
         if self._prep is not None:
+            self._reg_hurry.set()  # a save is waiting: page-lock the rest without yielding to training
             self._prep.join()  # background allocation / page-locking of the snapshot buffer
             self._prep = None
         if self._snap is None:
@@ -256,7 +324,7 @@ class AsyncCheckpointer:
             self._stream.wait_stream(cur)
             with torch.cuda.stream(self._stream):
                 for dst, s in srcs:
-                    dst.copy_(s, non_blocking=True)
+                    self._copy_to_snap(dst, s)
                 ev = torch.cuda.Event()
                 ev.record(self._stream)
             self._capture_ev = ev
@@ -619,9 +687,15 @@ class AsyncCheckpointer:
         self.wait()
         if self._before_optimizer_step in self.engine.pre_step_hooks:
             self.engine.pre_step_hooks.remove(self._before_optimizer_step)
-        if self._pinned_shm and self._snap is not None:
-            torch.cuda.cudart().cudaHostUnregister(self._snap.data_ptr())
-            self._pinned_shm = False
+        if self._prep is not None:  # background page-locking still running: stop it before unregistering
+            self._reg_stop.set()
+            self._prep.join()
+            self._prep = None
+        if self.cuda and self._reg:
+            for p_, _ in self._reg:
+                self._unreg(p_)
+        self._reg = []
+        self._pinned_shm = False
         self._snap = None
         if discard_shm:
             self.discard_shm()

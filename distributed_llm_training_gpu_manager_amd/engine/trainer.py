@@ -109,10 +109,25 @@ class MetricsPusher:
             self._thread.join(timeout_s)
 
 
+def _process_start() -> float:
+    try:
+        import psutil
+        return float(psutil.Process().create_time())
+    except Exception:  # noqa: BLE001
+        return _T_IMPORTED
+
+
+_T_IMPORTED = time.time()  # this module (and torch) imported
+
+
 class Trainer:
     def __init__(self, args: argparse.Namespace):
         self.args = args
+        # restart timeline (MTTR breakdown): process start -> imports -> process group -> engine -> restore ->
+        # first completed step; printed once after the first step
+        self.timeline: Dict[str, float] = {"process_start": _process_start(), "imported": _T_IMPORTED}
         self.env = init_distributed(args.device)
+        self.timeline["dist_init"] = time.time()
         self.comm = Comm()
         over = {"max_seq_len": max(args.seq_len, 1)} if args.seq_len else {}
         if getattr(args, "n_layers", 0):
@@ -150,6 +165,7 @@ class Trainer:
         self.global_batch = self._elastic_batch(args)
         save_dir = args.save_dir or os.environ.get("DLGM_SAVE_DIR")
         self.engine = ZeroEngine(self.mcfg, self.ecfg, self.env.device, self.comm)
+        self.timeline["engine"] = time.time()
         self.monitor = LossSpikeMonitor(MonitorConfig())
         self.trap = NanTrap(self.env.device, self.monitor)
         shm = {"auto": "auto", "on": True, "off": False}[args.ckpt_shm]
@@ -219,6 +235,12 @@ class Trainer:
         a = self.args
         if self.env.rank == 0:
             write_status(step, loss=loss, nonfinite=bad)
+            if "first_step" not in self.timeline:
+                self.timeline["first_step"] = now
+                t = self.timeline
+                keys = ["process_start", "imported", "dist_init", "engine", "restored", "first_step"]
+                self._say("startup: " + json.dumps({f"{b}_s": round(t[b] - t[a_], 2) for a_, b in zip(keys, keys[1:])}
+                                                    | {"total_s": round(now - t["process_start"], 2)}))
             hbm = self.telemetry.aggs["hbm_used_gib"].max if self.telemetry is not None else None
             alerts = self.monitor.ingest(TrainingMetrics(step=step, loss=loss, learning_rate=rec["lr"],
                                                          gradient_norm=rec["grad_norm"],
@@ -262,8 +284,13 @@ class Trainer:
                           f"(rollbacks: {getattr(self.ckpt, 'rollbacks', [])}; "
                           f"restore {json.dumps(getattr(self.ckpt, 'restore_stats', {}))})")
                 self.monitor.reset()
-        if self.ckpt is not None:
-            self.ckpt.prepare_async()  # snapshot buffer allocated / page-locked while the first steps run
+        self.timeline["restored"] = time.time()
+        # snapshot buffer allocated / page-locked in the background while the first steps run. Page-locking
+        # ~100 GB contends with kernel launches for seconds, so after a restore it starts once the first step
+        # has completed: recovery (MTTR) is not held up by a buffer the next save needs.
+        self._prep_after_first = self.ckpt is not None and start > 0
+        if self.ckpt is not None and not self._prep_after_first:
+            self.ckpt.prepare_async()
         for n in self.notes:
             self._say(f"note: {n}")
         self._tokens_step = self.ecfg.micro_batch_size * self.ecfg.seq_len * self.ecfg.grad_accum * self.env.world
@@ -291,6 +318,9 @@ class Trainer:
                 self.read_behind += 1  # read with a later step already queued behind it
                 stop = self._decide(self._report(*prev), step)
                 prev = None
+                if self._prep_after_first:
+                    self._prep_after_first = False
+                    self.ckpt.prepare_async()
                 if stop is not None:
                     rc = stop
                     break

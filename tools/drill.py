@@ -55,7 +55,7 @@ def drill_nan(a, work):
 def drill_sigkill(a, work):
     ck = os.path.join(work, "ck")
     reg = JobRegistry()
-    argv = train_argv(a, ["--steps", str(a.k + 2), "--save-interval", str(a.save_interval), "--kill-at-step",
+    argv = train_argv(a, ["--steps", str(a.k + 2 + a.steps_after), "--save-interval", str(a.save_interval), "--kill-at-step",
                           str(a.k), "--log-json", os.path.join(work, "kill.json")])
     t0 = time.time()
     job = reg.submit(JobSpec(job_id="sigkill-drill", argv=argv, env={"PYTHONPATH": ROOT}, save_dir=ck,
@@ -66,14 +66,19 @@ def drill_sigkill(a, work):
     resumed = re.findall(r"resumed from step (\d+) in ([0-9.]+)s", log)
     via = re.findall(r"resumed from step \d+ in [0-9.]+s via (\S+)", log)
     stats = [json.loads(x) for x in re.findall(r"restore (\{.*?\})\)", log)]
-    hist = {}
+    startup = [json.loads(x) for x in re.findall(r"\[train\] startup: (\{.*?\})", log)]
+    hist, steps_after = {}, []
     if os.path.exists(os.path.join(work, "kill.json")):
-        hist = json.load(open(os.path.join(work, "kill.json"))).get("ckpt", [])
+        kj = json.load(open(os.path.join(work, "kill.json")))
+        hist = kj.get("ckpt", [])
+        steps_after = [[r["step"], round(r["step_s"], 2)] for r in kj.get("log", [])]
     return {"drill": "sigkill", "status": job.status, "exit_codes": job.exit_codes, "restarts": job.restarts,
             "mttr_s": [round(x, 2) for x in job.mttr_s], "resume_load_s": [float(s) for _, s in resumed],
             "resumed_from_step": [int(s) for s, _ in resumed], "restored_from": via, "restore_breakdown": stats,
+            "startup_timeline": startup,  # per launch: imports / process group / engine / restore / first step
             "events": job.events,
             "ckpt_after_resume": hist,
+            "step_s_after_resume": steps_after,
             "tail": log[-800:]}
 
 
@@ -112,6 +117,7 @@ def main():
     ap.add_argument("--ga", type=int, default=1)
     ap.add_argument("--k", type=int, default=3)
     ap.add_argument("--save-interval", type=int, default=2)
+    ap.add_argument("--steps-after", type=int, default=0, help="sigkill drill: extra steps after the resume")
     ap.add_argument("--timeout", type=float, default=900)
     ap.add_argument("--keep-last", type=int, default=1)
     ap.add_argument("--ckpt-shm", default="auto", choices=["auto", "on", "off"])
