@@ -205,6 +205,36 @@ void dlgm_crc32c_chunks(const void* ptr, size_t n, size_t chunk, int nthreads, u
   for (auto& t : ts) t.join();
 }
 
+// dst <- src (n bytes) on `nthreads` threads in `chunk` pieces, with the CRC32C of every chunk of the copied
+// bytes. Used to restore from a memory-mapped /dev/shm snapshot: first touch of the shared pages through the
+// mapping runs at ~90 GB/s on 16 threads where pread of the same never-read pages ran at ~16 GB/s.
+void dlgm_copy_crc32c_chunks(const void* src, void* dst, size_t n, size_t chunk, int nthreads, uint32_t* crcs) {
+  const size_t nchunks = (n + chunk - 1) / chunk;
+  std::atomic<size_t> next{0};
+  const bool hw = have_sse42();
+  auto worker = [&]() {
+    for (;;) {
+      const size_t i = next.fetch_add(1);
+      if (i >= nchunks) return;
+      const size_t len = std::min(chunk, n - i * chunk);
+      const uint8_t* a = (const uint8_t*)src + i * chunk;
+      uint8_t* b = (uint8_t*)dst + i * chunk;
+      // copy and checksum in 1 MiB steps so the checksum reads the copy while it is still in cache
+      uint32_t c = 0;
+      for (size_t o = 0; o < len; o += (1u << 20)) {
+        const size_t l = std::min<size_t>(1u << 20, len - o);
+        memcpy(b + o, a + o, l);
+        if (crcs) c = hw ? crc32c_hw(b + o, l, c) : crc32c_sw(b + o, l, c);
+      }
+      if (crcs) crcs[i] = c;
+    }
+  };
+  nthreads = std::max(1, std::min<int>(nthreads, (int)std::max<size_t>(nchunks, 1)));
+  std::vector<std::thread> ts;
+  for (int t = 0; t < nthreads; ++t) ts.emplace_back(worker);
+  for (auto& t : ts) t.join();
+}
+
 // AdamW on host fp32 state (ZeRO-Offload). g may be pre-scaled; gscale multiplies it.
 void dlgm_cpu_adamw(float* p, float* m, float* v, const float* g, uint16_t* p16, size_t n, float lr, float b1,
                     float b2, float eps, float wd, float bc1, float bc2, float gscale) {

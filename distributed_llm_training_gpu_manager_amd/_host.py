@@ -47,6 +47,9 @@ def lib():
         L.dlgm_crc32c_chunks.restype = None
         L.dlgm_crc32c_chunks.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
                                          ctypes.POINTER(ctypes.c_uint32)]
+        L.dlgm_copy_crc32c_chunks.restype = None
+        L.dlgm_copy_crc32c_chunks.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                              ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)]
         L.dlgm_close_file.restype = ctypes.c_int
         L.dlgm_close_file.argtypes = [ctypes.c_int, ctypes.c_int]
         L.dlgm_aio_create.restype = ctypes.c_void_p
@@ -134,6 +137,22 @@ def crc32c_chunks(t: torch.Tensor) -> List[int]:
         return [_crc_py(mv[i * CHUNK:(i + 1) * CHUNK]) for i in range(nch)]
     crcs = (ctypes.c_uint32 * max(nch, 1))()
     L.dlgm_crc32c_chunks(ctypes.c_void_p(t.data_ptr()), n, CHUNK, THREADS, crcs)
+    return list(crcs)[:nch]
+
+
+def copy_crc32c_chunks(src: torch.Tensor, dst: torch.Tensor) -> List[int]:
+    """dst <- src (contiguous CPU byte tensors of one size, e.g. a mapped /dev/shm file slice into a pinned
+    slot) on THREADS threads, with the per-CHUNK CRC32C of the copied bytes."""
+    n = src.numel() * src.element_size()
+    assert dst.numel() * dst.element_size() == n and src.is_contiguous() and dst.is_contiguous()
+    nch = (n + CHUNK - 1) // CHUNK
+    L = lib()
+    if L is None:
+        dst.view(torch.uint8).copy_(src.view(torch.uint8))
+        return crc32c_chunks(dst)
+    crcs = (ctypes.c_uint32 * max(nch, 1))()
+    L.dlgm_copy_crc32c_chunks(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()), n, CHUNK, THREADS,
+                              crcs)
     return list(crcs)[:nch]
 
 

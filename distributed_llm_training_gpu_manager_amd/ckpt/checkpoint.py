@@ -161,6 +161,7 @@ class AsyncCheckpointer:
         self._reg_hurry = threading.Event()
         self._reg_stop = threading.Event()
         self._unreg = None
+        self._restored_map: Optional[torch.Tensor] = None  # the shm file mapped by a restore (reused, see _load_shm)
         self._ring: List[torch.Tensor] = []
         self._stream = torch.cuda.Stream(self.dev) if self.cuda else None
         self._capture_ev = None
@@ -207,12 +208,17 @@ class AsyncCheckpointer:
     def _alloc_snapshot(self) -> None:
         nb = self.snap_bytes
         if self.mode == "shm":
-            fd = os.open(self.shm_path, os.O_RDWR | os.O_CREAT, 0o600)
-            try:
-                os.ftruncate(fd, nb)
-            finally:
-                os.close(fd)
-            snap = torch.from_file(self.shm_path, shared=True, size=nb, dtype=torch.uint8)
+            keep, self._restored_map = self._restored_map, None
+            if keep is not None and self.shm_path == self.shm_src_path and keep.numel() == nb:
+                snap = keep  # the file this rank just restored from, already mapped (and its pages touched)
+            else:
+                del keep
+                fd = os.open(self.shm_path, os.O_RDWR | os.O_CREAT, 0o600)
+                try:
+                    os.ftruncate(fd, nb)
+                finally:
+                    os.close(fd)
+                snap = torch.from_file(self.shm_path, shared=True, size=nb, dtype=torch.uint8)
             if self.cuda:
                 self._pinned_shm = self._register_chunked(snap.data_ptr(), nb)
             self._snap = snap
@@ -559,9 +565,11 @@ class AsyncCheckpointer:
         return hashlib.sha1(json.dumps(lay, sort_keys=True).encode()).hexdigest()[:16]
 
     def _load_shm(self) -> Dict[str, Any]:
-        """Restore from the /dev/shm snapshot: the C++ reader streams CHUNK-aligned pieces of the file into two
-        pinned slots (16 threads, CRC32C computed while reading) and each piece goes on to the fp32 state on
-        the device while the next one is read -- page-cache bandwidth, not a page-faulting mmap."""
+        """Restore from the /dev/shm snapshot: the file is memory-mapped and CHUNK-aligned pieces are copied into
+        two pinned slots by 16 C++ threads (CRC32C of the copied bytes on the fly); each piece goes on to the
+        fp32 state on the device while the next one is copied. Copying through the mapping touches the
+        never-read shared pages at ~90 GB/s on an MI355X host where pread of them ran at ~16 GB/s
+        (tools/diag/shm_read_bench.cpp)."""
         with open(self.shm_src_meta) as f:
             m = json.load(f)
         eng, n = self.engine, self.n
@@ -578,14 +586,24 @@ class AsyncCheckpointer:
         q: "queue.Queue" = queue.Queue(maxsize=1)
         free = [threading.Semaphore(1), threading.Semaphore(1)]
 
+        tm = time.time()
+        fmap = torch.from_file(self.shm_src_path, shared=True, size=os.path.getsize(self.shm_src_path),
+                               dtype=torch.uint8) if _host.lib() is not None else None
+        self.restore_stats["map_s"] = round(time.time() - tm, 2)
+
         def reader():
             try:
                 for k, off, ln in jobs:
                     free[k % 2].acquire()
-                    q.put((k, off, ln, read_slot(self.shm_src_path, slots[k % 2][:ln], off)))
+                    if fmap is not None:
+                        crcs = _host.copy_crc32c_chunks(fmap[off:off + ln], slots[k % 2][:ln])
+                    else:
+                        crcs = read_slot(self.shm_src_path, slots[k % 2][:ln], off)
+                    q.put((k, off, ln, crcs))
             except Exception as e:  # noqa: BLE001
                 q.put(e)
         th = threading.Thread(target=reader, daemon=True)
+        tl = time.time()
         th.start()
         for _ in jobs:
             tw = time.time()
@@ -610,6 +628,8 @@ class AsyncCheckpointer:
                 waited[1] += time.time() - tw
             free[k % 2].release()
         th.join()
+        self.restore_stats["loop_s"] = round(time.time() - tl, 2)
+        tt = time.time()
         self.restore_stats.update(wait_read_s=round(waited[0], 2), wait_h2d_s=round(waited[1], 2),
                                   pieces=len(jobs), piece_MiB=piece >> 20, GiB=round(end / 2 ** 30, 1))
         if check and end % _host.CHUNK:  # the chunk straddling the fp32/bf16 boundary: verify it whole
@@ -617,6 +637,10 @@ class AsyncCheckpointer:
             c = read_slot(self.shm_src_path, tail, (end // _host.CHUNK) * _host.CHUNK)
             if c[0] != m["crc"][end // _host.CHUNK]:
                 raise CorruptCheckpoint("shm snapshot: checksum mismatch")
+        self.restore_stats["tail_s"] = round(time.time() - tt, 2)
+        # keep the mapping: unmapping ~90 GiB of populated page tables took ~3 s on the restore's critical
+        # path, and the snapshot buffer the next save needs is this same file (_alloc_snapshot reuses it)
+        self._restored_map = fmap
         eng.step_count = int(m["meta"]["global_steps"])
         return m["meta"].get("client_state", {})
 
@@ -697,6 +721,7 @@ class AsyncCheckpointer:
         self._reg = []
         self._pinned_shm = False
         self._snap = None
+        self._restored_map = None
         if discard_shm:
             self.discard_shm()
 
