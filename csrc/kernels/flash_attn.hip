@@ -55,6 +55,12 @@ constexpr float kRescaleLog2 = 8.f;
 // softmax does not need (arguments are <= 0 up to the deferred-rescale slack; underflow -> 0).
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// Packed fp32 pairs: v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 do two lanes' worth of softmax arithmetic per
+// issue slot. The attention loops are bound by vector-instruction issue next to the MFMAs (PMC: 5-8 VALU per
+// MFMA), so the elementwise work runs on pairs of accumulator registers.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+
 // A condition the caller knows is wave-uniform, made provably so (scalar branch, no exec masking).
 __device__ __forceinline__ bool uniform(bool c) { return __builtin_amdgcn_readfirstlane((int)c) != 0; }
 
@@ -85,6 +91,11 @@ __device__ __forceinline__ int swz_dual(int row, int ch) {
   if constexpr (D == 128) return ch ^ (((row & 3) << 2) | ((row >> 2) & 3));
   else return ch ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3));
 }
+
+// Makes x opaque to the optimiser: a per-lane LDS offset computed once before a loop then stays in its
+// register instead of being rebuilt from its row and swizzle parts inside the loop (hipcc re-added
+// them before every read: one v_add_u32 per ds_read in the backward's tile loops).
+__device__ __forceinline__ void pin(int& x) { asm volatile("" : "+v"(x)); }
 
 template <typename E>
 __device__ __forceinline__ vec8_t<E> lds_read_b128(const E* base) {
@@ -388,12 +399,15 @@ __global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams<E> 
 // Backward
 // ----------------------------------------------------------------------------------
 
-// delta[b, hq, q] = sum_d dO[b,q,hq,d] * O[b,q,hq,d]. A row of D bf16 is D/8 lanes x 16 B, so a
-// wave64 covers 64 / (D/8) rows at once (4 at D = 128, 8 at D = 64): every lane loads, and the row
-// sum is a shuffle over the row's lane group only.
+// nd[b, hq, q] = -sum_d dO[b,q,hq,d] * O[b,q,hq,d] and nls[b, hq, q] = -lse / scale (nls = nd + B*Hq*S):
+// the start values of the backward's dP and S accumulators, stored ready to use so that the dK/dV
+// loop loads them into the MFMA C operands with no negation or scaling per tile. A row of D bf16 is
+// D/8 lanes x 16 B, so a wave64 covers 64 / (D/8) rows at once (4 at D = 128, 8 at D = 64): every lane
+// loads, and the row sum is a shuffle over the row's lane group only.
 template <typename E, int D>
 __global__ __launch_bounds__(256) void flash_bwd_delta_kernel(const E* __restrict__ dout, const E* __restrict__ out,
-                                                              float* __restrict__ delta, int B, int S, int Hq,
+                                                              const float* __restrict__ lse, float* __restrict__ nd,
+                                                              float neg_inv_scale, int B, int S, int Hq,
                                                               int64_t do_ss, int64_t do_sh, int64_t do_sb) {
   constexpr int LPR = D / 8;             // lanes per row
   constexpr int RPB = 256 / LPR;         // rows per block
@@ -411,7 +425,11 @@ __global__ __launch_bounds__(256) void flash_bwd_delta_kernel(const E* __restric
   for (int j = 0; j < 8; ++j) acc += a[j] * c[j];
 #pragma unroll
   for (int o = LPR / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-  if (ok && sub == 0) delta[((int64_t)b * Hq + hq) * S + q] = acc;
+  if (ok && sub == 0) {
+    const int64_t o = ((int64_t)b * Hq + hq) * S + q;
+    nd[o] = -acc;
+    nd[(int64_t)B * Hq * S + o] = lse[o] * neg_inv_scale;
+  }
 }
 
 template <typename E>
@@ -421,7 +439,7 @@ struct BwdParams {
   const E* v;
   const E* dout;
   const float* lse;    // [B, Hq, S], natural log of sum exp(scale * s)
-  const float* delta;  // [B, Hq, S]
+  const float* delta;  // [2, B, Hq, S]: -delta, then -lse / scale (flash_bwd_delta_kernel)
   E* dq;            // [B, S, Hq, D]
   float* dk_part;      // [group, B, S, Hkv, D] fp32 partials (one per q head of the GQA group)
   float* dv_part;
@@ -472,7 +490,7 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
   constexpr int DT = D / 32;
   constexpr int QT = kKvBQ * D;
   __shared__ __attribute__((aligned(16))) E smem[2 * 2 * QT + kKvBKV * D];  // [buf][Q | dO], then V rows
-  __shared__ __attribute__((aligned(16))) float rc[2][64];        // [buf][lse 0..31 | delta 32..63]
+  __shared__ __attribute__((aligned(16))) float rc[2][64];        // [buf][-lse/scale 0..31 | -delta 32..63]
   E* vimg = smem + 2 * 2 * QT;  // this block's 128 V rows (row image): B operand of dP, re-read per tile
 
   const int lane = threadIdx.x & 63;
@@ -492,8 +510,8 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
   const E* vb = p.v + b * p.v_sb + hk * p.v_sh;
   const E* qb = p.q + b * p.q_sb + hq * p.q_sh;
   const E* dob = p.dout + b * p.do_sb + hq * p.do_sh;
-  const float* lseb = p.lse + ((int64_t)b * p.Hq + hq) * p.S;
-  const float* dlb = p.delta + ((int64_t)b * p.Hq + hq) * p.S;
+  const float* dlb = p.delta + ((int64_t)b * p.Hq + hq) * p.S;        // -delta
+  const float* lseb = dlb + (int64_t)p.B * p.Hq * p.S;                  // -lse / scale
 
   // K^T B-operand fragments of this wave's 32 keys stay in registers for the whole block; the V
   // rows go to LDS once (registers are the binding constraint at 2 waves / SIMD)
@@ -512,6 +530,15 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
   }
   const int nqt = (p.S + kKvBQ - 1) / kKvBQ;
   const int t0 = p.causal ? k0 / kKvBQ : 0;
+  const int vrow = 32 * w + r;
+  int qoff[KK], voff[KK];  // element offsets of this lane's Q / dO (dual image) and V (row image) fragments
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) {
+    qoff[kk] = r * D + swz_dual<D>(r, 2 * kk + h) * 8;
+    voff[kk] = vrow * D + swz_row<D>(vrow, 2 * kk + h) * 8;
+    pin(qoff[kk]);
+    pin(voff[kk]);
+  }
 
   const TileDma<E, D, kKvBQ, 1, TAIL> qdma(qb, p.q_ss, p.S, w, lane), dodma(dob, p.do_ss, p.S, w, lane);
   auto stage = [&](int buf, int t) {
@@ -541,32 +568,42 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int qr = (i & 3) + 8 * (i >> 2) + 4 * h;
-        sacc[i] = rc[buf][qr] * p.neg_inv_scale;  // S' = S - lse/scale  ->  p = exp2(S' * scale * log2e)
-        dpacc[i] = -rc[buf][32 + qr];
+        sacc[i] = rc[buf][qr];        // S' = S - lse/scale  ->  p = exp2(S' * scale * log2e)
+        dpacc[i] = rc[buf][32 + qr];  // dP - delta
       }
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
-        vec8_t<E> a = lds_read_b128(qi + r * D + swz_dual<D>(r, 2 * kk + h) * 8);
+        vec8_t<E> a = lds_read_b128(qi + qoff[kk]);
         sacc = mfma32(a, kf[kk], sacc);
       }
-      const int vrow = 32 * w + r;
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
-        vec8_t<E> a = lds_read_b128(di + r * D + swz_dual<D>(r, 2 * kk + h) * 8);
-        vec8_t<E> vv = lds_read_b128(vimg + vrow * D + swz_row<D>(vrow, 2 * kk + h) * 8);
+        vec8_t<E> a = lds_read_b128(di + qoff[kk]);
+        vec8_t<E> vv = lds_read_b128(vimg + voff[kk]);
         dpacc = mfma32(a, vv, dpacc);
       }
-      // dS = P (dP - delta); the softmax scale is applied once to dK at the end
+      // dS = P (dP - delta); the softmax scale is applied once to dK at the end. Masked scores go to
+      // -inf BEFORE the exponentials (exp2 -> 0), in a block of its own: a mask test inside the
+      // exponential loop became one scalar branch per element, which kept the exps out of the MFMA
+      // schedule (the forward's structure)
       const bool need_mask = uniform((p.causal && q0 < kw0 + 31) || q0 + kKvBQ > p.S || kw0 + 32 > p.S);
+      if (need_mask) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float pv = fast_exp2(sacc[i] * p.scale_log2);
-        if (need_mask) {
+        for (int i = 0; i < 16; ++i) {
           const int q = q0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-          if (key >= p.S || q >= p.S || (p.causal && key > q)) pv = 0.f;
+          if (key >= p.S || q >= p.S || (p.causal && key > q)) sacc[i] = -INFINITY;
         }
-        sacc[i] = pv;
-        dpacc[i] *= pv;
+      }
+      const f32x2 sl2 = {p.scale_log2, p.scale_log2};
+#pragma unroll
+      for (int i = 0; i < 16; i += 2) {
+        const f32x2 x = (f32x2){sacc[i], sacc[i + 1]} * sl2;
+        const f32x2 pv = {fast_exp2(x.x), fast_exp2(x.y)};
+        const f32x2 ds = (f32x2){dpacc[i], dpacc[i + 1]} * pv;
+        sacc[i] = pv.x;
+        sacc[i + 1] = pv.y;
+        dpacc[i] = ds.x;
+        dpacc[i + 1] = ds.y;
       }
       vec8_t<E> pfr[2], dsf[2];
 #pragma unroll
@@ -688,7 +725,7 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams<E
   }
   const int64_t rowc = ((int64_t)b * p.Hq + hq) * p.S;
   const float lse2 = qcol < p.S ? p.lse[rowc + qcol] * kLog2e : INFINITY;
-  const float dl = qcol < p.S ? p.delta[rowc + qcol] : 0.f;
+  const float nd = qcol < p.S ? p.delta[rowc + qcol] : 0.f;  // -delta
 
   f32x16 dqt[DT];
 #pragma unroll
@@ -696,6 +733,16 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams<E
 
   const int kv_end = p.causal ? min(p.S, q0 + kDqBQ) : p.S;
   const int nt = (kv_end + kDqBKV - 1) / kDqBKV;
+  // element offsets of this lane's K (dual image) and V (row image) fragments; row 32 + r has the same
+  // swizzle as row r, so the second 32-key subtile is an immediate offset away
+  int koff[KK], voff[KK];
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) {
+    koff[kk] = r * D + swz_dual<D>(r, 2 * kk + h) * 8;
+    voff[kk] = r * D + swz_row<D>(r, 2 * kk + h) * 8;
+    pin(koff[kk]);
+    pin(voff[kk]);
+  }
   const TileDma<E, D, kDqBKV, 1, TAIL> kdma(kb, p.k_ss, p.S, w, lane);
   const TileDma<E, D, kDqBKV, 0, TAIL> vdma(vb, p.v_ss, p.S, w, lane);
   auto stage = [&](int buf, int t) {
@@ -714,30 +761,39 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams<E
       const E* kt = smem + buf * 2 * TILE;
       const E* vt = kt + TILE;
       f32x16 s[2] = {(f32x16)(0.f), (f32x16)(0.f)};
-      f32x16 dp[2] = {(f32x16)(-dl), (f32x16)(-dl)};
+      f32x16 dp[2] = {(f32x16)(0.f), (f32x16)(0.f)};
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-          const int row = 32 * u + r;
-          vec8_t<E> a = lds_read_b128(kt + row * D + swz_dual<D>(row, 2 * kk + h) * 8);
+          vec8_t<E> a = lds_read_b128(kt + 32 * u * D + koff[kk]);
           s[u] = mfma32(a, qf[kk], s[u]);
-          vec8_t<E> c = lds_read_b128(vt + row * D + swz_row<D>(row, 2 * kk + h) * 8);
+          vec8_t<E> c = lds_read_b128(vt + 32 * u * D + voff[kk]);
           dp[u] = mfma32(c, dof[kk], dp[u]);
         }
       }
       vec8_t<E> dsf[2][2];
+      // masked scores -> -inf before the exponentials, in a block of their own (see dK/dV)
       const bool need_mask = uniform((p.causal && kv0 + kDqBKV - 1 > q0w) || kv0 + kDqBKV > p.S);
+      if (need_mask) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int kv = kv0 + 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
+            if (kv >= p.S || (p.causal && kv > qcol)) s[u][i] = -INFINITY;
+          }
+      }
+      const f32x2 sl2 = {p.scale_log2, p.scale_log2}, nl2 = {-lse2, -lse2}, nd2 = {nd, nd};
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float pv = fast_exp2(s[u][i] * p.scale_log2 - lse2);
-          if (need_mask) {
-            const int kv = kv0 + 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
-            if (kv >= p.S || (p.causal && kv > qcol)) pv = 0.f;
-          }
-          s[u][i] = pv * dp[u][i];
+        for (int i = 0; i < 16; i += 2) {
+          const f32x2 x = pk_fma((f32x2){s[u][i], s[u][i + 1]}, sl2, nl2);
+          const f32x2 pv = {fast_exp2(x.x), fast_exp2(x.y)};
+          const f32x2 ds = ((f32x2){dp[u][i], dp[u][i + 1]} + nd2) * pv;  // dS = P (dP - delta)
+          s[u][i] = ds.x;
+          s[u][i + 1] = ds.y;
         }
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2)
@@ -876,7 +932,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
     dq = at::empty({B, S, Hq, D}, q.options());
   }
   if (B == 0 || S == 0) return {dq.zero_(), dk.zero_(), dv.zero_()};
-  auto delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
+  auto delta = at::empty({2, B, Hq, S}, q.options().dtype(at::kFloat));  // -delta, -lse/scale
   at::Tensor dk_part, dv_part;
   if (group > 1) {
     dk_part = at::empty({group, B, S, Hkv, D}, q.options().dtype(at::kFloat));
@@ -893,11 +949,13 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
     auto dop = reinterpret_cast<const E*>(dout.data_ptr());
     auto outp = reinterpret_cast<const E*>(out.data_ptr());
     if (D == 128)
-      flash_bwd_delta_kernel<E, 128><<<(rows + 15) / 16, 256, 0, stream>>>(dop, outp, delta.data_ptr<float>(), B, S, Hq,
-                                                                          dout.stride(1), dout.stride(2), dout.stride(0));
+      flash_bwd_delta_kernel<E, 128><<<(rows + 15) / 16, 256, 0, stream>>>(
+          dop, outp, lse.data_ptr<float>(), delta.data_ptr<float>(), (float)(-1.0 / softmax_scale), B, S, Hq,
+          dout.stride(1), dout.stride(2), dout.stride(0));
     else
-      flash_bwd_delta_kernel<E, 64><<<(rows + 31) / 32, 256, 0, stream>>>(dop, outp, delta.data_ptr<float>(), B, S, Hq,
-                                                                         dout.stride(1), dout.stride(2), dout.stride(0));
+      flash_bwd_delta_kernel<E, 64><<<(rows + 31) / 32, 256, 0, stream>>>(
+          dop, outp, lse.data_ptr<float>(), delta.data_ptr<float>(), (float)(-1.0 / softmax_scale), B, S, Hq,
+          dout.stride(1), dout.stride(2), dout.stride(0));
     DLGM_CHECK_HIP(hipGetLastError());
     BwdParams<E> p{reinterpret_cast<const E*>(q.data_ptr()), reinterpret_cast<const E*>(k.data_ptr()),
                    reinterpret_cast<const E*>(v.data_ptr()), dop, lse.data_ptr<float>(), delta.data_ptr<float>(),
