@@ -571,16 +571,15 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
         sacc[i] = rc[buf][qr];        // S' = S - lse/scale  ->  p = exp2(S' * scale * log2e)
         dpacc[i] = rc[buf][32 + qr];  // dP - delta
       }
+      // S^T and dP^T as two interleaved accumulation chains: each MFMA's operand reads are covered by the
+      // other chain's MFMA instead of stalling a single chain on LDS latency
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
         vec8_t<E> a = lds_read_b128(qi + qoff[kk]);
-        sacc = mfma32(a, kf[kk], sacc);
-      }
-#pragma unroll
-      for (int kk = 0; kk < KK; ++kk) {
-        vec8_t<E> a = lds_read_b128(di + qoff[kk]);
+        vec8_t<E> d = lds_read_b128(di + qoff[kk]);
         vec8_t<E> vv = lds_read_b128(vimg + voff[kk]);
-        dpacc = mfma32(a, vv, dpacc);
+        sacc = mfma32(a, kf[kk], sacc);
+        dpacc = mfma32(d, vv, dpacc);
       }
       // dS = P (dP - delta); the softmax scale is applied once to dK at the end. Masked scores go to
       // -inf BEFORE the exponentials (exp2 -> 0), in a block of its own: a mask test inside the
