@@ -443,6 +443,8 @@ struct BwdParams {
   E* dq;            // [B, S, Hq, D]
   float* dk_part;      // [group, B, S, Hkv, D] fp32 partials (one per q head of the GQA group)
   float* dv_part;
+  E* ds;            // dS^T (unscaled) written by dK/dV for the dQ pass, or nullptr: [B, Hq, S/32 key blocks,
+                    // S/32 query blocks, 32 keys, 32 queries] -- one 2 KiB block per (32 keys, 32 queries)
   E* dk;            // [B, S, Hkv, D] (written directly when group == 1)
   E* dv;
   int64_t q_sb, q_ss, q_sh;
@@ -484,7 +486,7 @@ constexpr int kKvThreads = 256;
 constexpr int kKvBKV = 128;
 constexpr int kKvBQ = 32;
 
-template <typename E, int D, bool TAIL>
+template <typename E, int D, bool TAIL, bool STORE_DS = false>
 __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams<E> p) {
   constexpr int KK = D / 16;
   constexpr int DT = D / 32;
@@ -553,11 +555,31 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
     }
   };
 
+  // STORE_DS: the previous active tile's packed dS^T row, stored once this tile's DMA wait is behind us
+  uint4 ds_pend[2];
+  int ds_q0 = 0;
+  bool ds_has = false;
+  // blocked dS^T: this wave's 32 keys x 32 queries of one tile are one contiguous 2 KiB block (whole cache
+  // lines: a row-major [key][query] image took 64-byte pieces of 32 rows per tile and cost +25 % in dK/dV)
+  E* const ds_row = STORE_DS ? p.ds + ((((int64_t)b * p.Hq + hq) * (p.S / 32) + kw0 / 32) * (p.S / 32)) * 1024 +
+                                   r * 32 + 8 * h
+                             : nullptr;
+  auto flush_ds = [&]() {
+    if constexpr (STORE_DS) {
+      if (uniform(ds_has)) {
+        E* dst = ds_row + (ds_q0 / 32) * 1024;
+        *reinterpret_cast<uint4*>(dst) = ds_pend[0];
+        *reinterpret_cast<uint4*>(dst + 16) = ds_pend[1];
+        ds_has = false;
+      }
+    }
+  };
   // unrolled by two: the LDS buffer is a compile-time constant in each copy (immediate ds_read offsets)
   auto tile = [&](auto bufc, int t) {
     constexpr int buf = decltype(bufc)::value;
     vm_drain();  // this tile's LDS-DMA has landed ...
     __syncthreads();  // ... for every wave, and the other buffer's readers are done
+    flush_ds();
     if (t + 1 < nqt) stage(buf ^ 1, t + 1);
     const int q0 = t * kKvBQ;
     const bool active = uniform(!(p.causal && q0 + kKvBQ - 1 < kw0));
@@ -604,6 +626,23 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
         dpacc[i] = ds.x;
         dpacc[i + 1] = ds.y;
       }
+      if constexpr (STORE_DS) {
+        // dS^T row `key`, queries q0 .. q0 + 31: the accumulator is already key-on-lane, so this is the widened
+        // epilogue store (two 16-byte stores per lane, 64 contiguous bytes per key row). Packed now, stored
+        // at the start of the NEXT tile: vmcnt also counts stores on gfx950, so a store issued in this tile
+        // would hold up the next tile's wait for its LDS-DMA by the store's write-acknowledge latency.
+#pragma unroll
+        for (int k = 0; k < 4; k += 2) {
+          vec4_t<E> va = {(E)dpacc[4 * k], (E)dpacc[4 * k + 1], (E)dpacc[4 * k + 2], (E)dpacc[4 * k + 3]};
+          vec4_t<E> vb = {(E)dpacc[4 * k + 4], (E)dpacc[4 * k + 5], (E)dpacc[4 * k + 6], (E)dpacc[4 * k + 7]};
+          const uint2 a = __builtin_bit_cast(uint2, va), c = __builtin_bit_cast(uint2, vb);
+          const auto sx = __builtin_amdgcn_permlane32_swap(a.x, c.x, false, false);
+          const auto sy = __builtin_amdgcn_permlane32_swap(a.y, c.y, false, false);
+          ds_pend[k >> 1] = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+        }
+        ds_q0 = q0;
+        ds_has = true;
+      }
       vec8_t<E> pfr[2], dsf[2];
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
@@ -637,6 +676,7 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
     tile(std::integral_constant<int, 0>{}, t);
     if (t + 1 < nqt) tile(std::integral_constant<int, 1>{}, t + 1);
   }
+  flush_ds();
   if (group == 1) {  // the lane-pair swaps of the widened store need every lane, in or out of range
     store_rows_bf16<DT>(p.dk + ((int64_t)b * p.S + key) * p.dkv_ss + hk * D, dkt, p.scale, h, key < p.S);
     store_rows_bf16<DT>(p.dv + ((int64_t)b * p.S + key) * p.dkv_ss + hk * D, dvt, 1.f, h, key < p.S);
@@ -687,12 +727,15 @@ constexpr int kDqThreads = 256;
 constexpr int kDqBQ = 128;
 constexpr int kDqBKV = 64;
 
-template <typename E, int D, bool TAIL>
+template <typename E, int D, bool TAIL, bool FROM_DS = false>
 __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams<E> p) {
   constexpr int KK = D / 16;
   constexpr int DT = D / 32;
   constexpr int TILE = kDqBKV * D;
-  __shared__ __attribute__((aligned(16))) E smem[4 * TILE];  // [buf][K | V]
+  // FROM_DS: the second image is the dS^T tile [64 keys][128 queries] (written by dK/dV), read with the same
+  // transposed LDS reads as the K^T operand, so its fragments come out in the k order the MFMA pairs with K^T
+  constexpr int SLOT = FROM_DS ? TILE + kDqBKV * kDqBQ : 2 * TILE;
+  __shared__ __attribute__((aligned(16))) E smem[2 * SLOT];  // [buf][K | V or dS^T]
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -716,15 +759,18 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams<E
   const E* vb = p.v + b * p.v_sb + hk * p.v_sh;
 
   vec8_t<E> qf[KK], dof[KK];
+  float lse2 = 0.f, nd = 0.f;
+  if constexpr (!FROM_DS) {
 #pragma unroll
-  for (int kk = 0; kk < KK; ++kk) {
-    const bool ok = qcol < p.S;
-    qf[kk] = ok ? *reinterpret_cast<const vec8_t<E>*>(qb + (int64_t)qcol * p.q_ss + 16 * kk + 8 * h) : (vec8_t<E>)((E)0.f);
-    dof[kk] = ok ? *reinterpret_cast<const vec8_t<E>*>(dob + (int64_t)qcol * p.do_ss + 16 * kk + 8 * h) : (vec8_t<E>)((E)0.f);
+    for (int kk = 0; kk < KK; ++kk) {
+      const bool ok = qcol < p.S;
+      qf[kk] = ok ? *reinterpret_cast<const vec8_t<E>*>(qb + (int64_t)qcol * p.q_ss + 16 * kk + 8 * h) : (vec8_t<E>)((E)0.f);
+      dof[kk] = ok ? *reinterpret_cast<const vec8_t<E>*>(dob + (int64_t)qcol * p.do_ss + 16 * kk + 8 * h) : (vec8_t<E>)((E)0.f);
+    }
+    const int64_t rowc = ((int64_t)b * p.Hq + hq) * p.S;
+    lse2 = qcol < p.S ? p.lse[rowc + qcol] * kLog2e : INFINITY;
+    nd = qcol < p.S ? p.delta[rowc + qcol] : 0.f;  // -delta
   }
-  const int64_t rowc = ((int64_t)b * p.Hq + hq) * p.S;
-  const float lse2 = qcol < p.S ? p.lse[rowc + qcol] * kLog2e : INFINITY;
-  const float nd = qcol < p.S ? p.delta[rowc + qcol] : 0.f;  // -delta
 
   f32x16 dqt[DT];
 #pragma unroll
@@ -744,10 +790,31 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams<E
   }
   const TileDma<E, D, kDqBKV, 1, TAIL> kdma(kb, p.k_ss, p.S, w, lane);
   const TileDma<E, D, kDqBKV, 0, TAIL> vdma(vb, p.v_ss, p.S, w, lane);
+  // FROM_DS: the [64 keys][128 queries] dS^T tile gathered from eight 2 KiB blocks into a transposed-read
+  // image (the K-style recipe: 16 B per lane landing lane-linearly, the swizzle on the SOURCE offset). Lane
+  // (rin, phys) of piece j fills image row 4w + rin + 16j, physical chunk phys with logical chunk
+  // lc = swz_tr(row, phys); rows 32.. come from the next key block, so a piece's source offset is the
+  // lane's offset plus a per-piece and a per-tile scalar.
+  const int nqb = p.S / 32;
+  const E* dsl = FROM_DS ? p.ds + ((int64_t)b * p.Hq + hq) * p.S * p.S : p.k;
+  uint32_t ds_lane = 0;
+  if constexpr (FROM_DS) {
+    const int rin = lane / 16, phys = lane % 16;
+    const int lc = swz_tr<kDqBQ>(rin, phys);
+    ds_lane = (uint32_t)(((lc >> 2) * 1024 + (lc & 3) * 8 + (4 * w + rin) * 32) * 2);
+  }
   auto stage = [&](int buf, int t) {
-    E* img = smem + buf * 2 * TILE;
+    E* img = smem + buf * SLOT;
     kdma.issue(img, t * kDqBKV);
-    vdma.issue(img + TILE, t * kDqBKV);
+    if constexpr (FROM_DS) {
+      const uint32_t soff_t = (uint32_t)(((2 * t) * nqb + q0 / 32) * 1024 * 2);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        dma16(dsl, (int)((int64_t)p.S * p.S * 2), ds_lane,
+              soff_t + (uint32_t)(((j & 1) * 16 * 32 + (j >> 1) * nqb * 1024) * 2), img + TILE + (w + 4 * j) * 512);
+    } else {
+      vdma.issue(img + TILE, t * kDqBKV);
+    }
   };
   // unrolled by two: the LDS buffer is a compile-time constant in each copy (immediate ds_read offsets)
   auto tile = [&](auto bufc, int t) {
@@ -757,8 +824,34 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams<E
     if (t + 1 < nt) stage(buf ^ 1, t + 1);
     const int kv0 = t * kDqBKV;
     if (!(p.causal && kv0 > q0w + 31)) {
-      const E* kt = smem + buf * 2 * TILE;
+      const E* kt = smem + buf * SLOT;
       const E* vt = kt + TILE;
+      vec8_t<E> dsf[2][2];
+      if constexpr (FROM_DS) {
+        const int col = 32 * w + 16 * (g & 1) + 4 * (i16 & 3);  // this wave's 32 query columns
+        const int ch = col >> 3, within = col & 7;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const int r1 = 32 * u + 16 * s2 + 4 * h + (i16 >> 2);
+            const int r2 = r1 + 8;
+            dsf[u][s2] = cat(lds_read_tr(vt + r1 * kDqBQ + swz_tr<kDqBQ>(r1, ch) * 8 + within),
+                             lds_read_tr(vt + r2 * kDqBQ + swz_tr<kDqBQ>(r2, ch) * 8 + within));
+          }
+        // diagonal tiles: dS^T blocks above the diagonal were never written (the dK/dV wave skipped them)
+        if (uniform(p.causal && kv0 + kDqBKV - 1 > q0w)) {
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const int kv = kv0 + 32 * u + 16 * s2 + 8 * (j >> 2) + 4 * h + (j & 3);
+                if (kv > qcol) dsf[u][s2][j] = (E)0.f;
+              }
+        }
+      } else {
       f32x16 s[2] = {(f32x16)(0.f), (f32x16)(0.f)};
       f32x16 dp[2] = {(f32x16)(0.f), (f32x16)(0.f)};
 #pragma unroll
@@ -771,7 +864,6 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams<E
           dp[u] = mfma32(c, dof[kk], dp[u]);
         }
       }
-      vec8_t<E> dsf[2][2];
       // masked scores -> -inf before the exponentials, in a block of their own (see dK/dV)
       const bool need_mask = uniform((p.causal && kv0 + kDqBKV - 1 > q0w) || kv0 + kDqBKV > p.S);
       if (need_mask) {
@@ -800,6 +892,7 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams<E
                                 (E)s[u][8 * s2 + 3], (E)s[u][8 * s2 + 4], (E)s[u][8 * s2 + 5],
                                 (E)s[u][8 * s2 + 6], (E)s[u][8 * s2 + 7]};
       }
+      }  // FROM_DS
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         const int col = dt * 32 + 16 * (g & 1) + 4 * (i16 & 3);
@@ -828,6 +921,15 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams<E
 // DLGM_ATTN_BWD_STREAMS=1: the dQ pass on a side stream beside dK/dV. Off by default: measured at S 8192,
 // 32/8 heads the concurrent passes took 2.20 ms against 1.92 ms back to back (they contend for the same CUs
 // and L2; each already fills the chip with 2048 workgroups).
+// DLGM_ATTN_DQ_FROM_DS=1: dQ from the dS^T blocks the dK/dV pass stores (read per call, so a test or a
+// run can switch it). Off by default: at S 8192, 32/8 heads the dQ pass drops 750 -> 519 us but dK/dV
+// rises 1116 -> 1307 us for its 2.15 GB of dS^T writes (the board is at its power limit), and the
+// headline step moved 0.1-0.2 % for +2.3 GiB of peak memory (profiles/attn_experiments_r01.md).
+bool dq_from_ds() {
+  const char* e = std::getenv("DLGM_ATTN_DQ_FROM_DS");
+  return e != nullptr && std::atoi(e) != 0;
+}
+
 bool bwd_two_streams() {
   static const bool on = [] {
     const char* e = std::getenv("DLGM_ATTN_BWD_STREAMS");
@@ -959,15 +1061,23 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
     BwdParams<E> p{reinterpret_cast<const E*>(q.data_ptr()), reinterpret_cast<const E*>(k.data_ptr()),
                    reinterpret_cast<const E*>(v.data_ptr()), dop, lse.data_ptr<float>(), delta.data_ptr<float>(),
                    reinterpret_cast<E*>(dq.data_ptr()), group > 1 ? dk_part.data_ptr<float>() : nullptr,
-                   group > 1 ? dv_part.data_ptr<float>() : nullptr, reinterpret_cast<E*>(dk.data_ptr()),
+                   group > 1 ? dv_part.data_ptr<float>() : nullptr, /*ds=*/nullptr, reinterpret_cast<E*>(dk.data_ptr()),
                    reinterpret_cast<E*>(dv.data_ptr()), q.stride(0), q.stride(1), q.stride(2), k.stride(0),
                    k.stride(1), k.stride(2), v.stride(0), v.stride(1), v.stride(2), dout.stride(0), dout.stride(1),
                    dout.stride(2), dq_ss, dkv_ss, B, S, Hq, Hkv, (float)softmax_scale,
                    (float)(softmax_scale * kLog2e), (float)(-1.0 / softmax_scale), causal};
     const bool tail = S % 128 != 0;
+    // dQ from the stored dS^T (DLGM_ATTN_DQ_FROM_DS, full tiles only): the dK/dV pass writes dS^T as 16-bit
+    // rows and the dQ pass stages it like K instead of recomputing S, P and dP
+    const bool from_ds = !tail && dq_from_ds();
+    at::Tensor dsT;
+    if (from_ds) {
+      dsT = at::empty({B, Hq, S, S}, q.options());
+      p.ds = reinterpret_cast<E*>(dsT.data_ptr());
+    }
     // dK/dV and dQ are independent passes over the same inputs: optionally the dQ pass runs on a side stream
     // (forked and joined with events, so it also works under HIP graph capture)
-    const bool fork = bwd_two_streams();
+    const bool fork = bwd_two_streams() && !from_ds;
     hipStream_t qs = stream;
     if (fork) {
       qs = c10::hip::getStreamFromPool(false, q.get_device()).stream();
@@ -978,6 +1088,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
       if (tail) {
         flash_bwd_dkdv_kernel<E, 128, true><<<kv_blocks, kKvThreads, 0, stream>>>(p);
         flash_bwd_dq_kernel<E, 128, true><<<dq_blocks, kDqThreads, 0, qs>>>(p);
+      } else if (from_ds) {
+        flash_bwd_dkdv_kernel<E, 128, false, true><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+        flash_bwd_dq_kernel<E, 128, false, true><<<dq_blocks, kDqThreads, 0, stream>>>(p);
       } else {
         flash_bwd_dkdv_kernel<E, 128, false><<<kv_blocks, kKvThreads, 0, stream>>>(p);
         flash_bwd_dq_kernel<E, 128, false><<<dq_blocks, kDqThreads, 0, qs>>>(p);
@@ -986,6 +1099,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
       if (tail) {
         flash_bwd_dkdv_kernel<E, 64, true><<<kv_blocks, kKvThreads, 0, stream>>>(p);
         flash_bwd_dq_kernel<E, 64, true><<<dq_blocks, kDqThreads, 0, qs>>>(p);
+      } else if (from_ds) {
+        flash_bwd_dkdv_kernel<E, 64, false, true><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+        flash_bwd_dq_kernel<E, 64, false, true><<<dq_blocks, kDqThreads, 0, stream>>>(p);
       } else {
         flash_bwd_dkdv_kernel<E, 64, false><<<kv_blocks, kKvThreads, 0, stream>>>(p);
         flash_bwd_dq_kernel<E, 64, false><<<dq_blocks, kDqThreads, 0, qs>>>(p);

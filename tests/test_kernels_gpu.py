@@ -183,6 +183,26 @@ def test_flash_attention_fwd_bwd(B, S, Hq, Hkv, D, causal):
     assert rel_err(dq, dq_ref) < 3e-2, rel_err(dq, dq_ref)
 
 
+@pytest.mark.parametrize("S,Hq,Hkv,D", [(512, 8, 2, 128), (256, 4, 4, 64)])
+def test_flash_attention_bwd_dq_from_stored_ds(monkeypatch, S, Hq, Hkv, D):
+    """DLGM_ATTN_DQ_FROM_DS=1: dK/dV stores dS^T in 2 KiB blocks and dQ stages it instead of recomputing S, P,
+    dP -- same gradients as the fp32 reference and (to bf16 rounding of dS) as the recompute path."""
+    torch.manual_seed(0)
+    B = 1
+    q, k, v = (torch.randn(B, S, h, D, dtype=torch.bfloat16, device=DEV) for h in (Hq, Hkv, Hkv))
+    do = torch.randn(B, S, Hq, D, dtype=torch.bfloat16, device=DEV)
+    scale = 1 / math.sqrt(D)
+    o, lse = ops.flash_attn_fwd(q, k, v, scale, True)
+    monkeypatch.setenv("DLGM_ATTN_DQ_FROM_DS", "0")
+    base = ops.flash_attn_bwd(do, q, k, v, o, lse, scale, True)
+    monkeypatch.setenv("DLGM_ATTN_DQ_FROM_DS", "1")
+    ds_path = ops.flash_attn_bwd(do, q, k, v, o, lse, scale, True)
+    ref = attn_ops._ref_bwd(do.cpu(), q.cpu(), k.cpu(), v.cpu(), o.cpu(), lse.cpu(), scale, True)
+    for got, want, b in zip(ds_path, ref, base):
+        assert rel_err(got, want) < 3e-2, rel_err(got, want)
+        assert rel_err(got, b.cpu()) < 1e-2, rel_err(got, b.cpu())
+
+
 def test_flash_attention_rescale_branch():
     """Force the online-softmax rescale: one huge key late in the sequence for one query."""
     torch.manual_seed(1)
