@@ -50,6 +50,8 @@ def test_bench_single_process():
                 "--ga", "2"])
     _check(out, 1, 2, 1)
     assert out["extra"]["comm_busbw"] is None
+    # the headline metric name belongs to the headline model only; other presets name what they measured
+    assert out["metric"] == "tokens/sec (node) llama-tiny ZeRO-3", out["metric"]
 
 
 def test_bench_torchrun_two_ranks():
