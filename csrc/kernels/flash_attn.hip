@@ -189,9 +189,12 @@ struct TileDma {
     const int logical = SWZ == 2 ? swz_tr<D>(row, phys) : SWZ == 1 ? swz_dual<D>(row, phys) : swz_row<D>(row, phys);
     off0 = (uint32_t)((row * row_stride + logical * 8) * 2);
   }
-  __device__ __forceinline__ void issue(E* img, int row0) const {
+  // extra_soff: a wave-uniform byte offset added to every piece (the second head of a dK/dV workgroup),
+  // covered by extend()
+  __device__ __forceinline__ void extend(int64_t bytes) { nbytes += (int)bytes; }
+  __device__ __forceinline__ void issue(E* img, int row0, uint32_t extra_soff = 0) const {
     if (!TAIL || row0 + ROWS <= nrows) {  // whole tile in range: scalar row advance
-      const uint32_t soff = (uint32_t)(row0 * stride * 2), step = (uint32_t)(NW * PR * stride * 2);
+      const uint32_t soff = (uint32_t)(row0 * stride * 2) + extra_soff, step = (uint32_t)(NW * PR * stride * 2);
 #pragma unroll
       for (int j = 0; j < PPW; ++j) dma16(base, nbytes, off0, soff + j * step, img + (wave + NW * j) * 512);
       return;
@@ -204,7 +207,7 @@ struct TileDma {
 #pragma unroll
       for (int j = 0; j < PPW; ++j) {
         const int r = min(row0 + NW * PR * j + rin, nrows - 1);
-        dma16(base, nbytes, off0 + (uint32_t)((int64_t)(r - rin) * stride * 2), 0, img + (wave + NW * j) * 512);
+        dma16(base, nbytes, off0 + (uint32_t)((int64_t)(r - rin) * stride * 2), extra_soff, img + (wave + NW * j) * 512);
       }
     }
   }
@@ -486,8 +489,12 @@ constexpr int kKvThreads = 256;
 constexpr int kKvBKV = 128;
 constexpr int kKvBQ = 32;
 
-template <typename E, int D, bool TAIL, bool STORE_DS = false>
+// HP: q heads per workgroup (2 when the GQA group is even): the heads of a pair share this block's K / V, so
+// the workgroup walks both heads' query tiles into one dK/dV accumulator -- half the fp32 partials written
+// and summed by gqa_reduce, half the K / V block loads.
+template <typename E, int D, bool TAIL, bool STORE_DS = false, int HP = 1>
 __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams<E> p) {
+  static_assert(!(STORE_DS && HP > 1), "the stored-dS path runs one head per workgroup");
   constexpr int KK = D / 16;
   constexpr int DT = D / 32;
   constexpr int QT = kKvBQ * D;
@@ -501,9 +508,9 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
   const int nkt = (p.S + kKvBKV - 1) / kKvBKV;
   const int group = p.Hq / p.Hkv;
   const int work = xcd_remap(blockIdx.x, gridDim.x);
-  const int bh = work / nkt;                 // blocks of one (b, hq) share the Q / dO stream -> one XCD
+  const int bh = work / nkt;                 // blocks of one (b, head pair) share the Q / dO stream -> one XCD
   const int kt = work - bh * nkt;            // ascending = most queries first under the causal mask
-  const int b = bh / p.Hq, hq = bh % p.Hq;
+  const int b = bh / (p.Hq / HP), hq = (bh % (p.Hq / HP)) * HP;  // first head of the workgroup
   const int hk = hq / group, hh = hq % group;
   const int k0 = kt * kKvBKV;
   const int kw0 = k0 + 32 * w;
@@ -542,16 +549,24 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
     pin(voff[kk]);
   }
 
-  const TileDma<E, D, kKvBQ, 1, TAIL> qdma(qb, p.q_ss, p.S, w, lane), dodma(dob, p.do_ss, p.S, w, lane);
-  auto stage = [&](int buf, int t) {
-    const int q0 = t * kKvBQ;
+  TileDma<E, D, kKvBQ, 1, TAIL> qdma(qb, p.q_ss, p.S, w, lane), dodma(dob, p.do_ss, p.S, w, lane);
+  if constexpr (HP > 1) {
+    qdma.extend((int64_t)(HP - 1) * p.q_sh * 2);
+    dodma.extend((int64_t)(HP - 1) * p.do_sh * 2);
+  }
+  // tile index j over (head of the pair, query tile): head j / nt_h, query tile t0 + j % nt_h
+  const int nt_h = nqt - t0 > 0 ? nqt - t0 : 0;
+  const int ntot = HP * nt_h;
+  auto stage = [&](int buf, int j) {
+    const int hp = HP > 1 ? j / nt_h : 0;
+    const int q0 = (t0 + j - hp * nt_h) * kKvBQ;
     E* img = smem + buf * 2 * QT;
-    qdma.issue(img, q0);
-    dodma.issue(img + QT, q0);
+    qdma.issue(img, q0, (uint32_t)(hp * p.q_sh * 2));
+    dodma.issue(img + QT, q0, (uint32_t)(hp * p.do_sh * 2));
     if (w == 0) {
       int q = q0 + (lane & 31);
       q = q < p.S ? q : p.S - 1;
-      glds4((lane < 32 ? lseb : dlb) + q, &rc[buf][0]);
+      glds4((lane < 32 ? lseb : dlb) + (int64_t)hp * p.S + q, &rc[buf][0]);
     }
   };
 
@@ -575,12 +590,13 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
     }
   };
   // unrolled by two: the LDS buffer is a compile-time constant in each copy (immediate ds_read offsets)
-  auto tile = [&](auto bufc, int t) {
+  auto tile = [&](auto bufc, int j) {
     constexpr int buf = decltype(bufc)::value;
     vm_drain();  // this tile's LDS-DMA has landed ...
     __syncthreads();  // ... for every wave, and the other buffer's readers are done
     flush_ds();
-    if (t + 1 < nqt) stage(buf ^ 1, t + 1);
+    if (j + 1 < ntot) stage(buf ^ 1, j + 1);
+    const int t = t0 + (HP > 1 ? j % nt_h : j);
     const int q0 = t * kKvBQ;
     const bool active = uniform(!(p.causal && q0 + kKvBQ - 1 < kw0));
     if (active) {
@@ -671,13 +687,14 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
       }
     }
   };
-  if (t0 < nqt) stage(0, t0);
-  for (int t = t0; t < nqt; t += 2) {
-    tile(std::integral_constant<int, 0>{}, t);
-    if (t + 1 < nqt) tile(std::integral_constant<int, 1>{}, t + 1);
+  if (ntot > 0) stage(0, 0);
+  for (int j = 0; j < ntot; j += 2) {
+    tile(std::integral_constant<int, 0>{}, j);
+    if (j + 1 < ntot) tile(std::integral_constant<int, 1>{}, j + 1);
   }
   flush_ds();
-  if (group == 1) {  // the lane-pair swaps of the widened store need every lane, in or out of range
+  if (group == HP) {  // one partial per kv head: written directly (the lane-pair swaps of the widened store
+                      // need every lane, in or out of range)
     store_rows_bf16<DT>(p.dk + ((int64_t)b * p.S + key) * p.dkv_ss + hk * D, dkt, p.scale, h, key < p.S);
     store_rows_bf16<DT>(p.dv + ((int64_t)b * p.S + key) * p.dkv_ss + hk * D, dvt, 1.f, h, key < p.S);
     return;
@@ -686,7 +703,7 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) dkt[dt] *= p.scale;
   {
-    const int64_t off = ((((int64_t)hh * p.B + b) * p.S + key) * p.Hkv + hk) * D;
+    const int64_t off = ((((int64_t)(hh / HP) * p.B + b) * p.S + key) * p.Hkv + hk) * D;
     float* dkr = p.dk_part + off;
     float* dvr = p.dv_part + off;
 #pragma unroll
@@ -1034,17 +1051,24 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
   }
   if (B == 0 || S == 0) return {dq.zero_(), dk.zero_(), dv.zero_()};
   auto delta = at::empty({2, B, Hq, S}, q.options().dtype(at::kFloat));  // -delta, -lse/scale
+  const bool tail = S % 128 != 0;
+  // dQ from the stored dS^T (DLGM_ATTN_DQ_FROM_DS, full tiles only): the dK/dV pass writes dS^T blocks and
+  // the dQ pass stages them instead of recomputing S, P and dP
+  const bool from_ds = !tail && dq_from_ds();
+  // two q heads per dK/dV workgroup when the GQA group is even (one head with the stored-dS path)
+  const int hp = (group % 2 == 0 && !from_ds) ? 2 : 1;
+  const int nparts = group / hp;  // fp32 dK/dV partials summed by gqa_reduce
   at::Tensor dk_part, dv_part;
-  if (group > 1) {
-    dk_part = at::empty({group, B, S, Hkv, D}, q.options().dtype(at::kFloat));
-    dv_part = at::empty({group, B, S, Hkv, D}, q.options().dtype(at::kFloat));
+  if (nparts > 1) {
+    dk_part = at::empty({nparts, B, S, Hkv, D}, q.options().dtype(at::kFloat));
+    dv_part = at::empty({nparts, B, S, Hkv, D}, q.options().dtype(at::kFloat));
   }
   auto stream = c10::hip::getCurrentHIPStream();
   const int64_t rows = (int64_t)B * S * Hq;
   TORCH_CHECK(k.scalar_type() == q.scalar_type() && v.scalar_type() == q.scalar_type() &&
                   dout.scalar_type() == q.scalar_type() && out.scalar_type() == q.scalar_type(),
               "flash_attn_bwd: mixed dtypes");
-  const int64_t kv_blocks = (int64_t)B * Hq * ((S + kKvBKV - 1) / kKvBKV);
+  const int64_t kv_blocks = (int64_t)B * (Hq / hp) * ((S + kKvBKV - 1) / kKvBKV);
   const int64_t dq_blocks = (int64_t)B * Hq * ((S + kDqBQ - 1) / kDqBQ);
   DLGM_DISPATCH_16(q.scalar_type(), E, {
     auto dop = reinterpret_cast<const E*>(dout.data_ptr());
@@ -1060,16 +1084,12 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
     DLGM_CHECK_HIP(hipGetLastError());
     BwdParams<E> p{reinterpret_cast<const E*>(q.data_ptr()), reinterpret_cast<const E*>(k.data_ptr()),
                    reinterpret_cast<const E*>(v.data_ptr()), dop, lse.data_ptr<float>(), delta.data_ptr<float>(),
-                   reinterpret_cast<E*>(dq.data_ptr()), group > 1 ? dk_part.data_ptr<float>() : nullptr,
-                   group > 1 ? dv_part.data_ptr<float>() : nullptr, /*ds=*/nullptr, reinterpret_cast<E*>(dk.data_ptr()),
+                   reinterpret_cast<E*>(dq.data_ptr()), nparts > 1 ? dk_part.data_ptr<float>() : nullptr,
+                   nparts > 1 ? dv_part.data_ptr<float>() : nullptr, /*ds=*/nullptr, reinterpret_cast<E*>(dk.data_ptr()),
                    reinterpret_cast<E*>(dv.data_ptr()), q.stride(0), q.stride(1), q.stride(2), k.stride(0),
                    k.stride(1), k.stride(2), v.stride(0), v.stride(1), v.stride(2), dout.stride(0), dout.stride(1),
                    dout.stride(2), dq_ss, dkv_ss, B, S, Hq, Hkv, (float)softmax_scale,
                    (float)(softmax_scale * kLog2e), (float)(-1.0 / softmax_scale), causal};
-    const bool tail = S % 128 != 0;
-    // dQ from the stored dS^T (DLGM_ATTN_DQ_FROM_DS, full tiles only): the dK/dV pass writes dS^T as 16-bit
-    // rows and the dQ pass stages it like K instead of recomputing S, P and dP
-    const bool from_ds = !tail && dq_from_ds();
     at::Tensor dsT;
     if (from_ds) {
       dsT = at::empty({B, Hq, S, S}, q.options());
@@ -1086,24 +1106,28 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
     }
     if (D == 128) {
       if (tail) {
-        flash_bwd_dkdv_kernel<E, 128, true><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+        if (hp == 2) flash_bwd_dkdv_kernel<E, 128, true, false, 2><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+        else flash_bwd_dkdv_kernel<E, 128, true><<<kv_blocks, kKvThreads, 0, stream>>>(p);
         flash_bwd_dq_kernel<E, 128, true><<<dq_blocks, kDqThreads, 0, qs>>>(p);
       } else if (from_ds) {
         flash_bwd_dkdv_kernel<E, 128, false, true><<<kv_blocks, kKvThreads, 0, stream>>>(p);
         flash_bwd_dq_kernel<E, 128, false, true><<<dq_blocks, kDqThreads, 0, stream>>>(p);
       } else {
-        flash_bwd_dkdv_kernel<E, 128, false><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+        if (hp == 2) flash_bwd_dkdv_kernel<E, 128, false, false, 2><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+        else flash_bwd_dkdv_kernel<E, 128, false><<<kv_blocks, kKvThreads, 0, stream>>>(p);
         flash_bwd_dq_kernel<E, 128, false><<<dq_blocks, kDqThreads, 0, qs>>>(p);
       }
     } else {
       if (tail) {
-        flash_bwd_dkdv_kernel<E, 64, true><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+        if (hp == 2) flash_bwd_dkdv_kernel<E, 64, true, false, 2><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+        else flash_bwd_dkdv_kernel<E, 64, true><<<kv_blocks, kKvThreads, 0, stream>>>(p);
         flash_bwd_dq_kernel<E, 64, true><<<dq_blocks, kDqThreads, 0, qs>>>(p);
       } else if (from_ds) {
         flash_bwd_dkdv_kernel<E, 64, false, true><<<kv_blocks, kKvThreads, 0, stream>>>(p);
         flash_bwd_dq_kernel<E, 64, false, true><<<dq_blocks, kDqThreads, 0, stream>>>(p);
       } else {
-        flash_bwd_dkdv_kernel<E, 64, false><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+        if (hp == 2) flash_bwd_dkdv_kernel<E, 64, false, false, 2><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+        else flash_bwd_dkdv_kernel<E, 64, false><<<kv_blocks, kKvThreads, 0, stream>>>(p);
         flash_bwd_dq_kernel<E, 64, false><<<dq_blocks, kDqThreads, 0, qs>>>(p);
       }
     }
@@ -1112,13 +1136,13 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
       DLGM_CHECK_HIP(hipEventRecord(bwd_event(1), qs));
       DLGM_CHECK_HIP(hipStreamWaitEvent(stream, bwd_event(1), 0));
     }
-    if (group > 1) {
+    if (nparts > 1) {
       const int64_t n = (int64_t)B * S * Hkv * D;
       const int64_t grid = std::min<int64_t>((n / 8 + 255) / 256, 4096);
       gqa_reduce_kernel<E><<<grid, 256, 0, stream>>>(dk_part.data_ptr<float>(), reinterpret_cast<E*>(dk.data_ptr()),
-                                                     group, n, Hkv * D, dkv_ss);
+                                                     nparts, n, Hkv * D, dkv_ss);
       gqa_reduce_kernel<E><<<grid, 256, 0, stream>>>(dv_part.data_ptr<float>(), reinterpret_cast<E*>(dv.data_ptr()),
-                                                     group, n, Hkv * D, dkv_ss);
+                                                     nparts, n, Hkv * D, dkv_ss);
       DLGM_CHECK_HIP(hipGetLastError());
     }
   });
