@@ -1054,7 +1054,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
   const bool tail = S % 128 != 0;
   // dQ from the stored dS^T (DLGM_ATTN_DQ_FROM_DS, full tiles only): the dK/dV pass writes dS^T blocks and
   // the dQ pass stages them instead of recomputing S, P and dP
-  const bool from_ds = !tail && dq_from_ds();
+  // the dS^T buffer is B*Hq*S^2 16-bit values (4.3 GB for Llama-3-8B at S 8192): long sequences fall back
+  const bool from_ds = !tail && dq_from_ds() && (int64_t)B * Hq * S * S * 2 <= (int64_t(16) << 30);
   // two q heads per dK/dV workgroup when the GQA group is even (one head with the stored-dS path)
   const int hp = (group % 2 == 0 && !from_ds) ? 2 : 1;
   const int nparts = group / hp;  // fp32 dK/dV partials summed by gqa_reduce
