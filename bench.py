@@ -1,8 +1,14 @@
 #!/usr/bin/env python3
 """Headline benchmark: Llama-3-8B ZeRO-3 bf16 training tokens/sec on N MI355X GPUs of one node.
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it is
-started under ``torch.distributed.run`` (one rank per GPU, RCCL over xGMI). W untimed
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it runs
+one rank per GPU (RCCL over xGMI) under ``torch.distributed.run``. Started WITHOUT a
+launcher (no ``WORLD_SIZE`` in the environment) with ``--gpus N > 1``, bench.py starts
+``python -m torch.distributed.run --nproc-per-node N`` itself as a child process --
+before anything touches the GPU -- relays its output and exits with its code, so the
+multi-GPU number can never silently be a one-GPU number (the reference's launcher owns
+the multi-process command the same way: ``/root/reference/ai_engine/deepspeed_launcher.py:277-300``).
+A ``WORLD_SIZE`` that disagrees with ``--gpus`` is an error (exit 2). W untimed
 warmup optimizer steps, then exactly K timed steps bracketed by a barrier +
 ``torch.cuda.synchronize()``; the elapsed time is the MAX over ranks; rank 0 prints
 one JSON line. ``value`` is whole-job tokens/sec (all N GPUs); per-GPU work is fixed
@@ -32,6 +38,51 @@ METRIC = "tokens/sec (node) Llama-3-8B ZeRO-3"
 def _knob(v: str):
     """A ZeRO-3 residency knob from the command line: 'hbm' or a number."""
     return v if v in ("hbm", "auto") else float(v)
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _self_launch(n: int, argv) -> int:
+    """Run this script under torch.distributed.run with `n` local ranks as a CHILD process (never exec:
+    this process has not touched the GPU, and must not be replaced once anything has). Output is
+    inherited, so rank 0's JSON line is this process's stdout; the exit code is the launcher's."""
+    import signal
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__), *argv]
+    print(f"[bench] no launcher: starting {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, cwd=ROOT)
+
+    def _forward(sig, _frame):
+        proc.send_signal(sig)
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, _forward)
+    return proc.wait()
+
+
+def _check_ranks(env, n: int) -> None:
+    """After init: the process group has exactly `n` ranks and every rank drives its own device."""
+    import torch.distributed as dist
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    if world != n:
+        raise SystemExit(f"[bench] error: --gpus {n} but the process group has {world} ranks")
+    if world == 1:
+        return
+    ids = torch.tensor([env.local_rank, env.device.index if env.device.type == "cuda" else -1],
+                       dtype=torch.int64, device=env.device)
+    got = [torch.zeros_like(ids) for _ in range(world)]
+    dist.all_gather(got, ids)
+    local = [int(g[0]) for g in got]
+    devs = [int(g[1]) for g in got]
+    if len(set(local)) != world or (env.device.type == "cuda" and len(set(devs)) != world):
+        raise SystemExit(f"[bench] error: ranks share a device (LOCAL_RANK {local}, device {devs})")
 
 
 def main() -> int:
@@ -70,14 +121,24 @@ def main() -> int:
                          "the headline always runs the full preset)")
     args = ap.parse_args()
 
+    # launch topology is decided before any GPU call
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            return _self_launch(args.gpus, sys.argv[1:])
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print(f"[bench] error: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}", file=sys.stderr)
+        return 2
+
     from distributed_llm_training_gpu_manager_amd.models import get_config
     from distributed_llm_training_gpu_manager_amd.parallel.comm import Comm, init_distributed
     from distributed_llm_training_gpu_manager_amd.parallel.zero import EngineConfig, ZeroEngine
     from distributed_llm_training_gpu_manager_amd import _native
 
+    if torch.cuda.is_available() and args.gpus > torch.cuda.device_count():
+        print(f"[bench] error: --gpus {args.gpus} but {torch.cuda.device_count()} GPUs are visible", file=sys.stderr)
+        return 2
     env = init_distributed("cuda" if torch.cuda.is_available() else "cpu")
-    if env.world != args.gpus and env.rank == 0:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={env.world}", file=sys.stderr)
+    _check_ranks(env, args.gpus)
     if env.device.type == "cuda":
         _native.hip_ops()  # fail loudly if the HIP kernels are not built
     comm = Comm()
@@ -128,6 +189,11 @@ def main() -> int:
     t = torch.tensor([elapsed], dtype=torch.float64, device=env.device)
     comm.all_reduce_max(t)
     elapsed = float(t.item())
+    # per-rank peak HBM, max over ranks (ZeRO-3 shards differ in size by at most one padding unit)
+    peak = torch.tensor([torch.cuda.max_memory_allocated(env.device) / 1024 ** 3 if env.device.type == "cuda"
+                         else 0.0], dtype=torch.float64, device=env.device)
+    comm.all_reduce_max(peak)
+    peak_gib = float(peak.item())
 
     if args.profile_steps > 0:  # outside the timed region: never part of the reported number
         from distributed_llm_training_gpu_manager_amd.utils.profiling import trace_window
@@ -184,6 +250,8 @@ def main() -> int:
                 "zero3_allgathers_per_step": eng.live_plan.gathers_per_step(args.ga),
                 "zero3_resident_gathered_params": eng.live_plan.resident_params,
                 "mem": {k: round(v, 1) for k, v in eng.memory_report().items()},
+                "peak_GiB_max_over_ranks": round(peak_gib, 1),
+                "launch": "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ else "single process",
                 "telemetry": telem,
                 "comm_busbw": None,
             },

@@ -24,13 +24,16 @@ at::Tensor dlgm_swiglu_fwd(const at::Tensor& gu);
 at::Tensor dlgm_swiglu_bwd(const at::Tensor& dy, const at::Tensor& gu);
 // cross_entropy.hip
 std::tuple<at::Tensor, at::Tensor> dlgm_cross_entropy_(at::Tensor logits, const at::Tensor& labels,
-                                                       int64_t ignore_index, double grad_scale, bool compute_grad);
+                                                       int64_t ignore_index, double grad_scale, bool compute_grad,
+                                                       const c10::optional<at::Tensor>& scale);
 // optim.hip
 void dlgm_grad_stats(at::TensorList grads, at::Tensor out, bool accumulate);
 void dlgm_adamw_step_(at::Tensor p, at::Tensor m, at::Tensor v, const at::Tensor& g,
                       const c10::optional<at::Tensor>& p16, const c10::optional<at::Tensor>& stats, double lr,
                       double beta1, double beta2, double eps, double weight_decay, double bc1, double bc2,
-                      double grad_scale, double max_norm);
+                      double grad_scale, double max_norm, const c10::optional<at::Tensor>& scale_state);
+void dlgm_loss_scale_update_(at::Tensor state, const at::Tensor& stats, int64_t window, int64_t hysteresis,
+                             double min_scale);
 void dlgm_accumulate_(at::Tensor dst, const at::Tensor& src, double alpha, double beta);
 void dlgm_cast_f32_bf16_(at::Tensor dst, const at::Tensor& src);
 // flash_attn.hip
@@ -69,9 +72,10 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("rope_(Tensor(a!) qkv, Tensor cos, Tensor sin, Tensor? pos_ids, int n_rope_heads, int head_dim, int seq_len, bool inverse) -> ()");
   m.def("swiglu_fwd(Tensor gu) -> Tensor");
   m.def("swiglu_bwd(Tensor dy, Tensor gu) -> Tensor");
-  m.def("cross_entropy_(Tensor(a!) logits, Tensor labels, int ignore_index, float grad_scale, bool compute_grad) -> (Tensor, Tensor)");
+  m.def("cross_entropy_(Tensor(a!) logits, Tensor labels, int ignore_index, float grad_scale, bool compute_grad, Tensor? scale=None) -> (Tensor, Tensor)");
   m.def("grad_stats(Tensor[] grads, Tensor(a!) out, bool accumulate) -> ()");
-  m.def("adamw_step_(Tensor(a!) p, Tensor(b!) m, Tensor(c!) v, Tensor g, Tensor(d!)? p16, Tensor? stats, float lr, float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2, float grad_scale, float max_norm) -> ()");
+  m.def("adamw_step_(Tensor(a!) p, Tensor(b!) m, Tensor(c!) v, Tensor g, Tensor(d!)? p16, Tensor? stats, float lr, float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2, float grad_scale, float max_norm, Tensor? scale_state=None) -> ()");
+  m.def("loss_scale_update_(Tensor(a!) state, Tensor stats, int window, int hysteresis, float min_scale) -> ()");
   m.def("accumulate_(Tensor(a!) dst, Tensor src, float alpha, float beta) -> ()");
   m.def("cast_f32_bf16_(Tensor(a!) dst, Tensor src) -> ()");
   m.def("flash_attn_fwd(Tensor q, Tensor k, Tensor v, float softmax_scale, bool causal) -> (Tensor, Tensor)");
@@ -98,6 +102,7 @@ TORCH_LIBRARY_IMPL(dlgm, CUDA, m) {
   m.impl("cross_entropy_", &dlgm_cross_entropy_);
   m.impl("grad_stats", &dlgm_grad_stats);
   m.impl("adamw_step_", &dlgm_adamw_step_);
+  m.impl("loss_scale_update_", &dlgm_loss_scale_update_);
   m.impl("accumulate_", &dlgm_accumulate_);
   m.impl("cast_f32_bf16_", &dlgm_cast_f32_bf16_);
   m.impl("flash_attn_fwd", &dlgm_flash_attn_fwd);

@@ -24,7 +24,8 @@ template <typename E>
 __global__ __launch_bounds__(kThreads) void ce_kernel(E* __restrict__ logits, const int64_t* __restrict__ labels,
                                                       float* __restrict__ loss, float* __restrict__ lse_out,
                                                       int64_t V, int64_t row_stride, int64_t ignore_index,
-                                                      float grad_scale, bool compute_grad) {
+                                                      float grad_scale, const float* __restrict__ scale,
+                                                      bool compute_grad) {
   __shared__ float red[kWaves];
   const int64_t row = blockIdx.x;
   E* x = logits + row * row_stride;
@@ -61,7 +62,8 @@ __global__ __launch_bounds__(kThreads) void ce_kernel(E* __restrict__ logits, co
   }
   if (!compute_grad) return;
   __syncthreads();  // the label logit is read above before being overwritten below
-  const float gs = valid ? grad_scale : 0.f;
+  // fp16 path: the dynamic loss scale lives on the device (no host read per step)
+  const float gs = valid ? grad_scale * (scale ? scale[0] : 1.f) : 0.f;
   for (int64_t c = threadIdx.x; c < nvec; c += kThreads) {
     f32x8 v = load8f(x + c * 8);
     f32x8 g;
@@ -80,15 +82,21 @@ __global__ __launch_bounds__(kThreads) void ce_kernel(E* __restrict__ logits, co
 }  // namespace
 
 // Returns (loss_per_row fp32 [T], lse fp32 [T]). When compute_grad, logits is overwritten
-// with d(loss_sum * grad_scale)/d logits.
+// with d(loss_sum * grad_scale * scale[0])/d logits (scale: optional device fp32, the loss scale).
 std::tuple<at::Tensor, at::Tensor> dlgm_cross_entropy_(at::Tensor logits, const at::Tensor& labels,
                                                        int64_t ignore_index, double grad_scale,
-                                                       bool compute_grad) {
+                                                       bool compute_grad, const c10::optional<at::Tensor>& scale) {
   TORCH_CHECK(logits.is_cuda() && DLGM_IS16(logits) && logits.dim() == 2 && logits.stride(1) == 1,
               "cross_entropy: logits must be a [T, V] bf16/fp16 GPU tensor with unit inner stride");
   TORCH_CHECK(logits.stride(0) % 8 == 0, "cross_entropy: row stride must be a multiple of 8");
   TORCH_CHECK(labels.scalar_type() == at::kLong && labels.numel() == logits.size(0) && labels.is_contiguous(),
               "cross_entropy: labels must be contiguous int64 [T]");
+  const float* sp = nullptr;
+  if (scale.has_value() && scale->defined()) {
+    TORCH_CHECK(scale->is_cuda() && scale->scalar_type() == at::kFloat && scale->numel() >= 1,
+                "cross_entropy: scale must be a device fp32 tensor");
+    sp = scale->data_ptr<float>();
+  }
   const int64_t T = logits.size(0), V = logits.size(1);
   auto loss = at::empty({T}, logits.options().dtype(at::kFloat));
   auto lse = at::empty({T}, logits.options().dtype(at::kFloat));
@@ -98,7 +106,7 @@ std::tuple<at::Tensor, at::Tensor> dlgm_cross_entropy_(at::Tensor logits, const 
                    ce_kernel<E><<<T, kThreads, 0, stream>>>(reinterpret_cast<E*>(logits.data_ptr()),
                                                             labels.data_ptr<int64_t>(), loss.data_ptr<float>(),
                                                             lse.data_ptr<float>(), V, logits.stride(0), ignore_index,
-                                                            (float)grad_scale, compute_grad));
+                                                            (float)grad_scale, sp, compute_grad));
   DLGM_CHECK_HIP(hipGetLastError());
   return {loss, lse};
 }

@@ -1055,7 +1055,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
   // dQ from the stored dS^T (DLGM_ATTN_DQ_FROM_DS, full tiles only): the dK/dV pass writes dS^T blocks and
   // the dQ pass stages them instead of recomputing S, P and dP
   // the dS^T buffer is B*Hq*S^2 16-bit values (4.3 GB for Llama-3-8B at S 8192): long sequences fall back
-  const bool from_ds = !tail && dq_from_ds() && (int64_t)B * Hq * S * S * 2 <= (int64_t(16) << 30);
+  // the dQ pass addresses each head's dS^T region through a 32-bit buffer resource: also bound it per head
+  const bool from_ds = !tail && dq_from_ds() && (int64_t)B * Hq * S * S * 2 <= (int64_t(16) << 30) &&
+                       (int64_t)S * S * 2 < (int64_t(1) << 31);
   // two q heads per dK/dV workgroup when the GQA group is even (one head with the stored-dS path)
   const int hp = (group % 2 == 0 && !from_ds) ? 2 : 1;
   const int nparts = group / hp;  // fp32 dK/dV partials summed by gqa_reduce

@@ -117,15 +117,18 @@ struct AdamHyper {
   float lr, b1, b2, eps, wd, bc1, bc2, grad_scale, max_norm;
 };
 
-__device__ __forceinline__ float clip_coef(const float* stats, const AdamHyper& h, bool& skip) {
+// inv_scale: optional device word, 1 / (dynamic loss scale) of the fp16 path
+__device__ __forceinline__ float clip_coef(const float* stats, const float* inv_scale, const AdamHyper& h,
+                                           bool& skip) {
+  const float gsc = h.grad_scale * (inv_scale ? *inv_scale : 1.f);
   if (!stats) {
     skip = false;
-    return h.grad_scale;
+    return gsc;
   }
   skip = stats[1] > 0.f;
-  float coef = h.grad_scale;
+  float coef = gsc;
   if (h.max_norm > 0.f) {
-    const float norm = sqrtf(stats[0]) * h.grad_scale;
+    const float norm = sqrtf(stats[0]) * gsc;
     coef *= fminf(1.f, h.max_norm / (norm + 1e-6f));
   }
   return coef;
@@ -135,9 +138,10 @@ template <typename GT, typename PT>
 __global__ __launch_bounds__(kThreads) void adamw_kernel(float* __restrict__ p, float* __restrict__ m,
                                                          float* __restrict__ v, const GT* __restrict__ g,
                                                          PT* __restrict__ p16, const float* __restrict__ stats,
-                                                         int64_t n, AdamHyper h) {
+                                                         const float* __restrict__ inv_scale, int64_t n,
+                                                         AdamHyper h) {
   bool skip;
-  const float gc = clip_coef(stats, h, skip);
+  const float gc = clip_coef(stats, inv_scale, h, skip);
   if (skip) return;  // overflow / NaN: the whole step is dropped (fp16 loss-scaler semantics)
   const float decay = 1.f - h.lr * h.wd;
   const float step_size = h.lr / h.bc1;
@@ -199,6 +203,30 @@ __global__ __launch_bounds__(kThreads) void cast_kernel(const float* __restrict_
     for (int64_t i = nv * 4 + threadIdx.x; i < n; i += kThreads) dst[i] = (PT)src[i];
 }
 
+// DeepSpeed dynamic loss scaler, one thread, on the device: state = [scale, 1/scale, good steps, hysteresis
+// left]; stats[1] = non-finite gradient count of the step just taken (reference fp16 block,
+// deepspeed_launcher.py:175-183: initial_scale_power, loss_scale_window, hysteresis, min_loss_scale).
+__global__ void loss_scale_update_kernel(float* __restrict__ st, const float* __restrict__ stats, float window,
+                                         float hysteresis, float min_scale) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  float scale = st[0], good = st[2], hyst = st[3];
+  if (stats[1] > 0.f) {
+    hyst -= 1.f;
+    if (hyst <= 0.f) {
+      scale = fmaxf(scale * 0.5f, min_scale);
+      hyst = hysteresis;
+    }
+    good = 0.f;
+  } else {
+    good += 1.f;
+    if (fmodf(good, window) == 0.f) scale *= 2.f;
+  }
+  st[0] = scale;
+  st[1] = 1.f / scale;
+  st[2] = good;
+  st[3] = hyst;
+}
+
 void check_flat(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.is_contiguous(), name, " must be a contiguous GPU tensor");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
@@ -241,7 +269,7 @@ void dlgm_grad_stats(at::TensorList grads, at::Tensor out, bool accumulate) {
 void dlgm_adamw_step_(at::Tensor p, at::Tensor m, at::Tensor v, const at::Tensor& g,
                       const c10::optional<at::Tensor>& p16, const c10::optional<at::Tensor>& stats, double lr,
                       double beta1, double beta2, double eps, double weight_decay, double bc1, double bc2,
-                      double grad_scale, double max_norm) {
+                      double grad_scale, double max_norm, const c10::optional<at::Tensor>& scale_state) {
   check_flat(p, "param");
   check_flat(m, "exp_avg");
   check_flat(v, "exp_avg_sq");
@@ -260,6 +288,12 @@ void dlgm_adamw_step_(at::Tensor p, at::Tensor m, at::Tensor v, const at::Tensor
     TORCH_CHECK(stats->scalar_type() == at::kFloat && stats->numel() >= 2 && stats->is_cuda(), "adamw: bad stats");
     sp = stats->data_ptr<float>();
   }
+  const float* inv = nullptr;
+  if (scale_state.has_value() && scale_state->defined()) {
+    TORCH_CHECK(scale_state->is_cuda() && scale_state->scalar_type() == at::kFloat && scale_state->numel() >= 2,
+                "adamw: bad loss-scale state");
+    inv = scale_state->data_ptr<float>() + 1;
+  }
   if (n == 0) return;
   AdamHyper h{(float)lr, (float)beta1, (float)beta2, (float)eps, (float)weight_decay, (float)bc1, (float)bc2,
               (float)grad_scale, (float)max_norm};
@@ -270,11 +304,12 @@ void dlgm_adamw_step_(at::Tensor p, at::Tensor m, at::Tensor v, const at::Tensor
     PT* p16p = has16 ? reinterpret_cast<PT*>(p16->data_ptr()) : nullptr;
     if (g.scalar_type() == at::kFloat)
       adamw_kernel<float, PT><<<grid, kThreads, 0, stream>>>(p.data_ptr<float>(), m.data_ptr<float>(),
-                                                             v.data_ptr<float>(), g.data_ptr<float>(), p16p, sp, n, h);
+                                                             v.data_ptr<float>(), g.data_ptr<float>(), p16p, sp, inv, n,
+                                                             h);
     else
       DLGM_DISPATCH_16(g.scalar_type(), GT, adamw_kernel<GT, PT><<<grid, kThreads, 0, stream>>>(
                                                 p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
-                                                reinterpret_cast<const GT*>(g.data_ptr()), p16p, sp, n, h));
+                                                reinterpret_cast<const GT*>(g.data_ptr()), p16p, sp, inv, n, h));
   });
   DLGM_CHECK_HIP(hipGetLastError());
 }
@@ -308,5 +343,16 @@ void dlgm_cast_f32_bf16_(at::Tensor dst, const at::Tensor& src) {
   auto stream = c10::hip::getCurrentHIPStream();
   DLGM_DISPATCH_16(dst.scalar_type(), PT, cast_kernel<PT><<<stream_grid(n / 4), kThreads, 0, stream>>>(
                                              src.data_ptr<float>(), reinterpret_cast<PT*>(dst.data_ptr()), n));
+  DLGM_CHECK_HIP(hipGetLastError());
+}
+
+void dlgm_loss_scale_update_(at::Tensor state, const at::Tensor& stats, int64_t window, int64_t hysteresis,
+                             double min_scale) {
+  TORCH_CHECK(state.is_cuda() && state.scalar_type() == at::kFloat && state.numel() >= 4 && state.is_contiguous(),
+              "loss_scale_update: state must be a contiguous device fp32 [4]");
+  TORCH_CHECK(stats.is_cuda() && stats.scalar_type() == at::kFloat && stats.numel() >= 2, "loss_scale_update: stats");
+  loss_scale_update_kernel<<<1, 64, 0, c10::hip::getCurrentHIPStream()>>>(
+      state.data_ptr<float>(), stats.data_ptr<float>(), (float)std::max<int64_t>(1, window), (float)hysteresis,
+      (float)min_scale);
   DLGM_CHECK_HIP(hipGetLastError());
 }

@@ -361,7 +361,8 @@ class AsyncCheckpointer:
                 "client_state": client_state, "lr_scheduler": {"last_batch_iteration": step},
                 "param_shapes": [{f"{g['prefix']}.{p[0]}": p[2] for p in g["params"]} for g in groups],
                 "buffer_names": [], "module": None,
-                "loss_scaler": ({"cur_scale": eng.scaler.scale} if eng.scaler is not None else None)}
+                # DeepSpeed keeps the scaler in the checkpoint; restore resumes at the saved scale and counters
+                "loss_scaler": (eng.scaler.state_dict() if eng.scaler is not None else None)}
 
     @property
     def busy(self) -> bool:
@@ -537,17 +538,23 @@ class AsyncCheckpointer:
             if lo >= 0 and lo == hi and lo >= newest_disk:
                 cands.append(("shm", _tag(int(lo))))
         cands += [("disk", t) for t in disk]
+        touched = False  # some candidate wrote into the engine's state before failing
         for kind, t in cands:
             err = ""
             cs: Optional[Dict[str, Any]] = None
             t0 = time.time()
+            self._touched, self._loaded_meta = False, None
             try:
                 cs = self._load_shm() if kind == "shm" else self._load_tag(t, verify)
             except (CorruptCheckpoint, FileNotFoundError, OSError, KeyError, ValueError, RuntimeError) as e:
                 err = f"{type(e).__name__}: {e}"
+            touched = touched or self._touched
             t1 = time.time()
             if agree.min(0.0 if err else 1.0) > 0:
                 t2 = time.time()
+                ls = (self._loaded_meta or {}).get("loss_scaler")
+                if self.engine.scaler is not None and isinstance(ls, dict) and "cur_scale" in ls:
+                    self.engine.scaler.load_state_dict(ls)
                 self.engine.sync_params_from_master()
                 if self.cuda:
                     torch.cuda.synchronize(self.dev)
@@ -558,6 +565,11 @@ class AsyncCheckpointer:
             self.rollbacks.append(f"{kind}:{t}: {err or 'failed on another rank'}")
             if not auto:
                 raise CorruptCheckpoint(f"{t}: {err or 'failed on another rank'}")
+        if agree.max(1.0 if touched else 0.0) > 0:
+            # a candidate failed part-way through overwriting the optimizer state and no later one replaced
+            # it: the engine holds a mix of checkpoints, never something to train on (or to start from step 0)
+            raise CorruptCheckpoint("every checkpoint candidate failed after a partial restore: "
+                                    + "; ".join(self.rollbacks))
         return None
 
     def _src_sig(self) -> str:
@@ -581,53 +593,47 @@ class AsyncCheckpointer:
         slots = [torch.empty(piece, dtype=torch.uint8, pin_memory=self.cuda) for _ in range(2)]
         self.restore_stats["pin_s"] = round(time.time() - ta, 2)
         waited = [0.0, 0.0]  # [main thread waiting for a read, waiting for an H2D]
-        evs: List[Any] = [None, None]
         jobs = [(k, off, min(piece, end - off)) for k, off in enumerate(range(0, end, piece))]
         q: "queue.Queue" = queue.Queue(maxsize=1)
         free = [threading.Semaphore(1), threading.Semaphore(1)]
+        stop = threading.Event()  # set when the main loop gives up: the reader must not block forever
 
         tm = time.time()
         fmap = torch.from_file(self.shm_src_path, shared=True, size=os.path.getsize(self.shm_src_path),
                                dtype=torch.uint8) if _host.lib() is not None else None
         self.restore_stats["map_s"] = round(time.time() - tm, 2)
 
+        def put(item) -> bool:
+            while not stop.is_set():
+                try:
+                    q.put(item, timeout=0.05)
+                    return True
+                except queue.Full:
+                    pass
+            return False
+
         def reader():
             try:
                 for k, off, ln in jobs:
-                    free[k % 2].acquire()
+                    while not free[k % 2].acquire(timeout=0.05):
+                        if stop.is_set():
+                            return
                     if fmap is not None:
                         crcs = _host.copy_crc32c_chunks(fmap[off:off + ln], slots[k % 2][:ln])
                     else:
                         crcs = read_slot(self.shm_src_path, slots[k % 2][:ln], off)
-                    q.put((k, off, ln, crcs))
+                    if not put((k, off, ln, crcs)):
+                        return
             except Exception as e:  # noqa: BLE001
-                q.put(e)
+                put(e)
         th = threading.Thread(target=reader, daemon=True)
         tl = time.time()
         th.start()
-        for _ in jobs:
-            tw = time.time()
-            item = q.get()
-            waited[0] += time.time() - tw
-            if isinstance(item, Exception):
-                raise item
-            k, off, ln, crcs = item
-            first, nfull = off // _host.CHUNK, ln // _host.CHUNK  # a partial last chunk is verified below
-            if check and crcs[:nfull] != m["crc"][first:first + nfull]:
-                raise CorruptCheckpoint("shm snapshot: checksum mismatch")
-            src = slots[k % 2]
-            for base, dst in dsts:
-                lo, hi = max(off, base), min(off + ln, base + dst.numel())
-                if lo < hi:
-                    dst[lo - base:hi - base].copy_(src[lo - off:hi - off], non_blocking=True)
-            if self.cuda:
-                ev = torch.cuda.Event()
-                ev.record()
-                tw = time.time()
-                ev.synchronize()
-                waited[1] += time.time() - tw
-            free[k % 2].release()
-        th.join()
+        try:
+            self._restore_pieces(jobs, q, free, slots, dsts, m, check, waited)
+        finally:
+            stop.set()
+            th.join()
         self.restore_stats["loop_s"] = round(time.time() - tl, 2)
         tt = time.time()
         self.restore_stats.update(wait_read_s=round(waited[0], 2), wait_h2d_s=round(waited[1], 2),
@@ -642,7 +648,34 @@ class AsyncCheckpointer:
         # path, and the snapshot buffer the next save needs is this same file (_alloc_snapshot reuses it)
         self._restored_map = fmap
         eng.step_count = int(m["meta"]["global_steps"])
+        self._loaded_meta = m["meta"]
         return m["meta"].get("client_state", {})
+
+    def _restore_pieces(self, jobs, q, free, slots, dsts, m, check, waited) -> None:
+        """Main-thread half of the shm restore: verify each piece the reader copied and send it to the device."""
+        for _ in jobs:
+            tw = time.time()
+            item = q.get()
+            waited[0] += time.time() - tw
+            if isinstance(item, Exception):
+                raise item
+            k, off, ln, crcs = item
+            first, nfull = off // _host.CHUNK, ln // _host.CHUNK  # a partial last chunk is verified below
+            if check and crcs[:nfull] != m["crc"][first:first + nfull]:
+                raise CorruptCheckpoint("shm snapshot: checksum mismatch")
+            src = slots[k % 2]
+            self._touched = True
+            for base, dst in dsts:
+                lo, hi = max(off, base), min(off + ln, base + dst.numel())
+                if lo < hi:
+                    dst[lo - base:hi - base].copy_(src[lo - off:hi - off], non_blocking=True)
+            if self.cuda:
+                ev = torch.cuda.Event()
+                ev.record()
+                tw = time.time()
+                ev.synchronize()
+                waited[1] += time.time() - tw
+            free[k % 2].release()
 
     def _load_tag(self, tag: str, verify: bool) -> Dict[str, Any]:
         d = os.path.join(self.save_dir, tag)
@@ -660,6 +693,7 @@ class AsyncCheckpointer:
         old = mans.get(src)
         same = old is not None and json.dumps(old["layout"], sort_keys=True) == json.dumps(
             dict(self.layout, rank=src), sort_keys=True)
+        self._touched = True  # from here on the engine's state is being overwritten
         if same:
             info = old["files"][optim_file(src)]
             path = os.path.join(d, optim_file(src))
@@ -668,6 +702,7 @@ class AsyncCheckpointer:
         else:
             self._reshard_from(d, meta, mans, verify)
         self.engine.step_count = int(meta["global_steps"])
+        self._loaded_meta = meta
         return meta.get("client_state", {})
 
     def _read_into(self, path: str, info: Dict[str, Any], dst: torch.Tensor, verify: bool) -> None:

@@ -167,7 +167,7 @@ class Trainer:
         self.engine = ZeroEngine(self.mcfg, self.ecfg, self.env.device, self.comm)
         self.timeline["engine"] = time.time()
         self.monitor = LossSpikeMonitor(MonitorConfig())
-        self.trap = NanTrap(self.env.device, self.monitor)
+        self.trap = NanTrap(self.env.device, self.monitor, width=5)
         shm = {"auto": "auto", "on": True, "off": False}[args.ckpt_shm]
         self.ckpt = AsyncCheckpointer(self.engine, save_dir, mode=args.ckpt_mode, keep_last=args.keep_last, shm=shm,
                                       disk=bool(args.ckpt_disk)) if save_dir else None
@@ -223,12 +223,13 @@ class Trainer:
         rank takes the same halt / preemption decision at the same loop iteration."""
         v = self.trap.get(step)
         if v is None:
-            v = [float(x) for x in torch.cat([self.engine.stats, issued["m"]["loss"].reshape(1).float()]).tolist()]
-        ss, bad, flag, loss = v[0], v[1], v[2], v[3]
+            v = [float(x) for x in torch.cat([self.engine.stats, issued["m"]["loss"].reshape(1).float(),
+                                              issued["m"]["grad_norm"].reshape(1).float()]).tolist()]
+        ss, bad, flag, loss, gnorm = v[0], v[1], v[2], v[3], v[4]
         now = time.time()
         dt = now - self._t_last
         self._t_last = now
-        rec = {"step": step, "loss": loss, "grad_norm": math.sqrt(max(ss, 0.0)) * issued["inv_scale"],
+        rec = {"step": step, "loss": loss, "grad_norm": gnorm,
                "lr": issued["m"]["lr"], "step_s": dt, "tokens_per_sec": self._tokens_step / max(dt, 1e-9),
                "nonfinite": bad, "preempt": flag > 0}
         self.log.append(rec)
@@ -309,9 +310,10 @@ class Trainer:
                 m = self.engine.train_step(self.data.batches(step))
                 for _ in range(a.profile_steps - 1 if prof else 0):  # extra traced steps reuse this step's data
                     self.engine.train_step(self.data.batches(step))
-            inv = 1.0 / self.engine.scaler.scale if self.engine.scaler else 1.0
-            self.trap.record(step, torch.cat([self.engine.stats, m["loss"].reshape(1).float()]))
-            issued = {"m": m, "inv_scale": inv}
+            # [sum g^2, non-finite, flags, loss, unscaled grad norm]: the fp16 loss scale stays on the device
+            self.trap.record(step, torch.cat([self.engine.stats, m["loss"].reshape(1).float(),
+                                              m["grad_norm"].reshape(1).float()]))
+            issued = {"m": m}
             last = step
             # step t-1's outcome, read while step t runs on the device
             if prev is not None:

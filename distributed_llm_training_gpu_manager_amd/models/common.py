@@ -63,6 +63,8 @@ class StepContext:
     # units may keep weight-gradient operands across the step's micro-batches and run ONE GEMM with the
     # micro-batches concatenated along K at the last one (their gradients go straight to fp32 targets)
     defer_wgrad: bool = False
+    # fp16 path: the dynamic loss scale as a device word (multiplied into the loss gradient on the device)
+    loss_scale: Optional[torch.Tensor] = None
 
     @property
     def tokens(self) -> int:

@@ -118,7 +118,8 @@ class GPT2Head(Unit):
             torch.mm(h, w.t(), out=logits)
         else:
             logits = mm(h, w.t())
-        loss_rows, _ = ops.cross_entropy_fwd_bwd_(logits, ctx.labels.reshape(-1), ctx.grad_scale)
+        loss_rows, _ = ops.cross_entropy_fwd_bwd_(logits, ctx.labels.reshape(-1), ctx.grad_scale,
+                                                   scale=ctx.loss_scale)
         # logits now hold d(loss)/d(logits) (scaled by grad_scale); keep them for backward
         return loss_rows.sum(), (x, logits)
 

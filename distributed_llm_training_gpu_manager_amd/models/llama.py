@@ -207,7 +207,7 @@ class LlamaHead(Unit):
                 del logits
             return loss, (x, rstd, hn, None)
         logits = mm(hn, p["lm_head"].t())
-        loss_rows, _ = ops.cross_entropy_fwd_bwd_(logits, labels, ctx.grad_scale)
+        loss_rows, _ = ops.cross_entropy_fwd_bwd_(logits, labels, ctx.grad_scale, scale=ctx.loss_scale)
         # logits now hold d(loss)/d(logits); keep them for backward
         return loss_rows.sum(), (x, rstd, hn, logits)
 
@@ -221,7 +221,7 @@ class LlamaHead(Unit):
                 n = min(self.chunk_tokens, T - lo)
                 hc = hn.narrow(0, lo, n)
                 dl = mm(hc, p["lm_head"].t())
-                ops.cross_entropy_fwd_bwd_(dl, labels.narrow(0, lo, n), ctx.grad_scale)
+                ops.cross_entropy_fwd_bwd_(dl, labels.narrow(0, lo, n), ctx.grad_scale, scale=ctx.loss_scale)
                 grad_mm(g["lm_head"], dl.t(), hc, ctx.grad_acc or i > 0)
                 dhn.narrow(0, lo, n).copy_(dx_mm(dl, p, "lm_head"))
                 del dl

@@ -227,7 +227,8 @@ class MixtralBlock(LlamaBlock):
         if c.router_aux_coef > 0:
             # d(coef * mean_l aux_l)/d logits, times the micro-batch share of the loss (grad_scale * tokens)
             scale = c.router_aux_coef * E / (c.n_layers * T) * ctx.grad_scale * ctx.tokens
-            dlogits += scale * probs * (f - (probs * f).sum(-1, keepdim=True))
+            daux = scale * probs * (f - (probs * f).sum(-1, keepdim=True))
+            dlogits += daux * ctx.loss_scale if ctx.loss_scale is not None else daux
         dl = dlogits.to(hn2.dtype)
         grad_mm(g["router"], dl.t(), hn2, ctx.grad_acc)
         dhn2 = dhn2 + torch.mm(dl, p["router"])

@@ -6,7 +6,7 @@ the loss gradient in advance (1 / tokens), so no second sweep is needed.
 """
 from __future__ import annotations
 
-from typing import Tuple
+from typing import Optional, Tuple
 
 import torch
 
@@ -14,10 +14,13 @@ from .._native import hip_ops, use_native
 
 
 def cross_entropy_fwd_bwd_(logits: torch.Tensor, labels: torch.Tensor, grad_scale: float,
-                           ignore_index: int = -100, compute_grad: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Return (loss_per_row fp32 [T], lse fp32 [T]); logits [T, V] become the gradient in place."""
+                           ignore_index: int = -100, compute_grad: bool = True,
+                           scale: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Return (loss_per_row fp32 [T], lse fp32 [T]); logits [T, V] become the gradient in place, scaled by
+    grad_scale times the optional device word ``scale[0]`` (the fp16 path's dynamic loss scale, read on the
+    device: no host synchronisation)."""
     if use_native(logits):
-        return hip_ops().cross_entropy_(logits, labels, ignore_index, grad_scale, compute_grad)
+        return hip_ops().cross_entropy_(logits, labels, ignore_index, grad_scale, compute_grad, scale)
     x = logits.float()
     lse = torch.logsumexp(x, dim=-1)
     valid = labels != ignore_index
@@ -28,5 +31,7 @@ def cross_entropy_fwd_bwd_(logits: torch.Tensor, labels: torch.Tensor, grad_scal
         g = torch.softmax(x, dim=-1)
         g.scatter_add_(1, safe.unsqueeze(1), -torch.ones_like(picked).unsqueeze(1))
         g = g * (grad_scale * valid.float()).unsqueeze(1)
+        if scale is not None:
+            g = g * scale[0].to(g.device)
         logits.copy_(g.to(logits.dtype))
     return loss, lse

@@ -38,14 +38,17 @@ def grad_stats(grads: Sequence[torch.Tensor], out: torch.Tensor, accumulate: boo
 def adamw_step_(p: torch.Tensor, m: torch.Tensor, v: torch.Tensor, g: torch.Tensor,
                 p16: Optional[torch.Tensor], stats: Optional[torch.Tensor], *, lr: float, beta1: float,
                 beta2: float, eps: float, weight_decay: float, step: int, grad_scale: float = 1.0,
-                max_norm: float = 0.0) -> None:
+                max_norm: float = 0.0, scale_state: Optional[torch.Tensor] = None) -> None:
+    """scale_state: the device loss-scaler state [scale, 1/scale, ...]; its 1/scale multiplies grad_scale on
+    the device (fp16 path)."""
     bc1 = 1.0 - beta1 ** step
     bc2 = 1.0 - beta2 ** step
     if use_native(p):
         hip_ops().adamw_step_(p, m, v, g, p16, stats, lr, beta1, beta2, eps, weight_decay, bc1, bc2,
-                              grad_scale, max_norm)
+                              grad_scale, max_norm, scale_state)
         return
-    coef = grad_scale
+    coef = grad_scale * (float(scale_state[1]) if scale_state is not None else 1.0)
+    grad_scale = coef
     if stats is not None:
         if float(stats[1]) > 0:
             return
@@ -78,3 +81,24 @@ def cast_f32_bf16_(dst: torch.Tensor, src: torch.Tensor) -> None:
         hip_ops().cast_f32_bf16_(dst, src)
         return
     dst.copy_(src.to(dst.dtype))
+
+
+def loss_scale_update_(state: torch.Tensor, stats: torch.Tensor, window: int, hysteresis: int,
+                       min_scale: float) -> None:
+    """DeepSpeed dynamic loss-scale update on the device: state = [scale, 1/scale, good steps, hysteresis left],
+    stats[1] = non-finite gradient count of the step (no host synchronisation on the GPU)."""
+    if use_native(state):
+        hip_ops().loss_scale_update_(state, stats, int(window), int(hysteresis), float(min_scale))
+        return
+    scale, _, good, hyst = (float(x) for x in state[:4].tolist())
+    if float(stats[1]) > 0:
+        hyst -= 1
+        if hyst <= 0:
+            scale = max(scale / 2.0, min_scale)
+            hyst = hysteresis
+        good = 0
+    else:
+        good += 1
+        if good % max(1, window) == 0:
+            scale *= 2.0
+    state[:4] = torch.tensor([scale, 1.0 / scale, good, hyst], dtype=state.dtype)

@@ -220,11 +220,17 @@ class Comm:
                 dist.barrier(group=self.group)
 
     def new_group(self, ranks: List[int]) -> Optional["Comm"]:
-        """A sub-communicator over `ranks` of this communicator's world (collective: every rank calls it for
-        every group); None on ranks outside `ranks`."""
+        """A sub-communicator over `ranks` (indices into THIS communicator, mapped to global ranks) ; None on
+        ranks outside `ranks`. Collective over the DEFAULT group, as dist.new_group is: every rank of the job
+        calls it, for every group, in the same order -- also when it is called on a sub-communicator."""
         if self.world == 1:
             return Comm()
-        g = dist.new_group(ranks) if len(ranks) < dist.get_world_size() else dist.group.WORLD
+        # `ranks` index THIS communicator; dist.new_group takes global ranks
+        glob = [self._peer(r) for r in ranks]
+        if len(ranks) == self.world and self.group is None:
+            g = dist.group.WORLD
+        else:
+            g = dist.new_group(glob)
         return Comm(g) if self.rank in ranks else None
 
     def duplicate(self) -> "Comm":

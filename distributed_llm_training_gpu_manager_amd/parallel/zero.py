@@ -202,28 +202,41 @@ class _Scaled:
 
 
 class LossScaler:
-    """fp16 dynamic loss scaler kept on the device (DeepSpeed fp16 block semantics)."""
+    """fp16 dynamic loss scaler whose state lives on the device (DeepSpeed fp16 block semantics, reference
+    deepspeed_launcher.py:175-183).
+
+    ``state`` = [scale, 1/scale, good steps, hysteresis left] (fp32). The cross-entropy kernel multiplies
+    the loss gradient by ``state[0]``, AdamW unscales with ``state[1]`` and a one-thread kernel applies the
+    update rule from the step's non-finite count: a step never reads the scale on the host, so the
+    trainer's one-step-behind run-ahead holds on the fp16 path too. ``scale`` (a host read) is for
+    checkpoints, logs and tests.
+    """
 
     def __init__(self, cfg: EngineConfig, device):
         self.dynamic = cfg.loss_scale == 0
-        self.scale = float(cfg.loss_scale if cfg.loss_scale else 2.0 ** cfg.initial_scale_power)
+        s0 = float(cfg.loss_scale if cfg.loss_scale else 2.0 ** cfg.initial_scale_power)
         self.window, self.hyst, self.min_scale = cfg.loss_scale_window, cfg.hysteresis, cfg.min_loss_scale
-        self._good = 0
-        self._hyst_left = cfg.hysteresis
+        self.state = torch.tensor([s0, 1.0 / s0, 0.0, float(cfg.hysteresis)], dtype=torch.float32, device=device)
 
-    def update(self, overflow: bool) -> None:
-        if not self.dynamic:
-            return
-        if overflow:
-            self._hyst_left -= 1
-            if self._hyst_left <= 0:
-                self.scale = max(self.scale / 2.0, self.min_scale)
-                self._hyst_left = self.hyst
-            self._good = 0
-        else:
-            self._good += 1
-            if self._good % self.window == 0:
-                self.scale *= 2.0
+    @property
+    def scale(self) -> float:
+        return float(self.state[0])
+
+    def update_(self, stats: torch.Tensor) -> None:
+        """Apply the DeepSpeed rule to the step whose non-finite count is ``stats[1]`` (device, no sync)."""
+        if self.dynamic:
+            ops.loss_scale_update_(self.state, stats, self.window, self.hyst, self.min_scale)
+
+    def state_dict(self) -> Dict[str, Any]:
+        scale, _, good, hyst = (float(x) for x in self.state.tolist())
+        return {"cur_scale": scale, "cur_iter_good": int(good), "cur_hysteresis": int(hyst),
+                "dynamic": self.dynamic}
+
+    def load_state_dict(self, d: Dict[str, Any]) -> None:
+        scale = float(d["cur_scale"])
+        good = float(d.get("cur_iter_good", 0))
+        hyst = float(d.get("cur_hysteresis", self.hyst))
+        self.state.copy_(torch.tensor([scale, 1.0 / scale, good, hyst], dtype=torch.float32))
 
 
 def lr_at(cfg: EngineConfig, step: int) -> float:
@@ -703,6 +716,10 @@ class ZeroEngine:
             pending.append((g.comm.reduce_scatter(out, tgt, avg=avg, async_op=True), _Scaled(out, post, tgt)))
         elif g.comm.world > 1:  # ZeRO-0 / persistent (replicated) group: plain data parallel
             pending.append((g.comm.all_reduce(tgt, avg=avg, async_op=True), _Scaled(tgt, post)))
+        elif post != 1.0:
+            # no reduction for this group (W == 1, or an expert group at EP == W): the predivided gradient
+            # still gets its post-scale (factor / 1), or it would stay 1/factor too small
+            tgt.mul_(post)
 
     def _reduce_group_grad(self, gi: int, gbuf: torch.Tensor, first_micro: bool,
                            pending: List[Tuple[Handle, Any]]) -> None:
@@ -750,10 +767,9 @@ class ZeroEngine:
         gs = 1.0 / (B * S * self.cfg.grad_accum)
         if self.cfg.prescale_gradients:
             gs /= self.cfg.gradient_predivide_factor  # pre-divided before the SUM reductions
-        if self.scaler is not None:
-            gs *= self.scaler.scale
         return StepContext(batch=B, seq_len=S, input_ids=ids, labels=labels, grad_scale=gs, rope=self.rope,
-                           ep_group=self.ep_comm, sp_group=self.sp_comm)
+                           ep_group=self.ep_comm, sp_group=self.sp_comm,
+                           loss_scale=self.scaler.state[0:1] if self.scaler is not None else None)
 
     def micro_step(self, ids: torch.Tensor, labels: torch.Tensor, first: bool, last: bool) -> torch.Tensor:
         ctx = self._context(ids, labels)
@@ -913,15 +929,17 @@ class ZeroEngine:
         cfg = self.cfg
         self._global_grad_stats()
         lr = lr_at(cfg, self.step_count)
-        inv_scale = 1.0 / self.scaler.scale if self.scaler else 1.0
+        sst = self.scaler.state if self.scaler is not None else None
+        # the step's gradient norm, unscaled on the device before the scaler moves on
+        self.grad_norm = self.stats[0].sqrt() * sst[1] if sst is not None else self.stats[0].sqrt()
         if self.offload is not None:
-            self._offload_step(lr, inv_scale)
+            self._offload_step(lr, float(sst[1]) if sst is not None else 1.0)
         else:
             ops.adamw_step_(self.master, self.exp_avg, self.exp_avg_sq, self.grad_shard,
                             None if self.param_host else self.p16_shard,
                             self.stats, lr=lr,
                             beta1=cfg.betas[0], beta2=cfg.betas[1], eps=cfg.eps, weight_decay=cfg.weight_decay,
-                            step=self.step_count, grad_scale=inv_scale, max_norm=cfg.grad_clip)
+                            step=self.step_count, grad_scale=1.0, max_norm=cfg.grad_clip, scale_state=sst)
             if self.param_host:
                 self._p16_to_host()
         self._pver += 1  # the compute copy changes below: transposed caches are stale
@@ -934,7 +952,7 @@ class ZeroEngine:
             for h in hs:
                 h.wait()
         if self.scaler is not None:
-            self.scaler.update(bool(self.stats[1].item() > 0))
+            self.scaler.update_(self.stats)
         return {"lr": lr, "stats": self.stats}
 
     def _offload_step(self, lr: float, inv_scale: float) -> None:
@@ -964,8 +982,7 @@ class ZeroEngine:
             self._micro_loop(micro_batches)
         out = self.optimizer_step()
         tokens = sum(int(ids.numel()) for ids, _ in micro_batches)
-        metrics = {"loss": self.loss_acc / tokens, "grad_norm": self.stats[0].sqrt()
-                   * (1.0 / self.scaler.scale if self.scaler else 1.0),
+        metrics = {"loss": self.loss_acc / tokens, "grad_norm": self.grad_norm,
                    "nonfinite": self.stats[1], "lr": out["lr"], "step": self.step_count, "tokens": tokens}
         for hk in self.hooks:
             hk(self, metrics)
@@ -983,12 +1000,12 @@ class ZeroEngine:
 
         Single rank (every group P == 1: gradients land directly in the fp32 shard, no gather), dense
         model (MoE dispatch sizes are read on the host), no optimizer / activation offload (host
-        copies), no fp16 loss scaler (its scale is a host float baked into the gradient scale), no
-        per-phase timers (host-side event bookkeeping)."""
+        copies), no per-phase timers (host-side event bookkeeping). The fp16 loss scale is a device word
+        (LossScaler.state), so the fp16 path replays the same graph at every scale."""
         c = self.cfg
         return (c.hip_graphs and self.is_cuda and self.W == 1 and not self.has_experts and self.offload is None
                 and not self.param_host
-                and self.scaler is None and not c.cpu_checkpointing and not self.timers.enabled
+                and not c.cpu_checkpointing and not self.timers.enabled
                 and self.sp_size == 1 and self._graph_state != "failed")
 
     def _graphed_micro_loop(self, micro_batches: Sequence[Tuple[torch.Tensor, torch.Tensor]]) -> None:

@@ -1,9 +1,10 @@
 """bench.py driver contract, exercised on CPU/gloo with a tiny model.
 
-The round driver runs ``python -m torch.distributed.run --nnodes=1 --nproc-per-node N
---master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W`` and reads ONE JSON
-line from rank 0 with a fixed set of fields; the N > 1 path (process group, max over ranks, whole-job
-tokens/s) is checked here with two gloo ranks.
+The round driver runs either ``python bench.py --gpus N ...`` or ``python -m torch.distributed.run
+--nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K
+--warmup W`` and reads ONE JSON line from rank 0 with a fixed set of fields; both forms of the N > 1
+path (process group, max over ranks, whole-job tokens/s) are checked here with two gloo ranks, and a
+rank-count mismatch must fail instead of measuring one rank.
 """
 import json
 import os
@@ -24,9 +25,16 @@ def _port() -> int:
     return p
 
 
-def _run(cmd):
+def _env(**extra):
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
-    res = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "TORCHELASTIC_RUN_ID"):
+        env.pop(k, None)
+    env.update(extra)
+    return env
+
+
+def _run(cmd, **extra):
+    res = subprocess.run(cmd, cwd=ROOT, env=_env(**extra), capture_output=True, text=True, timeout=600)
     assert res.returncode == 0, res.stderr[-3000:]
     lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, res.stdout
@@ -62,3 +70,24 @@ def test_bench_torchrun_two_ranks():
     assert out["extra"]["zero3_allgathers_per_step"] > 0  # partitioned: the residency plan gathers once per unit
     ops = {r["op"] for r in out["extra"]["comm_busbw"]}  # the post-timing RCCL/xGMI sweep (gloo here)
     assert ops == {"all_gather", "mesh_all_gather", "reduce_scatter", "all_reduce", "all_to_all"}
+
+
+TINY = ["--steps", "2", "--warmup", "1", "--model", "llama-tiny", "--seq", "64", "--ga", "2", "--comm-sweep", "off"]
+
+
+def test_bench_self_launches_without_launcher():
+    """`python bench.py --gpus 2` with no launcher starts torch.distributed.run itself (a child process) and
+    reports a real 2-rank run -- never a silent one-rank number."""
+    out = _run([sys.executable, "bench.py", "--gpus", "2", *TINY])
+    _check(out, 2, 2, 1)
+    assert out["extra"]["launch"] == "torchrun"
+    assert out["extra"]["peak_GiB_max_over_ranks"] >= 0
+
+
+def test_bench_world_size_mismatch_fails():
+    res = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *TINY], cwd=ROOT,
+                         env=_env(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"), capture_output=True, text=True,
+                         timeout=300)
+    assert res.returncode != 0
+    assert not [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert "WORLD_SIZE" in res.stderr

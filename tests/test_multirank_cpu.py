@@ -541,6 +541,41 @@ def test_prescale_gradients_and_predivide_factor(tmp_path):
         assert float((res["pre"]["params"][k] - v).abs().max()) < 1e-4, k
 
 
+def _prescale_ep_worker(rank, world, port, kw, out):
+    _init(rank, world, port)
+    eng = ZeroEngine(_model("mixtral-tiny"), _cfg(3, 1, expert_parallel_size=world, **kw), torch.device("cpu"),
+                     Comm())
+    t = _data("mixtral-tiny", 1, world)[0][rank]
+    eng.micro_step(t[:, :-1], t[:, 1:], first=True, last=True)
+    grads = eng.full_grads()
+    if rank == 0:
+        torch.save(grads, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_prescale_groups_without_a_reduction(tmp_path):
+    """prescale_gradients on groups that issue no collective -- every group at W = 1, and the expert groups at
+    EP = W (their data-parallel communicator has one rank) -- still get the factor / 1 post-scale: the
+    gradients equal the default (AVG) ones instead of staying 1/factor too small (zero.py:752)."""
+    pre = {"prescale_gradients": True, "gradient_predivide_factor": 4.0}
+    for model in ("llama-tiny", "mixtral-tiny"):
+        _, g_avg = _single(model, 3, 2, 1)
+        _, g_pre = _single(model, 3, 2, 1, **pre)
+        for k, v in g_avg.items():
+            err = float((g_pre[k] - v).abs().max() / v.abs().max().clamp_min(1e-8))
+            assert err < 1e-5, (model, k, err)
+    res = {}
+    for name, kw in (("avg", {}), ("pre", pre)):
+        out = str(tmp_path / f"ep_{name}.pt")
+        mp.spawn(_prescale_ep_worker, args=(2, _port(), kw, out), nprocs=2, join=True)
+        res[name] = torch.load(out, weights_only=True)
+    assert any("experts" in k for k in res["avg"])
+    for k, v in res["avg"].items():
+        err = float((res["pre"][k] - v).abs().max() / v.abs().max().clamp_min(1e-8))
+        assert err < 1e-5, (k, err)
+
+
 def test_param_persistence_threshold_keeps_small_tensors_replicated(tmp_path):
     """stage3_param_persistence_threshold: norm weights (256 elements < 1e4) live in replicated '.persist'
     groups that are never all-gathered; training matches the fully partitioned layout."""

@@ -55,6 +55,54 @@ def test_corrupt_latest_rolls_back(tmp_path):
     assert cs["step"] == 2 and c.engine.step_count == 2 and "checksum" in c.ckpt.rollbacks[0]
 
 
+def _fp16_engine(seed=0):
+    mc = get_config("llama-tiny")
+    ec = EngineConfig(zero_stage=3, micro_batch_size=2, seq_len=32, grad_accum=1, lr=3e-3, scheduler="constant",
+                      init_device="cpu", fp16=True, initial_scale_power=24, hysteresis=2, loss_scale_window=1000,
+                      seed=seed)
+    return ZeroEngine(mc, ec, torch.device("cpu")), mc
+
+
+def test_fp16_loss_scaler_survives_checkpoint(tmp_path):
+    """The dynamic loss scale and its hysteresis / good-step counters are saved and restored (DeepSpeed keeps
+    the scaler in the checkpoint): a resumed fp16 run does not restart at 2**initial_scale_power and
+    overflow again (checkpoint.py:670)."""
+    eng, mc = _fp16_engine()
+    g = torch.Generator().manual_seed(0)
+    for _ in range(6):
+        t = torch.randint(0, mc.vocab_size, (2, 33), generator=g)
+        eng.train_step([(t[:, :-1], t[:, 1:])])
+    st = eng.scaler.state_dict()
+    assert st["cur_scale"] < 2.0 ** 24  # backed off from the initial scale
+    ck = AsyncCheckpointer(eng, str(tmp_path))
+    ck.save(6, {"step": 6}, blocking=True)
+    ck.close()
+    e2, _ = _fp16_engine(seed=5)
+    assert e2.scaler.scale == 2.0 ** 24
+    ck2 = AsyncCheckpointer(e2, str(tmp_path))
+    assert ck2.load("auto")["step"] == 6
+    assert e2.scaler.state_dict() == st
+    assert torch.equal(e2.scaler.state, eng.scaler.state)
+    ck2.close()
+
+
+def test_partial_restore_without_fallback_raises(tmp_path):
+    """A candidate that fails after overwriting part of the optimizer state, with no older candidate to
+    replace it, must not leave the engine to train from step 0 on a mix of checkpoints."""
+    from distributed_llm_training_gpu_manager_amd.ckpt.checkpoint import CorruptCheckpoint
+    b = _train(tmp_path, "--steps", "2", "--save-interval", "2")
+    b.run()
+    f = tmp_path / "global_step2" / "zero_pp_rank_0_mp_rank_00_optim_states.pt"
+    man = json.load(open(tmp_path / "global_step2" / "manifest_r0.json"))
+    info = man["files"]["zero_pp_rank_0_mp_rank_00_optim_states.pt"]["exp_avg"]  # master is read before it
+    data = bytearray(f.read_bytes())
+    data[info["offset"] + 100] ^= 0xFF
+    f.write_bytes(bytes(data))
+    c = _train(tmp_path, "--steps", "2")
+    with pytest.raises(CorruptCheckpoint, match="partial restore"):
+        c.ckpt.load("auto")
+
+
 def test_reshard_world_change(tmp_path):
     """Elastic restore: a W=1 ZeRO-3 checkpoint loaded into a different partition layout."""
     mc = get_config("llama-tiny")
