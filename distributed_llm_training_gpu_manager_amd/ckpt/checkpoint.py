@@ -131,7 +131,7 @@ class _Agree:
 class AsyncCheckpointer:
     def __init__(self, engine, save_dir: str, mode: str = "auto", keep_last: int = 3,
                  ring_bytes: int = 1 << 30, manifest_timeout_s: float = 600.0, shm: Any = "auto",
-                 disk: bool = True):
+                 disk: bool = True, module: Optional[bool] = None):
         self.engine = eng = engine
         self.save_dir = os.path.abspath(save_dir)
         self.keep_last = keep_last
@@ -175,6 +175,13 @@ class AsyncCheckpointer:
         self.rollbacks: List[str] = []
         self.restored_from: Optional[str] = None
         self._prep: Optional[threading.Thread] = None
+        # the 16-bit module state dict in mp_rank_00_model_states.pt (DeepSpeed: always for stages 0-2; stage 3
+        # with stage3_gather_16bit_weights_on_model_save): rank 0 keeps a pinned host copy per save
+        self.module = bool(module if module is not None else
+                           (eng.stage < 3 or getattr(eng.cfg, "gather_16bit_weights_on_model_save", True)))
+        self._mod_snap: Optional[torch.Tensor] = None
+        self._mod_index: List[Tuple[str, Tuple[int, ...], int]] = []  # (name, shape, element offset)
+        self._touched, self._loaded_meta = False, None
         self._thread = threading.Thread(target=self._writer, daemon=True, name="ckpt-writer")
         self._thread.start()
         eng.pre_step_hooks.append(self._before_optimizer_step)
@@ -338,13 +345,72 @@ class AsyncCheckpointer:
             for dst, s in srcs:
                 dst.copy_(s)
             ev = None
+        mod_ev = self._capture_module() if (self.module and self.disk) else None
         meta = self._meta(step, client_state or {})
+        meta["_module_ev"] = mod_ev
         with self._plock:
             self._pending += 1
         self._q.put((tag, step, save_id, ev, meta, t0))
         if blocking:
             self.wait()
         return tag
+
+    def _capture_module(self):
+        """Gather the 16-bit parameters group by group (a collective on every rank: ZeRO shards and EP experts)
+        and copy them, on rank 0, into a pinned host buffer on the snapshot stream. Returns what the writer
+        waits for before streaming the module into mp_rank_00_model_states.pt (True on CPU)."""
+        eng = self.engine
+        dt = eng.p16_shard.dtype
+        if self.is_rank0 and self._mod_snap is None:
+            off, idx = 0, []
+            for name, shp in eng.module_shapes():
+                idx.append((name, shp, off))
+                off += math.prod(shp)
+            self._mod_index = idx
+            self._mod_snap = torch.empty(off, dtype=dt, pin_memory=self.cuda)
+        pos = {n: (shp, o) for n, shp, o in self._mod_index}
+        cur = torch.cuda.current_stream(self.dev) if self.cuda else None
+        for items in eng.iter_full(eng.master, dt):
+            if not self.is_rank0:
+                continue
+            for name, t in items:
+                shp, o = pos[name]
+                dst = self._mod_snap[o:o + t.numel()]
+                if self.cuda:
+                    self._stream.wait_stream(cur)
+                    with torch.cuda.stream(self._stream):
+                        dst.copy_(t.reshape(-1), non_blocking=True)
+                    t.record_stream(self._stream)
+                else:
+                    dst.copy_(t.reshape(-1))
+        if not self.is_rank0:
+            return None
+        if not self.cuda:
+            return True
+        ev = torch.cuda.Event()
+        ev.record(self._stream)
+        return ev
+
+    def _write_model0(self, path: str, meta: Dict[str, Any], mod_ev) -> None:
+        meta = {k: v for k, v in meta.items() if k != "_module_ev"}
+        if mod_ev is None or self._mod_snap is None:
+            torch.save(meta, path)
+            return
+        if mod_ev is not True:
+            while not mod_ev.query():
+                time.sleep(0.0005)
+        dt = self._mod_snap.dtype
+        meta["module"] = {name: Slot("module/" + name, dt, shp) for name, shp, _ in self._mod_index}
+        w = PtWriter(path, meta)
+        for name, shp, o in self._mod_index:
+            self._stream_host(w, "module/" + name, self._mod_snap[o:o + math.prod(shp)])
+        w.close(fsync=True)
+
+    def _stream_host(self, w: PtWriter, name: str, src: torch.Tensor) -> None:
+        """Write a host tensor into slot `name` in ring-sized pieces."""
+        per = self.ring_elems * 4 // src.element_size()
+        for off in range(0, src.numel(), per):
+            w.write(name, src[off:off + per], off * src.element_size())
 
     def _meta(self, step: int, client_state: Dict[str, Any]) -> Dict[str, Any]:
         eng = self.engine
@@ -427,7 +493,8 @@ class AsyncCheckpointer:
             tmpm = self.shm_meta + ".tmp"
             with open(tmpm, "w") as f:
                 json.dump({"save_dir": self.save_dir, "step": step, "save_id": save_id, "sig": self.sig,
-                           "bytes": self.snap_bytes, "crc": crcs, "algo": _host.algo(), "meta": meta}, f)
+                           "bytes": self.snap_bytes, "crc": crcs, "algo": _host.algo(),
+                           "meta": {k: v for k, v in meta.items() if k != "_module_ev"}}, f)
             os.replace(tmpm, self.shm_meta)
             rec["shm_s"] = time.time() - t_cap
         if not self.disk:
@@ -461,7 +528,7 @@ class AsyncCheckpointer:
         self._stream_slot(w, "bf16", v["bf16"])
         files[model_file(self.rank)] = w.close(fsync=True)
         if self.is_rank0:
-            torch.save(meta, os.path.join(tmp, MODEL0))
+            self._write_model0(os.path.join(tmp, MODEL0), meta, meta.get("_module_ev"))
         man = {"rank": self.rank, "save_id": save_id, "step": step, "layout": lay, "files": files}
         mtmp = os.path.join(tmp, f".manifest_r{self.rank}.json")
         with open(mtmp, "w") as f:
@@ -681,7 +748,8 @@ class AsyncCheckpointer:
         d = os.path.join(self.save_dir, tag)
         if not os.path.exists(os.path.join(d, "COMPLETE")):
             raise CorruptCheckpoint("missing COMPLETE marker")
-        meta = torch.load(os.path.join(d, MODEL0), weights_only=True)
+        # mmap: the module state dict (16-bit weights) in this file is not read by a restore
+        meta = torch.load(os.path.join(d, MODEL0), weights_only=True, mmap=True)
         mans = {}
         for r in meta["writers"]:
             with open(os.path.join(d, f"manifest_r{r}.json")) as f:

@@ -49,7 +49,7 @@ def consolidate(save_dir: str, tag: Optional[str] = None, state: str = "master",
     """Full parameters (or an optimizer moment, ``state`` = exp_avg / exp_avg_sq) of one checkpoint."""
     assert state in STATE, state
     d = os.path.join(save_dir, _resolve_tag(save_dir, tag))
-    meta = torch.load(os.path.join(d, MODEL0), weights_only=True)
+    meta = torch.load(os.path.join(d, MODEL0), weights_only=True, mmap=True)
     mans = {}
     for r in meta["writers"]:
         with open(os.path.join(d, f"manifest_r{r}.json")) as f:

@@ -114,6 +114,31 @@ class GPUFleetStatus(BaseModel):
     source: str = "none"  # amdsmi | amd-smi-cli | nvidia-smi | mock | none
 
 
+# PCI device ids of the CDNA4 parts (amdsmi asic_info.device_id): used when the marketing name is generic
+_DEVICE_NAMES = {"0x75a3": "AMD Instinct MI355X", "0x75a2": "AMD Instinct MI350X"}
+_GENERIC = ("", "n/a", "amd radeon graphics", "amd instinct gpu", "unknown gpu")
+
+
+def market_name(asic: Dict[str, Any], board: Optional[Dict[str, Any]] = None) -> str:
+    """The product name of a GPU from amdsmi ASIC / board info. ``asic.market_name`` comes from libdrm's
+    amdgpu.ids table; where that file is missing it reads "AMD Radeon Graphics" for every part (seen on the
+    MI355X boxes), so fall back to the board FRU product name, then to the PCI device id, then to the gfx
+    target (gfx950 = CDNA4 / MI350 series)."""
+    asic, board = asic or {}, board or {}
+    name = str(asic.get("market_name", "") or "").strip()
+    if name.lower() not in _GENERIC:
+        return name
+    prod = str(board.get("product_name", "") or "").strip()
+    if prod.lower() not in _GENERIC:
+        return prod
+    dev = str(asic.get("device_id", "") or "").lower()
+    if dev in _DEVICE_NAMES:
+        return _DEVICE_NAMES[dev]
+    if str(asic.get("target_graphics_version", "")) == "gfx950":
+        return "AMD Instinct MI350-series (gfx950)"
+    return name or "AMD Instinct GPU"
+
+
 def _num(v: Any, default: float = 0.0) -> float:
     """amd-smi JSON values are numbers, {"value": x, "unit": u} dicts or "N/A" strings."""
     if isinstance(v, dict):
@@ -193,6 +218,7 @@ class GPUManager:
                     except Exception:
                         return default
                 asic = safe(lib.amdsmi_get_gpu_asic_info, default={}) or {}
+                board = safe(lib.amdsmi_get_gpu_board_info, default={}) or {}
                 enum = safe(lib.amdsmi_get_gpu_enumeration_info, default={}) or {}
                 act = safe(lib.amdsmi_get_gpu_activity, default={}) or {}
                 vram = safe(lib.amdsmi_get_gpu_vram_usage, default={}) or {}
@@ -222,7 +248,7 @@ class GPUManager:
                 limit_uw = _num(pw.get("power_limit"))
                 devs.append(self._make_device(
                     index=int(enum.get("hip_id", idx)) if isinstance(enum.get("hip_id", idx), int) else idx,
-                    name=str(asic.get("market_name", "AMD Instinct GPU")),
+                    name=market_name(asic, board),
                     uuid=str(safe(lib.amdsmi_get_gpu_device_uuid, default="") or ""),
                     pci=str(safe(lib.amdsmi_get_gpu_device_bdf, default="") or ""),
                     util=_num(act.get("gfx_activity")), mem_act=_opt(act.get("umc_activity")),
@@ -234,7 +260,8 @@ class GPUManager:
                     driver=str(drv.get("driver_version", "")), rocm=rocm, procs=procs,
                     ecc_c=int(_num(ecc.get("correctable_count"))), ecc_u=int(_num(ecc.get("uncorrectable_count"))),
                     links=links, vendor=str(asic.get("vendor_name", "AMD")),
-                    arch="gfx950" if "MI35" in str(asic.get("market_name", "")) else ""))
+                    arch=str(asic.get("target_graphics_version", "")) or
+                    ("gfx950" if "MI35" in market_name(asic, board) else "")))
             return devs
 
     # ------------------------------------------------------------------ amd-smi CLI JSON
@@ -324,14 +351,15 @@ class GPUManager:
             used = int(_num(mem.get("used_vram")))
             numa = s.get("numa", {})
             devs.append(self._make_device(
-                index=g, name=str(asic.get("market_name", "AMD Instinct GPU")), uuid=str(asic.get("asic_serial", "")),
+                index=g, name=market_name(asic, s.get("board", {})), uuid=str(asic.get("asic_serial", "")),
                 pci=str(bus.get("bdf", "")), util=_num(usage.get("gfx_activity")), mem_act=_opt(usage.get("umc_activity")),
                 total=total, used=used, power=_num(power.get("socket_power")), limit=limit,
                 hot=_int_or_none(temp.get("hotspot")), hbm=_int_or_none(temp.get("mem")), edge=_int_or_none(temp.get("edge")),
                 driver=str(drv.get("version", "")), rocm="", procs=procs_by.get(g, []),
                 ecc_c=int(_num(ecc.get("total_correctable_count"))), ecc_u=int(_num(ecc.get("total_uncorrectable_count"))),
                 links=links_by.get(g, []), vendor=str(asic.get("vendor_name", "AMD")),
-                arch="gfx950" if "MI35" in str(asic.get("market_name", "")) else "",
+                arch=str(asic.get("target_graphics_version", "")) or
+                ("gfx950" if "MI35" in market_name(asic, s.get("board", {})) else ""),
                 numa=int(_num(numa.get("node"))) if isinstance(numa, dict) and "node" in numa else None))
         return devs
 

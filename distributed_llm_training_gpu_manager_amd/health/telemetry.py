@@ -10,6 +10,7 @@ is a ctypes binding, so the GIL is released during every query and the training 
 """
 from __future__ import annotations
 
+import re
 import threading
 import time
 from typing import Any, Dict, List, Optional
@@ -61,8 +62,12 @@ class TelemetrySampler:
         self.links: Dict[str, int] = {}
         self.ecc_uncorrectable = 0
         self.worst = "healthy"
-        self.alerts: List[str] = []
+        # one entry per distinct alert (numbers masked: "Power 1359W near limit" and "Power 1379W ..." are one
+        # alert), {message (latest wording), count, first_s, last_s} -- the reference's message formats are
+        # kept (gpu_manager.py:93-98, 301-305), repeated samples are counted instead of listed
+        self.alerts: Dict[str, Dict[str, Any]] = {}
         self.name = ""
+        self._t0 = time.time()
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
 
@@ -101,9 +106,15 @@ class TelemetrySampler:
         h = getattr(d.health, "value", str(d.health))
         if rank.get(h, 0) > rank.get(self.worst, 0):
             self.worst = h
+        now = round(time.time() - self._t0, 1)
         for a in d.alerts:
-            if a not in self.alerts and len(self.alerts) < 20:
-                self.alerts.append(a)
+            key = re.sub(r"\d+(\.\d+)?", "#", a)
+            e = self.alerts.get(key)
+            if e is None:
+                if len(self.alerts) < 20:
+                    self.alerts[key] = {"message": a, "count": 1, "first_s": now, "last_s": now}
+            else:
+                e.update(message=a, count=e["count"] + 1, last_s=now)
 
     def _loop(self) -> None:
         while not self._stop.is_set():
@@ -132,7 +143,7 @@ class TelemetrySampler:
             if s is not None:
                 out[k] = s
         if self.alerts:
-            out["alerts"] = self.alerts
+            out["alerts"] = list(self.alerts.values())
         if self.errors and not self.samples:
             out["errors"] = self.errors
         return out

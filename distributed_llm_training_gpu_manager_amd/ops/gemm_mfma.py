@@ -1,11 +1,13 @@
-"""Python entry points of the hand-written MFMA GEMM (csrc/kernels/gemm_mfma.hip).
+"""Python entry points of the expert-grouped and hand-written MFMA GEMMs.
 
-``mfma_mm(out, a, b, acc)``   out (+)= a @ b for bf16 operand views of any unit-stride layout
+``mfma_mm(out, a, b, acc)``   out (+)= a @ b for bf16 operand views of any unit-stride layout (gemm_mfma.hip)
 ``grouped_mm(x, w, offsets)`` expert-grouped forward / input-gradient GEMM (rows split by offsets)
 ``grouped_wgrad(out, a, b, offsets)`` expert-grouped weight gradient (reduction rows split by offsets)
 
 The group offsets are an int32 device tensor, so an MoE layer launches its expert GEMMs without
-reading the routing counts on the host. CPU tensors take an fp32 reference path (tests).
+reading the routing counts on the host. Two device backends: hipBLASLt's grouped GEMM driven by
+device-side user arguments (csrc/kernels/gemm_grouped_lt.hip, the default) and the hand-written
+grouped MFMA kernel (gemm_mfma.hip). CPU tensors take an fp32 reference path (tests).
 """
 from __future__ import annotations
 
@@ -17,15 +19,19 @@ import torch
 from .._native import hip_ops, use_native
 
 DENSE, GROUP_M, GROUP_K = 0, 1, 2
-# Expert GEMM strategy (DLGM_MOE_GROUPED): "1" every expert GEMM as one grouped MFMA launch (device offsets,
-# no host read of the routing counts); "wgrad" only the weight gradients grouped (dX / forward per expert
-# through hipBLASLt, which needs the counts on the host once per layer); "0" the per-expert hipBLASLt loop.
-# Default "0": on Mixtral-8x7B (2 layers, seq 4096, GA 4, one MI355X) the loop measured 117.8k tok/s, the
-# grouped dW 111.0k and all-grouped 107.5k (profiles/mixtral_grouped_ab_r02.json): the grouped kernel's
-# 256x256x64 8-phase pipeline reaches 0.9-1.3 PF/s, below hipBLASLt's per-expert solutions.
-_MODE = os.environ.get("DLGM_MOE_GROUPED", "0")
-GROUPED = _MODE == "1"
-GROUPED_WGRAD = _MODE in ("1", "wgrad") and os.environ.get("DLGM_MOE_GROUPED_WGRAD", "1") != "0"
+# Expert GEMM strategy (DLGM_MOE_GROUPED):
+#   "lt"    (default) every expert GEMM as one hipBLASLt grouped GEMM whose per-expert sizes and pointers a
+#           HIP kernel writes into a device argument array from the routing offsets: no host read at all;
+#   "1"     the same with the hand-written grouped MFMA kernel;
+#   "wgrad" only the weight gradients grouped (MFMA), forward / dX per expert through hipBLASLt (host counts);
+#   "0"     the per-expert hipBLASLt loop (reads the routing counts on the host once per layer).
+# Round 2 measured (Mixtral-8x7B, 2 layers, seq 4096, GA 4): loop 117.8k tok/s, grouped MFMA dW 111.0k,
+# all-grouped MFMA 107.5k (profiles/mixtral_grouped_ab_r02.json).
+_MODE = os.environ.get("DLGM_MOE_GROUPED", "lt")
+GROUPED = _MODE in ("1", "lt")
+BACKEND = "lt" if _MODE == "lt" else "mfma"
+GROUPED_WGRAD = _MODE in ("1", "lt", "wgrad") and os.environ.get("DLGM_MOE_GROUPED_WGRAD", "1") != "0"
+LT_ALGO = int(os.environ.get("DLGM_MOE_LT_ALGO", "-1"))  # hipBLASLt heuristic rank to use (-1: the first)
 
 def _ok(t: torch.Tensor) -> bool:
     return t.dtype == torch.bfloat16 and t.data_ptr() % 16 == 0
@@ -53,6 +59,8 @@ def grouped_supported(x: torch.Tensor, wgrad: bool = False) -> bool:
     """Can the grouped kernels take rows `x` (bf16, row-major, 16-B aligned, on the GPU with the extension)?
     wgrad: asking for the weight-gradient GEMMs only (GROUPED_WGRAD), else for all expert GEMMs (GROUPED)."""
     on = GROUPED_WGRAD if wgrad else GROUPED
+    if BACKEND == "lt" and x.dtype == torch.float16:
+        return on and use_native(x) and x.is_contiguous() and x.dim() == 2
     return on and use_native(x) and _ok(x) and x.dim() == 2 and x.stride(1) == 1 and x.stride(0) % 8 == 0
 
 
@@ -78,6 +86,9 @@ def grouped_mm(x: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, transpos
     if out is None:
         out = torch.empty(R, N, dtype=x.dtype, device=x.device)
     if use_native(x):
+        if BACKEND == "lt":
+            hip_ops().grouped_lt(out, x.contiguous(), w.contiguous(), offsets, 0, transpose_w, 0.0, LT_ALGO)
+            return out
         b = w.transpose(1, 2) if transpose_w else w
         hip_ops().gemm_mfma(out, x, b, False, offsets, GROUP_M, R, N, K, G, w.stride(0))
         return out
@@ -95,6 +106,9 @@ def grouped_wgrad(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, offsets: 
     """out[e] (+)= a[rows of e]^T @ b[rows of e]: a [R, M], b [R, N] row-major (token rows), out [G, M, N]."""
     G, M, N = out.shape
     if use_native(out):
+        if BACKEND == "lt":
+            hip_ops().grouped_lt(out, a.contiguous(), b.contiguous(), offsets, 1, False, 1.0 if acc else 0.0, LT_ALGO)
+            return out
         hip_ops().gemm_mfma(out, a.t(), b, acc, offsets, GROUP_K, M, N, a.shape[0], G, 0)
         return out
     offs = offsets.tolist()

@@ -8,8 +8,13 @@ ring). Expert-data-parallel groups hold the same experts (rank i, i+ep, ...) and
 carry the ZeRO partitioning of the expert weights.
 
 The dispatcher moves permuted token rows to the ranks that own their experts and
-back with ``all_to_all_single`` and uneven splits; the split sizes are exchanged
-first (one tiny all-to-all + one host read per MoE layer and direction).
+back with ``all_to_all_single`` and uneven splits. The split sizes are exchanged
+first (one tiny all-to-all of the [W, El] count matrix) and read on the host ONCE per
+MoE layer and micro-batch -- the send and receive counts in a single device-to-host
+copy, because RCCL's uneven all-to-all takes its split sizes on the host; the
+backward reuses the forward's splits (no exchange, no read). The permutation from the
+received [source rank][local expert] order to local-expert-major order is built on the
+device (``_regroup_index``), never as a host list.
 """
 from __future__ import annotations
 
@@ -64,6 +69,22 @@ class DispatchCtx:
         return self.local_counts
 
 
+def _regroup_index(mat: torch.Tensor, total: int) -> torch.Tensor:
+    """Device permutation of the received rows, [source rank][local expert] order -> [local expert][source
+    rank] order: entry j of the output is the received row that goes to position j. mat [W, El] counts (on the
+    device); `total` = mat.sum() (known on the host). No host list, no host-to-device copy of indices."""
+    W, El = mat.shape
+    dev = mat.device
+    if total == 0:
+        return torch.zeros(0, dtype=torch.long, device=dev)
+    m = mat.to(torch.long)
+    src_start = (m.reshape(-1).cumsum(0) - m.reshape(-1)).view(W, El)  # block (s, e) in received order
+    mt = m.t().reshape(-1)  # blocks in output order (e, s)
+    dst_start = mt.cumsum(0) - mt
+    shift = src_start.t().reshape(-1) - dst_start  # received position - output position, per block
+    return torch.arange(total, device=dev) + torch.repeat_interleave(shift, mt, output_size=total)
+
+
 class ExpertDispatcher:
     def __init__(self, ep_comm: Optional[Comm], n_experts: int):
         self.comm = ep_comm
@@ -84,20 +105,17 @@ class ExpertDispatcher:
             return x_sorted, DispatchCtx([x_sorted.shape[0]], [x_sorted.shape[0]], None, None, offsets)
         recv = torch.empty_like(counts)
         self.comm.all_to_all_single(recv, counts.contiguous())  # [src, local expert] counts
-        c_send = counts.view(self.W, self.El).sum(1).tolist()
-        mat = recv.view(self.W, self.El).cpu()
+        # the only host read of the layer: send counts and received [src, local expert] counts in one copy
+        both = torch.cat([counts.reshape(-1), recv.reshape(-1)]).to(torch.int64).cpu()
+        mat = both[self.E:].view(self.W, self.El)
+        c_send = both[:self.E].view(self.W, self.El).sum(1).tolist()
         c_recv = mat.sum(1).tolist()
         out = x_sorted.new_empty((sum(c_recv), x_sorted.shape[1]))
         self.comm.all_to_all_single(out, x_sorted.contiguous(), c_recv, c_send)
-        # received rows are [src][local expert]; regroup to [local expert][src]
-        offs = torch.zeros(self.W, self.El, dtype=torch.long)
-        flat = mat.reshape(-1)
-        starts = torch.cumsum(flat, 0) - flat
-        offs = starts.view(self.W, self.El)
-        idx = [torch.arange(int(offs[s, e]), int(offs[s, e] + mat[s, e])) for e in range(self.El) for s in range(self.W)]
-        regroup = torch.cat(idx).to(x_sorted.device) if idx else torch.zeros(0, dtype=torch.long, device=x_sorted.device)
+        regroup = _regroup_index(recv.view(self.W, self.El), sum(c_recv))
         lc = mat.sum(0).tolist()
-        lo = torch.tensor([0] + lc, dtype=torch.int32).cumsum(0, dtype=torch.int32).to(x_sorted.device, non_blocking=True)
+        lo = torch.zeros(self.El + 1, dtype=torch.int32, device=x_sorted.device)
+        lo[1:] = recv.view(self.W, self.El).sum(0).cumsum(0)
         ctx = DispatchCtx(c_send, c_recv, regroup, lc, lo)
         return out.index_select(0, regroup), ctx
 

@@ -128,6 +128,10 @@ class EngineConfig:
     # next block and the reduce-scatter of the previous block's gradients run concurrently on xGMI
     separate_gather_comm: bool = True
     tuned_gemms: bool = True  # load TunableOp results for this model if present (utils/gemm_tuning.py)
+    # checkpoints carry the full 16-bit module state dict in mp_rank_00_model_states.pt (DeepSpeed does for
+    # stages 0-2; for stage 3 only with stage3_gather_16bit_weights_on_model_save, which the reference sets:
+    # deepspeed_launcher.py:74, 192) -- gathered group by group at save time (ckpt/checkpoint.py)
+    gather_16bit_weights_on_model_save: bool = True
     # keep W^T of the big 2-D weights while the compute copy is stationary (P == 1, ZeRO-0/1/2): the
     # input-gradient GEMMs then run with both operands K-contiguous (refreshed once per optimizer step)
     transposed_weight_cache: bool = True
@@ -1064,24 +1068,45 @@ class ZeroEngine:
         return self._gather_flat(self.grad_shard)
 
     def _gather_flat(self, buf: torch.Tensor) -> Dict[str, torch.Tensor]:
-        out = {}
+        return {k: v for grp in self.iter_full(buf) for k, v in grp}
+
+    def module_shapes(self) -> List[Tuple[str, Tuple[int, ...]]]:
+        """(name, full shape) of every parameter in iter_full order (experts: all EP ranks' experts)."""
+        out = []
+        epw = self.ep_comm.world if (self.ep_comm is not None and self.ep_comm.world > 1) else 1
+        for g in self.groups:
+            for s in g.specs:
+                shp = tuple(s.shape)
+                if g.kind == "expert" and epw > 1:
+                    shp = (shp[0] * epw, *shp[1:])
+                out.append((f"{g.prefix}.{s.name}", shp))
+        return out
+
+    def iter_full(self, buf: torch.Tensor, dtype: Optional[torch.dtype] = None):
+        """Per group, the list of (name, full tensor) of flat state `buf` (master / grads): ZeRO shards
+        all-gathered, expert tensors concatenated over the EP ranks (global expert order). Collective -- every
+        rank runs the whole loop; one group is materialised at a time (checkpoint module capture streams it).
+        `dtype`: cast the shard first (16-bit module state: half the gather bytes)."""
         for g in self.groups:
             shard = buf.narrow(0, g.shard_off, g.shard_numel)
             if shard.device != self.device:  # offloaded optimizer state: collectives run on device tensors
                 shard = shard.to(self.device)
+            if dtype is not None and shard.dtype != dtype:
+                shard = shard.to(dtype)
             if g.P > 1:
-                full = torch.empty(g.numel, dtype=torch.float32, device=self.device)
+                full = torch.empty(g.numel, dtype=shard.dtype, device=self.device)
                 g.comm.all_gather(full, shard, async_op=False).wait()
             else:
                 full = shard
+            items = []
             for k, v in g.views(full).items():
                 v = v.clone()
                 if g.kind == "expert" and self.ep_comm is not None and self.ep_comm.world > 1:
                     parts = torch.empty((self.ep_comm.world, *v.shape), dtype=v.dtype, device=v.device)
                     self.ep_comm.all_gather(parts.view(-1), v.reshape(-1), async_op=False).wait()
                     v = parts.reshape(-1, *v.shape[1:])
-                out[f"{g.prefix}.{k}"] = v
-        return out
+                items.append((f"{g.prefix}.{k}", v))
+            yield items
 
     def memory_report(self) -> Dict[str, float]:
         gb = 1024 ** 3

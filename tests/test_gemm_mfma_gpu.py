@@ -61,7 +61,15 @@ def test_weight_gradient_shape_accumulates_into_fp32():
     assert _rel(w, ref) < 1e-5
 
 
-def test_grouped_rows_forward_uneven_and_empty_groups():
+@pytest.fixture(params=["lt", "mfma"])
+def backend(request, monkeypatch):
+    """Both grouped backends: hipBLASLt grouped GEMM with device-side user arguments (the default), and the
+    hand-written grouped MFMA kernel."""
+    monkeypatch.setattr(gm, "BACKEND", request.param)
+    return request.param
+
+
+def test_grouped_rows_forward_uneven_and_empty_groups(backend):
     g = torch.Generator(device=dev).manual_seed(2)
     sizes = [300, 0, 1, 513, 256, 77]
     R, K, N, G = sum(sizes), 512, 512, len(sizes)
@@ -85,7 +93,7 @@ def test_grouped_rows_forward_uneven_and_empty_groups():
         lo += n
 
 
-def test_grouped_weight_gradient_uneven_and_empty_groups():
+def test_grouped_weight_gradient_uneven_and_empty_groups(backend):
     g = torch.Generator(device=dev).manual_seed(3)
     sizes = [130, 0, 700, 1]
     R, M, N, G = sum(sizes), 512, 256, len(sizes)
@@ -107,3 +115,34 @@ def test_grouped_weight_gradient_uneven_and_empty_groups():
             assert _rel(out[e], ref) < 1e-5, e
             assert _rel(out2[e], ref + acc[e]) < 1e-5, e
         lo += n
+
+
+def test_grouped_lt_reads_nothing_on_the_host():
+    """The hipBLASLt grouped path takes the routing offsets on the device only: the same call with other
+    offsets (same total rows) reuses the cached plan and needs no host read -- run it inside a HIP graph
+    capture, which fails on any synchronising call."""
+    if gm.BACKEND != "lt":
+        pytest.skip("hipBLASLt grouped backend not selected")
+    g = torch.Generator(device=dev).manual_seed(5)
+    R, K, N, G = 1024, 512, 768, 8
+    x = torch.randn(R, K, device=dev, generator=g).to(torch.bfloat16)
+    w = torch.randn(G, N, K, device=dev, generator=g).to(torch.bfloat16)
+    offs = torch.tensor([0, 100, 100, 400, 401, 700, 900, 1000, 1024], dtype=torch.int32, device=dev)
+    out = gm.grouped_mm(x, w, offs)  # plan creation (host work) outside the capture
+    torch.cuda.synchronize()
+    offs2 = torch.tensor([0, 0, 512, 512, 513, 600, 600, 1000, 1024], dtype=torch.int32, device=dev)
+    s = torch.cuda.Stream()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        gm.grouped_mm(x, w, offs2, out=out)  # warm the stream
+        torch.cuda.synchronize()
+        with torch.cuda.graph(graph, stream=s):
+            gm.grouped_mm(x, w, offs2, out=out)
+    out.zero_()
+    graph.replay()
+    torch.cuda.synchronize()
+    o = offs2.tolist()
+    for e in range(G):
+        if o[e + 1] > o[e]:
+            ref = x[o[e]:o[e + 1]].float() @ w[e].float().t()
+            assert _rel(out[o[e]:o[e + 1]], ref) < 1e-2, e

@@ -88,3 +88,44 @@ def test_nvidia_parsers_for_mixed_fleets():
     csv = "0, NVIDIA H100, GPU-1, 45, 10, 5, 1000, 81559, 80559, [Not Supported], [N/A], [Not Supported]\n"
     d = m.parse_csv(csv)[0]  # A6: no crash on [Not Supported]
     assert d.temperature_celsius == 45 and d.power_draw_watts == 0.0
+
+
+def test_market_name_falls_back_when_libdrm_name_is_generic():
+    """On the MI355X boxes libdrm's amdgpu.ids is missing and asic.market_name reads "AMD Radeon Graphics":
+    the device is named from the board FRU product name, then the PCI device id, then the gfx target."""
+    from distributed_llm_training_gpu_manager_amd.health.gpu_manager import market_name
+    asic = {"market_name": "AMD Radeon Graphics", "device_id": "0x75a3", "target_graphics_version": "gfx950"}
+    assert market_name(asic, {"product_name": "AMD Instinct MI355 OAM"}) == "AMD Instinct MI355 OAM"
+    assert market_name(asic, {}) == "AMD Instinct MI355X"
+    assert market_name({"market_name": "", "target_graphics_version": "gfx950"}) == "AMD Instinct MI350-series (gfx950)"
+    assert market_name({"market_name": "AMD Instinct MI355 OAM"}, {"product_name": "x"}) == "AMD Instinct MI355 OAM"
+
+
+def test_telemetry_alerts_are_deduplicated():
+    """Repeated samples of one alert (numbers differ: "Power 1359W ...", "Power 1379W ...") collapse into one
+    {message, count, first_s, last_s} entry; distinct alerts stay separate (reference formats kept)."""
+    import torch
+    from distributed_llm_training_gpu_manager_amd.health.gpu_manager import GPUDevice
+    from distributed_llm_training_gpu_manager_amd.health.telemetry import TelemetrySampler
+
+    class FakeMgr:
+        def __init__(self):
+            self.i = 0
+
+        def query_devices(self):
+            self.i += 1
+            d = GPUDevice(index=0, name="AMD Instinct MI355X", memory_total_mib=294912,
+                          alerts=[f"WARNING: Power {1350 + self.i}W near limit 1400W",
+                                  "WARNING: Utilization 100% at max capacity"])
+            return [d], "amdsmi"
+
+    s = TelemetrySampler(torch.device("cpu"), interval_s=0.0, manager=FakeMgr())
+    for _ in range(25):
+        s.sample()
+    out = s.summary()
+    assert out["device"] == "AMD Instinct MI355X"
+    alerts = out["alerts"]
+    assert len(alerts) == 2, alerts
+    power = next(a for a in alerts if "Power" in a["message"])
+    assert power["count"] == 25 and power["message"] == "WARNING: Power 1375W near limit 1400W"
+    assert power["first_s"] <= power["last_s"]

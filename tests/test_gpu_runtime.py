@@ -40,6 +40,8 @@ def test_in_job_telemetry_sampler():
     out = s.stop()
     assert out["samples"] >= 2 and out["source"] == "amdsmi", out
     assert out["junction_temp_c"]["max"] > 0 and out["hbm_used_gib"]["max"] > 0
+    assert "Radeon" not in out["device"] and "MI35" in out["device"], out["device"]  # the product, not libdrm's default
+    assert all(isinstance(a, dict) and a["count"] >= 1 for a in out.get("alerts", []))
 
 
 def _engine(seed=0):
