@@ -116,6 +116,43 @@ def main():
             res["torch_sdpa_fwd_bwd"] = {"ms": t * 1e3, "TFLOPs": 3.5 * flops_f / t / 1e12}
         except Exception as e:  # pragma: no cover
             res["torch_sdpa"] = {"error": str(e)[:200]}
+    if want("attn_ab"):
+        # A/B of kernel variants switched by environment variables, interleaved rounds in ONE process
+        # (cdna_hip_programming.md §5.4 rule 24): medians and minima per variant
+        B = 1
+        qkv = torch.randn(B, T, (H + 2 * Hk) * hd, device=dev, dtype=bf)
+        q = qkv[..., : H * hd].view(B, T, H, hd)
+        k = qkv[..., H * hd:(H + Hk) * hd].view(B, T, Hk, hd)
+        v = qkv[..., (H + Hk) * hd:].view(B, T, Hk, hd)
+        flops_f = 4 * B * H * T * T * hd / 2
+        o, lse = ops.flash_attn_fwd(q, k, v, None, True)
+        do = torch.randn_like(o)
+        variants = {"fwd_4wave": ("fwd", {"DLGM_ATTN_FWD_PP": "0"}), "fwd_pp": ("fwd", {"DLGM_ATTN_FWD_PP": "1"})}
+        for name in os.environ.get("DLGM_AB_EXTRA", "").split(","):
+            if "=" in name:  # extra backward variants: label:VAR=val
+                label, kv = name.split(":", 1)
+                var, val = kv.split("=", 1)
+                variants[label] = ("bwd", {var: val})
+        samples = {n: [] for n in variants}
+        for _ in range(5):
+            for n, (kind, envs) in variants.items():
+                old = {e: os.environ.get(e) for e in envs}
+                os.environ.update(envs)
+                if kind == "fwd":
+                    t = timeit(lambda: ops.flash_attn_fwd(q, k, v, None, True), iters=10)
+                else:
+                    t = timeit(lambda: ops.flash_attn_bwd(do, q, k, v, o, lse, None, True), iters=5)
+                for e, val in old.items():
+                    if val is None:
+                        os.environ.pop(e, None)
+                    else:
+                        os.environ[e] = val
+                samples[n].append(t)
+        for n, ts in samples.items():
+            ts = sorted(ts)
+            fl = flops_f if variants[n][0] == "fwd" else 2.5 * flops_f
+            res["ab_" + n] = {"median_ms": ts[len(ts) // 2] * 1e3, "min_ms": ts[0] * 1e3,
+                              "TFLOPs_median": fl / ts[len(ts) // 2] / 1e12}
     if want("gemm"):
         a = torch.randn(T, D, device=dev, dtype=bf)
         w = torch.randn(2 * F_, D, device=dev, dtype=bf)
