@@ -61,10 +61,6 @@ int64_t dlgm_gemm_lt(at::Tensor out, const at::Tensor& a, const at::Tensor& b, d
 at::Tensor dlgm_gemm_lt_tune(const at::Tensor& out, const at::Tensor& a, const at::Tensor& b, double beta,
                              int64_t n_heuristic, bool all_algos, int64_t reps);
 int64_t dlgm_gemm_lt_version();
-// gemm_grouped_lt.hip
-int64_t dlgm_grouped_lt(at::Tensor out, const at::Tensor& a, const at::Tensor& w, const at::Tensor& offsets,
-                        int64_t mode, bool trans_w, double beta, int64_t algo_index);
-std::string dlgm_grouped_lt_kernel(int64_t mode, int64_t G, int64_t N, int64_t K, int64_t R);
 // gemm_mfma.hip
 void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bool accumulate,
                     const c10::optional<at::Tensor>& offsets, int64_t mode, int64_t M, int64_t N, int64_t K,
@@ -94,8 +90,6 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("gemm_lt(Tensor(a!) out, Tensor a, Tensor b, float beta, int algo) -> int");
   m.def("gemm_lt_tune(Tensor out, Tensor a, Tensor b, float beta, int n_heuristic, bool all_algos, int reps) -> Tensor");
   m.def("gemm_lt_version() -> int", &dlgm_gemm_lt_version);
-  m.def("grouped_lt(Tensor(a!) out, Tensor a, Tensor w, Tensor offsets, int mode, bool trans_w, float beta, int algo) -> int");
-  m.def("grouped_lt_kernel(int mode, int G, int N, int K, int R) -> str", &dlgm_grouped_lt_kernel);
   m.def("gemm_mfma(Tensor(a!) out, Tensor a, Tensor b, bool accumulate, Tensor? offsets, int mode, int M, int N, int K, int G, int b_gstride) -> ()");
 }
 
@@ -122,6 +116,5 @@ TORCH_LIBRARY_IMPL(dlgm, CUDA, m) {
   m.impl("router_topk", &dlgm_router_topk);
   m.impl("gemm_lt", &dlgm_gemm_lt);
   m.impl("gemm_lt_tune", &dlgm_gemm_lt_tune);
-  m.impl("grouped_lt", &dlgm_grouped_lt);
   m.impl("gemm_mfma", &dlgm_gemm_mfma);
 }

@@ -44,8 +44,6 @@ namespace {
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 typedef __fp16 hf16x4 __attribute__((ext_vector_type(4)));  // the transpose-read builtin's f16 vector type
 typedef __attribute__((address_space(3))) hf16x4 lds_f16x4;
-typedef __attribute__((address_space(1))) const void* gptr_t;
-typedef __attribute__((address_space(3))) void* lptr_t;
 
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
@@ -140,28 +138,6 @@ __device__ __forceinline__ f16x4 lds_read_tr(const f16* p) {
   return __builtin_bit_cast(f16x4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((lds_f16x4*)(p)));
 }
 
-// The same transposed read as inline asm: invisible to the compiler's LDS-DMA alias tracking, which otherwise
-// puts an s_waitcnt vmcnt(0) in front of every transposed read that follows an LDS-DMA (it cannot tell the
-// ring slot a DMA fills from the slot being read). The caller waits lgkmcnt itself, then fences the
-// scheduler (cdna_hip_programming.md §5.4 rule 18).
-template <typename E>
-__device__ __forceinline__ vec4_t<E> lds_read_tr_asm(const E* p) {
-  vec4_t<E> v;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)(lptr_t)p));
-  return v;
-}
-template <typename E>
-__device__ __forceinline__ vec8_t<E> lds_read_b128_asm(const E* p) {
-  vec8_t<E> v;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)(lptr_t)p));
-  return v;
-}
-#define DLGM_LGKM_WAIT(n)                                   \
-  do {                                                      \
-    asm volatile("s_waitcnt lgkmcnt(" #n ")" ::: "memory"); \
-    __builtin_amdgcn_sched_barrier(0);                      \
-  } while (0)
-
 __device__ __forceinline__ bf16x8 cat(bf16x4 a, bf16x4 b) {
   return (bf16x8){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
@@ -169,6 +145,8 @@ __device__ __forceinline__ f16x8 cat(f16x4 a, f16x4 b) {
   return (f16x8){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
+typedef __attribute__((address_space(1))) const void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
 
 // One LDS-DMA piece: 64 lanes x 16 B = 1 KiB landing lane-linearly at `lds` (wave-uniform).
 __device__ __forceinline__ void glds16(const void* src, void* lds) {
@@ -418,261 +396,6 @@ __global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams<E> 
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
   store_rows_bf16<DT>(p.o + (((int64_t)b * p.S + qcol) * p.Hq + hq) * D, o, inv, h, qcol < p.S);
   if (qcol < p.S && h == 0) p.lse[((int64_t)b * p.Hq + hq) * p.S + qcol] = (m_run + log2f(l_tot)) * kLn2;
-}
-
-// ----------------------------------------------------------------------------------
-// Forward, ping-pong schedule (8 waves, two wave groups one phase apart)
-// ----------------------------------------------------------------------------------
-//
-// The 4-wave kernel above keeps the matrix pipe busy about half the time: each wave alternates 32
-// MFMAs (S^T = K Q^T, then O^T += V^T P^T) with a softmax block of ~100 vector instructions, and two
-// independent workgroups share a CU without coordinating which of them computes when. Here ONE
-// workgroup of 8 waves per CU covers 256 queries: group A (waves 0-3) and group B (waves 4-7) each
-// own 128 queries (32 per wave) and share every K / V tile in LDS. Every wave runs the same two-phase
-// program per KV tile t, with a workgroup barrier after each phase:
-//     P1(t)  matrix phase   O^T += V(t-1)^T P(t-1)^T; S^T(t) = K(t) Q^T        (32 MFMAs)
-//     P2(t)  vector phase   mask, row max, deferred rescale, exp2 -> P(t)     (+ group A: LDS-DMA)
-// and group B runs one phase behind (one extra barrier up front; A takes one at the end). Waves w and
-// w + 4 share a SIMD, so on every SIMD one wave is in its matrix phase while its partner does the
-// softmax: the MFMA pipe alternates between the two waves instead of idling through each softmax
-// (MI355X_MICROARCH.md 'Two waves per SIMD'; cdna_hip_programming.md T5/stagger).
-// K / V tiles (64 keys) sit in a 3-slot LDS ring. Group A stages K(t+2) and V(t+1) during its P2(t)
-// and retires them with a counted vmcnt at the end of P2(t+1) -- one phase before their first reader
-// (A's P1(t+2)) -- so DMA latency overlaps two phases of compute. Full tiles only (S % 256 == 0,
-// head dim 128); other shapes take the 4-wave kernel.
-constexpr int kPpThreads = 512;
-constexpr int kPpBQ = 256;
-constexpr int kPpBKV = 64;
-constexpr int kPpRing = 3;
-
-__device__ __forceinline__ void pp_barrier() {
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-template <typename E>
-__global__ __launch_bounds__(kPpThreads, 2) void flash_fwd_pp_kernel(FwdParams<E> p) {
-  constexpr int D = 128;
-  constexpr int KK = D / 16;
-  constexpr int DT = D / 32;
-  constexpr int TILE = kPpBKV * D;
-  __shared__ __attribute__((aligned(16))) E smem[2 * kPpRing * TILE];  // [K ring | V ring]
-  E* const kring = smem;
-  E* const vring = smem + kPpRing * TILE;
-
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int grp = w >> 2, wi = w & 3;  // group A = 0 (leads), B = 1 (one phase behind)
-  const int r = lane & 31, h = lane >> 5, i16 = lane & 15, g = lane >> 4;
-
-  const int nqt = p.S / kPpBQ;
-  const int group = p.Hq / p.Hkv;
-  const int work = xcd_remap(blockIdx.x, gridDim.x);
-  const int per_kv = group * nqt;
-  const int bk = work / per_kv;
-  const int rem = work - bk * per_kv;
-  const int qt = nqt - 1 - rem / group;  // heaviest (last) query tile first
-  const int hq = (bk % p.Hkv) * group + rem % group;
-  const int b = bk / p.Hkv;
-  const int hk = hq / group;
-  const int q0 = qt * kPpBQ;
-  const int q0w = q0 + 128 * grp + 32 * wi;
-  const int qcol = q0w + r;
-  const E* qb = p.q + b * p.q_sb + hq * p.q_sh;
-  const E* kb = p.k + b * p.k_sb + hk * p.k_sh;
-  const E* vb = p.v + b * p.v_sb + hk * p.v_sh;
-
-  vec8_t<E> qf[KK];
-#pragma unroll
-  for (int kk = 0; kk < KK; ++kk)
-    qf[kk] = *reinterpret_cast<const vec8_t<E>*>(qb + (int64_t)qcol * p.q_ss + 16 * kk + 8 * h);
-
-  const int kv_end = p.causal ? q0 + kPpBQ : p.S;
-  const int nt = kv_end / kPpBKV;
-  const TileDma<E, D, kPpBKV, 0, false> kdma(kb, p.k_ss, p.S, wi, lane);
-  const TileDma<E, D, kPpBKV, 2, false> vdma(vb, p.v_ss, p.S, wi, lane);
-
-  f32x16 o[DT];
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt) o[dt] = (f32x16)(0.f);
-  f32x16 s[2];
-  vec8_t<E> pf[2][2];
-  float m_run = -INFINITY, l_run = 0.f;
-  // a tile is live for this wave unless all its keys lie above the wave's last query (causal)
-  auto live = [&](int t) { return !(p.causal && t * kPpBKV > q0w + 31); };
-
-  // prologue: K(0), K(1), V(0) resident before the first phase (group A stages, everyone waits at the barrier)
-  if (grp == 0) {
-    kdma.issue(kring, 0);
-    if (nt > 1) kdma.issue(kring + TILE, kPpBKV);
-    vdma.issue(vring, 0);
-    vm_drain();
-  }
-  pp_barrier();
-  if (grp == 1) pp_barrier();  // group B runs one phase behind
-
-  // per-lane byte offsets inside a K tile (row image) and a V tile (tr image): every LDS read of the loop is
-  // (slot base + this offset + immediate). The reads are inline asm -- the compiler would otherwise wait for
-  // every outstanding LDS-DMA (vmcnt(0)) before the first read after one, unable to tell the ring slot a DMA
-  // fills from the slot being read -- so the loop waits lgkmcnt itself.
-  uint32_t koff[KK], voff[DT];
-#pragma unroll
-  for (int kk = 0; kk < KK; ++kk) koff[kk] = (uint32_t)((r * D + swz_row<D>(r, 2 * kk + h) * 8) * 2);
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt) {
-    const int col = dt * 32 + 16 * (g & 1) + 4 * (i16 & 3);
-    const int r1 = 4 * h + (i16 >> 2);  // + 32u + 16s2 (+ 8): multiples of 4 rows keep the swizzle
-    voff[dt] = (uint32_t)((r1 * D + swz_tr<D>(r1, col >> 3) * 8 + (col & 7)) * 2);
-  }
-  const uint32_t kbase = (uint32_t)(uintptr_t)(lptr_t)kring, vbase = (uint32_t)(uintptr_t)(lptr_t)vring;
-  auto rd_tr = [](uint32_t addr, auto imm) {
-    vec4_t<E> v;
-    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(decltype(imm)::value));
-    return v;
-  };
-  auto rd_128 = [](uint32_t addr, auto imm) {
-    vec8_t<E> v;
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(decltype(imm)::value));
-    return v;
-  };
-  using I0 = std::integral_constant<int, 0>;
-  // V^T fragments of head-dim tile dt: rows 32u + 16s2 (+8) of the tr image, 8 reads
-  auto rd_v = [&](uint32_t vslot, int dt, vec4_t<E>(&dst)[8]) {
-    const uint32_t a = vslot + voff[dt];
-    dst[0] = rd_tr(a, I0{});
-    dst[1] = rd_tr(a, std::integral_constant<int, 8 * D * 2>{});
-    dst[2] = rd_tr(a, std::integral_constant<int, 16 * D * 2>{});
-    dst[3] = rd_tr(a, std::integral_constant<int, 24 * D * 2>{});
-    dst[4] = rd_tr(a, std::integral_constant<int, 32 * D * 2>{});
-    dst[5] = rd_tr(a, std::integral_constant<int, 40 * D * 2>{});
-    dst[6] = rd_tr(a, std::integral_constant<int, 48 * D * 2>{});
-    dst[7] = rd_tr(a, std::integral_constant<int, 56 * D * 2>{});
-  };
-  auto mm_v = [&](int dt, const vec4_t<E>(&src)[8]) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-        o[dt] = mfma32(cat(src[4 * u + 2 * s2], src[4 * u + 2 * s2 + 1]), pf[u][s2], o[dt]);
-  };
-  // K fragments of k-steps kk, kk + 1 for both 32-key subtiles, 4 reads
-  auto rd_k = [&](uint32_t kslot, int kk, vec8_t<E>(&dst)[4]) {
-    dst[0] = rd_128(kslot + koff[kk], I0{});
-    dst[1] = rd_128(kslot + koff[kk], std::integral_constant<int, 32 * D * 2>{});
-    dst[2] = rd_128(kslot + koff[kk + 1], I0{});
-    dst[3] = rd_128(kslot + koff[kk + 1], std::integral_constant<int, 32 * D * 2>{});
-  };
-  auto mm_k = [&](int kk, const vec8_t<E>(&src)[4]) {
-    s[0] = mfma32(src[0], qf[kk], s[0]);
-    s[1] = mfma32(src[1], qf[kk], s[1]);
-    s[0] = mfma32(src[2], qf[kk + 1], s[0]);
-    s[1] = mfma32(src[3], qf[kk + 1], s[1]);
-  };
-
-  for (int t = 0; t <= nt; ++t) {
-    const int slot = t % kPpRing, pslot = (t + kPpRing - 1) % kPpRing;
-    // ---- P1(t): matrix phase
-    __builtin_amdgcn_s_setprio(1);
-    if (t > 0 && uniform(live(t - 1))) {  // O^T += V(t-1)^T P(t-1)^T, two head-dim tiles of reads in flight
-      const uint32_t vs = vbase + (uint32_t)(pslot * TILE * 2);
-      vec4_t<E> va[8], vb[8];
-      rd_v(vs, 0, va);
-      rd_v(vs, 1, vb);
-      DLGM_LGKM_WAIT(8);
-      mm_v(0, va);
-      rd_v(vs, 2, va);
-      DLGM_LGKM_WAIT(8);
-      mm_v(1, vb);
-      rd_v(vs, 3, vb);
-      DLGM_LGKM_WAIT(8);
-      mm_v(2, va);
-      DLGM_LGKM_WAIT(0);
-      mm_v(3, vb);
-    }
-    const bool act = t < nt && uniform(live(t));
-    if (act) {  // S^T(t) = K(t) Q^T
-      const uint32_t ks = kbase + (uint32_t)(slot * TILE * 2);
-      s[0] = (f32x16)(0.f);
-      s[1] = (f32x16)(0.f);
-      vec8_t<E> ka[4], kb2[4];
-      rd_k(ks, 0, ka);
-      rd_k(ks, 2, kb2);
-      DLGM_LGKM_WAIT(4);
-      mm_k(0, ka);
-      rd_k(ks, 4, ka);
-      DLGM_LGKM_WAIT(4);
-      mm_k(2, kb2);
-      rd_k(ks, 6, kb2);
-      DLGM_LGKM_WAIT(4);
-      mm_k(4, ka);
-      DLGM_LGKM_WAIT(0);
-      mm_k(6, kb2);
-    }
-    __builtin_amdgcn_s_setprio(0);
-    pp_barrier();
-    if (t == nt) break;
-    // ---- P2(t): vector phase
-    if (grp == 0) {  // stage K(t+2), V(t+1); retire what P2(t-1) staged (read from A's P1(t+1) on)
-      const bool k2 = t + 2 < nt, v1 = t + 1 < nt;
-      if (k2) kdma.issue(kring + ((t + 2) % kPpRing) * TILE, (t + 2) * kPpBKV);
-      if (v1) vdma.issue(vring + ((t + 1) % kPpRing) * TILE, (t + 1) * kPpBKV);
-      if (k2 && v1)
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else
-        vm_drain();
-    }
-    if (act) {
-      const int kv0 = t * kPpBKV;
-      if (uniform(p.causal && kv0 + kPpBKV - 1 > q0w)) {
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int kv = kv0 + 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
-            if (kv > qcol) s[u][i] = -INFINITY;
-          }
-      }
-      float mx = -INFINITY;
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[u][i]);
-      mx = fmaxf(mx, swap_halves(mx)) * p.scale_log2;
-      if (__any(mx > m_run + kRescaleLog2)) {
-        const float m_new = fmaxf(m_run, mx);
-        const float alpha = m_new == -INFINITY ? 1.f : fast_exp2(m_run - m_new);
-        m_run = m_new;
-        l_run *= alpha;
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
-      }
-      const float m_use = m_run == -INFINITY ? 0.f : m_run;
-      const f32x2 sl2 = {p.scale_log2, p.scale_log2}, nm2 = {-m_use, -m_use};
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-#pragma unroll
-        for (int i = 0; i < 16; i += 2) {
-          const f32x2 x = pk_fma((f32x2){s[u][i], s[u][i + 1]}, sl2, nm2);
-          s[u][i] = fast_exp2(x.x);
-          s[u][i + 1] = fast_exp2(x.y);
-          l_run += s[u][i] + s[u][i + 1];
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-          pf[u][s2] = (vec8_t<E>){(E)s[u][8 * s2 + 0], (E)s[u][8 * s2 + 1], (E)s[u][8 * s2 + 2],
-                                  (E)s[u][8 * s2 + 3], (E)s[u][8 * s2 + 4], (E)s[u][8 * s2 + 5],
-                                  (E)s[u][8 * s2 + 6], (E)s[u][8 * s2 + 7]};
-      }
-    }
-    pp_barrier();
-  }
-  if (grp == 0) pp_barrier();  // equal barrier counts: A idles through B's last phase
-
-  const float l_tot = l_run + swap_halves(l_run);
-  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-  store_rows_bf16<DT>(p.o + (((int64_t)b * p.S + qcol) * p.Hq + hq) * D, o, inv, h, true);
-  if (h == 0) p.lse[((int64_t)b * p.Hq + hq) * p.S + qcol] = (m_run + log2f(l_tot)) * kLn2;
 }
 
 // ----------------------------------------------------------------------------------
@@ -1219,12 +942,6 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams<E
 // run can switch it). Off by default: at S 8192, 32/8 heads the dQ pass drops 750 -> 519 us but dK/dV
 // rises 1116 -> 1307 us for its 2.15 GB of dS^T writes (the board is at its power limit), and the
 // headline step moved 0.1-0.2 % for +2.3 GiB of peak memory (profiles/attn_experiments_r01.md).
-// DLGM_ATTN_FWD_PP=0: the 4-wave forward instead of the 8-wave ping-pong one (A/B switch, read per call)
-bool fwd_pp() {
-  const char* e = std::getenv("DLGM_ATTN_FWD_PP");
-  return e == nullptr || std::atoi(e) != 0;
-}
-
 bool dq_from_ds() {
   const char* e = std::getenv("DLGM_ATTN_DQ_FROM_DS");
   return e != nullptr && std::atoi(e) != 0;
@@ -1283,9 +1000,7 @@ std::tuple<at::Tensor, at::Tensor> dlgm_flash_attn_fwd(const at::Tensor& q, cons
                    lse.data_ptr<float>(), q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
                    v.stride(0), v.stride(1), v.stride(2), B, S, Hq, Hkv, (float)(softmax_scale * kLog2e), causal};
     const bool tail = S % 128 != 0;  // a partial K/V tile exists: the clamped-staging instantiation
-    if (D == 128 && S % kPpBQ == 0 && fwd_pp()) {
-      flash_fwd_pp_kernel<E><<<(int64_t)(S / kPpBQ) * B * Hq, kPpThreads, 0, stream>>>(p);
-    } else if (D == 128) {
+    if (D == 128) {
       if (tail) flash_fwd_kernel<E, 128, true><<<blocks, kFwdThreads, 0, stream>>>(p);
       else flash_fwd_kernel<E, 128, false><<<blocks, kFwdThreads, 0, stream>>>(p);
     } else {

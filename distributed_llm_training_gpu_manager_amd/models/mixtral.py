@@ -118,11 +118,21 @@ class MixtralBlock(LlamaBlock):
             offs = dctx.local_offsets
             dy = dy.contiguous()
             da_all = gm.grouped_mm(dy, p["w_down"], offs, transpose_w=False)
-            gm.grouped_wgrad(g["w_down"], dy, a_all, offs, acc)
             dgu_all = ops.swiglu_bwd(da_all, gu_all)
             del da_all
+            dx = gm.grouped_mm(dgu_all, p["w_gate_up"], offs, transpose_w=False)
+            if ctx is not None and ctx.defer_wgrad:
+                # dW once per step over the micro-batches' rows regrouped expert-major on the device
+                if ctx.micro_index == 0:
+                    self._wstash, self._wflushed, self._wbytes = [], False, 0
+                self._wstash.append((dy, a_all, dgu_all, x, offs))
+                self._wbytes += sum(t.numel() * t.element_size() for t in (dy, a_all, dgu_all, x))
+                if ctx.last_micro or self._wbytes > getattr(ctx, "defer_budget_bytes", 48 << 30):
+                    self._flush_wgrad_grouped(g)
+                return dx
+            gm.grouped_wgrad(g["w_down"], dy, a_all, offs, acc)
             gm.grouped_wgrad(g["w_gate_up"], dgu_all, x, offs, acc)
-            return gm.grouped_mm(dgu_all, p["w_gate_up"], offs, transpose_w=False)
+            return dx
         counts = dctx.counts()
         if ctx is not None and ctx.defer_wgrad:
             return self._experts_bwd_deferred(p, g, x, dy, saved, counts, ctx)
@@ -211,6 +221,44 @@ class MixtralBlock(LlamaBlock):
             grad_mm(g["w_gate_up"][e], dgue.t(), xe, acc)
             del dgue, xe
         self._wstash, self._wflushed, self._wbytes = [], True, 0
+
+    def _flush_wgrad_grouped(self, g: Params) -> None:
+        """Deferred expert dW with device offsets: every stashed micro-batch's rows are scattered into one
+        expert-major tensor per operand (positions computed on the device from the routing counts; no host
+        read), then ONE grouped GEMM per weight reduces each expert over all its rows of the step."""
+        stash, acc = self._wstash, self._wflushed
+        self._wstash, self._wflushed, self._wbytes = [], True, 0
+        if len(stash) == 1:
+            dy, a, dgu, x, offs = stash[0]
+            gm.grouped_wgrad(g["w_down"], dy, a, offs, acc)
+            gm.grouped_wgrad(g["w_gate_up"], dgu, x, offs, acc)
+            return
+        dev = stash[0][0].device
+        counts = torch.stack([o[1:] - o[:-1] for *_, o in stash]).to(torch.long)  # [micro-batches, experts]
+        tot = counts.sum(0)
+        new_off = torch.zeros(self.E_local + 1, dtype=torch.int32, device=dev)
+        new_off[1:] = tot.cumsum(0)
+        # destination of micro-batch m's first row of expert e: the expert's start + rows of earlier micro-batches
+        dst0 = new_off[:-1].to(torch.long).unsqueeze(0) + (counts.cumsum(0) - counts)
+        rows = [t[0].shape[0] for t in stash]
+        R = sum(rows)
+        idx = []
+        for m, (*_, o) in enumerate(stash):
+            shift = dst0[m] - o[:-1].to(torch.long)
+            idx.append(torch.arange(rows[m], device=dev) +
+                       torch.repeat_interleave(shift, counts[m], output_size=rows[m]))
+
+        def merged(k: int) -> torch.Tensor:
+            t0 = stash[0][k]
+            out = t0.new_empty((R, t0.shape[1]))
+            for m in range(len(stash)):
+                out.index_copy_(0, idx[m], stash[m][k])
+            return out
+        dy_m, a_m = merged(0), merged(1)
+        gm.grouped_wgrad(g["w_down"], dy_m, a_m, new_off, acc)
+        del dy_m, a_m
+        dgu_m, x_m = merged(2), merged(3)
+        gm.grouped_wgrad(g["w_gate_up"], dgu_m, x_m, new_off, acc)
 
     def moe_backward(self, p: Params, g: Params, hn2: torch.Tensor, saved, dout: torch.Tensor, ctx: StepContext):
         c = self.cfg

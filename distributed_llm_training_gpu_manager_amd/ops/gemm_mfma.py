@@ -5,9 +5,15 @@
 ``grouped_wgrad(out, a, b, offsets)`` expert-grouped weight gradient (reduction rows split by offsets)
 
 The group offsets are an int32 device tensor, so an MoE layer launches its expert GEMMs without
-reading the routing counts on the host. Two device backends: hipBLASLt's grouped GEMM driven by
-device-side user arguments (csrc/kernels/gemm_grouped_lt.hip, the default) and the hand-written
-grouped MFMA kernel (gemm_mfma.hip). CPU tensors take an fp32 reference path (tests).
+reading the routing counts on the host (graph-capture safe). CPU tensors take an fp32 reference path
+(tests).
+
+Two device-offset alternatives were measured this round and dropped (profiles/moe_experiments_r01.md):
+hipBLASLt's grouped GEMM with device-side user arguments (hipblaslt_ext::GroupedGemm) fails at run time --
+the torch wheel bundles its own libhipblaslt (ROCm 7.0), which the process loads instead of /opt/rocm's 7.2,
+and its C++ extension API trips a Tensile "hardware != nullptr" assertion against the 7.2 headers (the C API
+used by ops/gemm.py is unaffected); torch._grouped_mm is not capture-safe on this stack ("operation not
+permitted when stream is capturing": it synchronises) and ran 117.5k tok/s against the loop's 128.3k.
 """
 from __future__ import annotations
 
@@ -20,18 +26,16 @@ from .._native import hip_ops, use_native
 
 DENSE, GROUP_M, GROUP_K = 0, 1, 2
 # Expert GEMM strategy (DLGM_MOE_GROUPED):
-#   "lt"    (default) every expert GEMM as one hipBLASLt grouped GEMM whose per-expert sizes and pointers a
-#           HIP kernel writes into a device argument array from the routing offsets: no host read at all;
-#   "1"     the same with the hand-written grouped MFMA kernel;
-#   "wgrad" only the weight gradients grouped (MFMA), forward / dX per expert through hipBLASLt (host counts);
-#   "0"     the per-expert hipBLASLt loop (reads the routing counts on the host once per layer).
-# Round 2 measured (Mixtral-8x7B, 2 layers, seq 4096, GA 4): loop 117.8k tok/s, grouped MFMA dW 111.0k,
-# all-grouped MFMA 107.5k (profiles/mixtral_grouped_ab_r02.json).
-_MODE = os.environ.get("DLGM_MOE_GROUPED", "lt")
-GROUPED = _MODE in ("1", "lt")
-BACKEND = "lt" if _MODE == "lt" else "mfma"
-GROUPED_WGRAD = _MODE in ("1", "lt", "wgrad") and os.environ.get("DLGM_MOE_GROUPED_WGRAD", "1") != "0"
-LT_ALGO = int(os.environ.get("DLGM_MOE_LT_ALGO", "-1"))  # hipBLASLt heuristic rank to use (-1: the first)
+#   "0"     (default) the per-expert hipBLASLt loop: reads the routing counts on the host once per layer and
+#           micro-batch (the forward's read is reused by the backward);
+#   "1"     every expert GEMM as one grouped MFMA launch with the device offsets: no host read at all;
+#   "wgrad" only the weight gradients grouped (MFMA), forward / dX per expert through hipBLASLt.
+# Mixtral-8x7B (2 layers, seq 4096, GA 4, one MI355X, round 3): loop 128.3k tok/s (MFU 0.294), all-grouped
+# MFMA 115.1k (0.263) -- the host read costs less than the grouped kernel's gap to hipBLASLt.
+_MODE = os.environ.get("DLGM_MOE_GROUPED", "0")
+GROUPED = _MODE == "1"
+GROUPED_WGRAD = _MODE in ("1", "wgrad") and os.environ.get("DLGM_MOE_GROUPED_WGRAD", "1") != "0"
+
 
 def _ok(t: torch.Tensor) -> bool:
     return t.dtype == torch.bfloat16 and t.data_ptr() % 16 == 0
@@ -59,8 +63,6 @@ def grouped_supported(x: torch.Tensor, wgrad: bool = False) -> bool:
     """Can the grouped kernels take rows `x` (bf16, row-major, 16-B aligned, on the GPU with the extension)?
     wgrad: asking for the weight-gradient GEMMs only (GROUPED_WGRAD), else for all expert GEMMs (GROUPED)."""
     on = GROUPED_WGRAD if wgrad else GROUPED
-    if BACKEND == "lt" and x.dtype == torch.float16:
-        return on and use_native(x) and x.is_contiguous() and x.dim() == 2
     return on and use_native(x) and _ok(x) and x.dim() == 2 and x.stride(1) == 1 and x.stride(0) % 8 == 0
 
 
@@ -86,9 +88,6 @@ def grouped_mm(x: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, transpos
     if out is None:
         out = torch.empty(R, N, dtype=x.dtype, device=x.device)
     if use_native(x):
-        if BACKEND == "lt":
-            hip_ops().grouped_lt(out, x.contiguous(), w.contiguous(), offsets, 0, transpose_w, 0.0, LT_ALGO)
-            return out
         b = w.transpose(1, 2) if transpose_w else w
         hip_ops().gemm_mfma(out, x, b, False, offsets, GROUP_M, R, N, K, G, w.stride(0))
         return out
@@ -106,9 +105,6 @@ def grouped_wgrad(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, offsets: 
     """out[e] (+)= a[rows of e]^T @ b[rows of e]: a [R, M], b [R, N] row-major (token rows), out [G, M, N]."""
     G, M, N = out.shape
     if use_native(out):
-        if BACKEND == "lt":
-            hip_ops().grouped_lt(out, a.contiguous(), b.contiguous(), offsets, 1, False, 1.0 if acc else 0.0, LT_ALGO)
-            return out
         hip_ops().gemm_mfma(out, a.t(), b, acc, offsets, GROUP_K, M, N, a.shape[0], G, 0)
         return out
     offs = offsets.tolist()

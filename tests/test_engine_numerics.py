@@ -74,8 +74,9 @@ def test_mixtral_manual_backward_matches_autograd_gpu():
 @pytest.mark.gpu
 @pytest.mark.parametrize("grouped,wgrad", [(True, True), (False, True), (False, False)])
 def test_mixtral_expert_gemm_modes_match_autograd_gpu(monkeypatch, grouped, wgrad):
-    """Experts as grouped MFMA launches (device offsets from moe_permute, no host read of the counts), the
-    grouped weight gradients only, and the per-expert hipBLASLt loop."""
+    """Experts as grouped MFMA launches (device offsets from moe_permute, no host read of the counts; with GA 2
+    the deferred grouped dW over both micro-batches), the grouped weight gradients only, and the per-expert
+    hipBLASLt loop."""
     from distributed_llm_training_gpu_manager_amd.ops import gemm_mfma as gm
     monkeypatch.setattr(gm, "GROUPED", grouped)
     monkeypatch.setattr(gm, "GROUPED_WGRAD", wgrad)
@@ -303,3 +304,31 @@ def test_llama_chunked_head_matches_autograd_gpu(monkeypatch):
     monkeypatch.setattr(LlamaHead, "logits_budget_bytes", 1)
     monkeypatch.setattr(LlamaHead, "chunk_tokens", 48)
     _check("cuda")
+
+
+def test_mixtral_grouped_deferred_wgrad_matches_per_micro_batch_cpu(monkeypatch):
+    """The grouped expert path (device offsets) with the weight gradients deferred to the step's last
+    micro-batch -- every micro-batch's rows scattered expert-major on the device, one grouped dW GEMM per
+    weight -- equals the per-micro-batch grouped dW. CPU run of the same code (grouped ops' reference path)."""
+    from distributed_llm_training_gpu_manager_amd.models.mixtral import MixtralBlock
+    from distributed_llm_training_gpu_manager_amd.parallel.zero import EngineConfig, ZeroEngine
+    monkeypatch.setattr(MixtralBlock, "_grouped", lambda self, x, wgrad=False: True)
+    mc = get_config("mixtral-tiny")
+    g = torch.Generator().manual_seed(4)
+    data = [torch.randint(0, mc.vocab_size, (2, 33), generator=g) for _ in range(3)]
+    grads = {}
+    orig = MixtralBlock._flush_wgrad_grouped
+    for dw in (False, True):
+        ec = EngineConfig(zero_stage=3, micro_batch_size=2, seq_len=32, grad_accum=3, lr=1e-3, scheduler="constant",
+                          init_device="cpu", defer_expert_wgrad=dw)
+        eng = ZeroEngine(mc, ec, torch.device("cpu"))
+        flushed = []
+        monkeypatch.setattr(MixtralBlock, "_flush_wgrad_grouped",
+                            lambda self, gg: (flushed.append(len(self._wstash)), orig(self, gg))[1])
+        for i, t in enumerate(data):
+            eng.micro_step(t[:, :-1], t[:, 1:], first=i == 0, last=i == 2)
+        assert (flushed and flushed[0] == 3) if dw else not flushed
+        grads[dw] = eng.full_grads()
+    for k, v in grads[False].items():
+        err = float((grads[True][k] - v).abs().max() / v.abs().max().clamp_min(1e-8))
+        assert err < 1e-2, (k, err)

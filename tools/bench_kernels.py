@@ -127,12 +127,13 @@ def main():
         flops_f = 4 * B * H * T * T * hd / 2
         o, lse = ops.flash_attn_fwd(q, k, v, None, True)
         do = torch.randn_like(o)
-        variants = {"fwd_4wave": ("fwd", {"DLGM_ATTN_FWD_PP": "0"}), "fwd_pp": ("fwd", {"DLGM_ATTN_FWD_PP": "1"})}
-        for name in os.environ.get("DLGM_AB_EXTRA", "").split(","):
-            if "=" in name:  # extra backward variants: label:VAR=val
-                label, kv = name.split(":", 1)
-                var, val = kv.split("=", 1)
-                variants[label] = ("bwd", {var: val})
+        # variants: DLGM_AB="label:fwd|bwd:VAR=val,..." (a label with no VAR=val runs the defaults)
+        variants = {"fwd": ("fwd", {}), "bwd": ("bwd", {})}
+        for item in os.environ.get("DLGM_AB", "").split(","):
+            parts = item.split(":")
+            if len(parts) == 3 and "=" in parts[2]:
+                var, val = parts[2].split("=", 1)
+                variants[parts[0]] = (parts[1], {var: val})
         samples = {n: [] for n in variants}
         for _ in range(5):
             for n, (kind, envs) in variants.items():
