@@ -42,6 +42,8 @@ def main(argv=None) -> int:
     ap.add_argument("--ep", type=int, default=1, help="expert-parallel size (Mixtral)")
     ap.add_argument("--n-layers", type=int, default=0)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--async-comm", action="store_true",
+                    help="collectives on per-communicator HIP streams, ordered like RCCL's (ShadowComm async_mode)")
     a = ap.parse_args(argv)
 
     import torch
@@ -60,7 +62,8 @@ def main(argv=None) -> int:
                         warmup_steps=100, total_steps=10000, grad_clip=1.0, activation_checkpointing=a.ckpt,
                         max_live_parameters="hbm", max_reuse_distance="hbm", expert_parallel_size=a.ep)
     t0 = time.time()
-    eng = ZeroEngine(mcfg, ecfg, dev, ShadowComm(a.world, a.rank))
+    comm = ShadowComm(a.world, a.rank, async_mode=a.async_comm)
+    eng = ZeroEngine(mcfg, ecfg, dev, comm)
     torch.cuda.synchronize()
     init_s = time.time() - t0
     print(f"[shadow] {mcfg.name} rank {a.rank}/{a.world}: engine built in {init_s:.1f}s, "
@@ -105,6 +108,8 @@ def main(argv=None) -> int:
         "step_s": [round(x, 3) for x in times], "per_micro_batch_s": round(sum(timed) / len(timed) / a.ga, 3),
         "tokens_per_s_per_rank_compute_only": round(a.mbs * a.seq * a.ga * len(timed) / sum(timed), 1),
         "init_s": round(init_s, 1),
+        "comm": "async (per-communicator HIP streams, RCCL ordering)" if a.async_comm else "sync (compute stream)",
+        "async_collectives_issued": comm.issued,
     }
     print(json.dumps(out), flush=True)
     if a.out:
