@@ -37,8 +37,6 @@ def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, model_cf
     off_p = zo.get("offload_param", {}).get("device", "none")
     if off_p != "none" and int(zo.get("stage", 0)) != 3:
         notes.append(f"offload_param={off_p} needs ZeRO-3 (as in DeepSpeed): parameters stay in HBM")
-    if off_p == "nvme":
-        notes.append("offload_param=nvme: the bf16 partition is served from pinned host memory")
     act = ds.get("activation_checkpointing")
     cfg = EngineConfig(
         zero_stage=int(zo.get("stage", 0)),
@@ -65,7 +63,7 @@ def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, model_cf
         hysteresis=int(ds.get("fp16", {}).get("hysteresis", 2)),
         min_loss_scale=float(ds.get("fp16", {}).get("min_loss_scale", 1.0)),
         offload_optimizer=off_o,
-        nvme_path=zo.get("offload_optimizer", {}).get("nvme_path"),
+        nvme_path=zo.get("offload_optimizer", {}).get("nvme_path") or zo.get("offload_param", {}).get("nvme_path"),
         offload_buffer_count=int(zo.get("offload_optimizer", {}).get("buffer_count", 4)),
         aio_threads=max(1, int(ds.get("aio", {}).get("thread_count", 1)) * int(ds.get("aio", {}).get("queue_depth", 8))),
         aio_block_size=int(ds.get("aio", {}).get("block_size", 8 << 20)),
@@ -78,6 +76,7 @@ def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, model_cf
         prescale_gradients=bool(ds.get("prescale_gradients", False)),
         gradient_predivide_factor=float(ds.get("gradient_predivide_factor", 1.0)),
         offload_param=off_p,
+        param_buffer_count=int(zo.get("offload_param", {}).get("buffer_count", 5)),
     )
     # engine knobs without a DeepSpeed key travel in the "mi355x" block (launcher.config.MI355XOptions)
     cfg.expert_parallel_size = int(mi.get("expert_parallel_size", cfg.expert_parallel_size))

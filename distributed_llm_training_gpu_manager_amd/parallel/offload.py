@@ -232,6 +232,100 @@ class HostOffloadOptimizer:
                 pass
 
 
+class NvmeParamStore:
+    """``offload_param.device = "nvme"`` (ZeRO-Infinity parameter offload, reference
+    ``ai_engine/deepspeed_launcher.py:205-212``): the rank's 16-bit parameter partition lives in a file under
+    ``nvme_path``, not in host RAM.
+
+    Hot paths go through the C++ AIO engine and a ring of ``buffer_count`` pinned slots, each one parameter
+    group's shard long:
+
+    * gather: the group's shard is read file -> slot (buffered I/O), then the engine copies it H2D on its
+      side stream and all-gathers; a slot is reused only after the H2D that read it has completed (event);
+    * after each optimizer step: the new 16-bit values are produced slot by slot (device cast + D2H, or the
+      host AdamW's output) and written back with the writes of ``buffer_count - 1`` slots in flight.
+
+    The file is also mapped (``mapped``) for the cold paths -- checkpoint capture / restore, the host
+    optimizer's in-place update, tests -- which share the page cache with the buffered AIO descriptor and
+    therefore always see the same bytes.
+    """
+
+    def __init__(self, numel: int, dtype: torch.dtype, root: Optional[str], rank: int, slot_elems: int,
+                 buffer_count: int = 5, cuda: bool = False, aio_threads: int = 8, aio_block_size: int = 8 << 20):
+        if _host.lib() is None:
+            raise RuntimeError("offload_param=nvme needs the host runtime (_dlgm_host.so); run build()")
+        root = root or os.environ.get("DLGM_NVME_PATH", "/tmp/dlgm_nvme")
+        os.makedirs(root, exist_ok=True)
+        self.n, self.dtype, self.cuda = numel, dtype, cuda
+        self.esize = torch.empty((), dtype=dtype).element_size()
+        self.path = os.path.join(root, f"zero_param_r{rank}.{str(dtype).split('.')[-1]}")
+        with open(self.path, "wb") as f:
+            f.truncate(numel * self.esize)
+        self.mapped = torch.from_file(self.path, shared=True, size=numel, dtype=dtype)
+        self.aio = _host.Aio(aio_threads, aio_block_size)
+        self.fh = self.aio.open(self.path, numel * self.esize)
+        self.slot_elems = max(1, min(slot_elems, numel))
+        nb = max(2, int(buffer_count))
+        self.slots = [torch.empty(self.slot_elems, dtype=dtype, pin_memory=cuda) for _ in range(nb)]
+        self._used: List[Optional["torch.cuda.Event"]] = [None] * nb  # last H2D out of the slot
+        self._writes: List[Optional[int]] = [None] * nb                # AIO write ticket out of the slot
+        self._next = 0
+        self.stats = {"read_GiB": 0.0, "write_GiB": 0.0, "io_wait_s": 0.0}
+
+    def _wait(self, ticket: int) -> None:
+        t0 = time.perf_counter()
+        self.aio.wait(ticket)
+        self.stats["io_wait_s"] += time.perf_counter() - t0
+
+    def _take(self) -> int:
+        i = self._next
+        self._next = (i + 1) % len(self.slots)
+        if self._used[i] is not None:
+            self._used[i].synchronize()
+            self._used[i] = None
+        if self._writes[i] is not None:
+            self._wait(self._writes[i])
+            self._writes[i] = None
+        return i
+
+    def read(self, off: int, n: int):
+        """Read elements [off, off + n) into a free slot; returns (slot index, host view)."""
+        assert n <= self.slot_elems, (n, self.slot_elems)
+        i = self._take()
+        t = self.slots[i][:n]
+        self._wait(self.aio.read(self.fh, t, off * self.esize))
+        self.stats["read_GiB"] += n * self.esize / 2 ** 30
+        return i, t
+
+    def release_after(self, i: int, ev) -> None:
+        """The slot may be refilled once `ev` (the H2D copy out of it) has completed."""
+        self._used[i] = ev
+
+    def write(self, produce) -> None:
+        """Stream the whole partition back: produce(off, ln, slot_view) fills each slot-sized piece."""
+        for off in range(0, self.n, self.slot_elems):
+            ln = min(self.slot_elems, self.n - off)
+            i = self._take()
+            t = self.slots[i][:ln]
+            produce(off, ln, t)
+            self._writes[i] = self.aio.write(self.fh, t, off * self.esize)
+            self.stats["write_GiB"] += ln * self.esize / 2 ** 30
+        self.flush()
+
+    def flush(self) -> None:
+        for i, tk in enumerate(self._writes):
+            if tk is not None:
+                self._wait(tk)
+                self._writes[i] = None
+
+    def close(self) -> None:
+        if self.aio is not None:
+            self.flush()
+            self.aio.close(self.fh)
+            self.aio.shutdown()
+            self.aio = None
+
+
 class ActivationOffloader:
     """``cpu_checkpointing`` (reference ``activation_checkpointing.cpu_checkpointing``, 70b preset,
     ``deepspeed_launcher.py:215-223, :403``): the per-unit checkpointed inputs kept for recompute

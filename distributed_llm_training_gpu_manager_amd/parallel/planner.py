@@ -175,7 +175,11 @@ def plan_rank(m: ModelConfig, *, world: int, zero_stage: int = 3, micro_batch: i
         parts["bf16_gathered_inflight"] = 2.0 * (top[0] + (top[1] if len(top) > 1 else 0))
     if host_par:
         parts["offload_param_staging"] = 2.0 * 2 * max(g.shard_numel for g in groups)
-        plan.notes.append(f"parameters on {offload_param}: {2.0 * shard / GiB:.1f} GiB host")
+        if offload_param == "nvme":  # the partition is a file; host RAM holds the AIO ring (5 group shards)
+            plan.notes.append(f"parameters on nvme: {2.0 * shard / GiB:.1f} GiB file, "
+                              f"{5 * 2.0 * max(g.shard_numel for g in groups) / GiB:.1f} GiB pinned ring")
+        else:
+            plan.notes.append(f"parameters on {offload_param}: {2.0 * shard / GiB:.1f} GiB host")
     parts["runtime_reserve"] = runtime_reserve(sum(parts.values()))
     tc_names = lambda g: [sp for sp in g.specs if sp.tcache and len(sp.shape) == 2]  # noqa: E731
     if zero_stage == 3 and not host_par:

@@ -102,9 +102,11 @@ class EngineConfig:
     sequence_parallel_size: int = 1
     offload_optimizer: str = "none"  # none | cpu | nvme (ZeRO-Offload parity path: parallel/offload.py)
     # ZeRO-Infinity parameter offload (reference offload_param, deepspeed_launcher.py:40, 205-212; ZeRO-3 only):
-    # the bf16 parameter partition lives in pinned host memory; each gather stages the shard H2D on a side
-    # stream and all-gathers from there ("nvme" is served from host memory too)
+    # "cpu": the bf16 parameter partition lives in pinned host memory; each gather stages the shard H2D on a
+    # side stream and all-gathers from there. "nvme": the partition is a file under nvme_path, read per gather
+    # through the C++ AIO engine into a ring of param_buffer_count pinned slots (offload.NvmeParamStore)
     offload_param: str = "none"
+    param_buffer_count: int = 5  # offload_param.buffer_count (DeepSpeed default 5)
     # parameter all-gathers as direct mesh exchanges (batched point-to-point over every xGMI link at once)
     # instead of RCCL's ring all-gather; opt-in, A/B'd by the bench's post-timing sweep (utils/commbench.py)
     mesh_allgather: bool = False
@@ -432,7 +434,18 @@ class ZeroEngine:
             self.exp_avg_sq = torch.zeros(n, **f32)
         self.grad_shard = torch.zeros(n, **f32)
         self.param_host = self.cfg.offload_param in ("cpu", "nvme") and self.stage == 3
-        if self.param_host:
+        self.param_nvme = None
+        if self.param_host and self.cfg.offload_param == "nvme":
+            from .offload import NvmeParamStore
+            self.param_nvme = NvmeParamStore(n, self.dtype, self.cfg.nvme_path, self.rank,
+                                             max(g.shard_numel for g in self.groups),
+                                             buffer_count=self.cfg.param_buffer_count, cuda=self.is_cuda,
+                                             aio_threads=self.cfg.aio_threads,
+                                             aio_block_size=self.cfg.aio_block_size)
+            self.p16_shard = self.param_nvme.mapped  # cold paths (checkpoints, host optimizer) use the mapping
+            self._h2d = torch.cuda.Stream(dev) if self.is_cuda else None
+            self._p16_ready = None
+        elif self.param_host:
             self.p16_shard = torch.zeros(n, dtype=self.dtype, pin_memory=self.is_cuda)
             self._h2d = torch.cuda.Stream(dev) if self.is_cuda else None
             self._p16_ready = None  # event: host bf16 partition final (after the device AdamW's D2H)
@@ -508,6 +521,19 @@ class ZeroEngine:
         """offload_param with the optimizer on the device: bf16(master) chunk by chunk into a device scratch,
         then D2H into the pinned host partition (stream-ordered, no host sync)."""
         n, step = self.shard_total, 1 << 26
+        if self.param_nvme is not None:
+            # NVMe: cast a slot's worth on the device, D2H into the pinned slot, write it to the file
+            scratch = torch.empty(min(n, self.param_nvme.slot_elems), dtype=self.dtype, device=self.device)
+
+            def produce(off: int, ln: int, slot: torch.Tensor) -> None:
+                if self.is_cuda:
+                    ops.cast_f32_bf16_(scratch[:ln], self.master.narrow(0, off, ln))
+                    slot.copy_(scratch[:ln], non_blocking=True)
+                    torch.cuda.current_stream(self.device).synchronize()  # the file write reads the slot
+                else:
+                    slot.copy_(self.master.narrow(0, off, ln))
+            self.param_nvme.write(produce)
+            return
         scratch = torch.empty(min(n, step), dtype=self.dtype, device=self.device)
         for off in range(0, n, step):
             ln = min(step, n - off)
@@ -522,8 +548,13 @@ class ZeroEngine:
 
     def _gather_from_host(self, g: FlatGroup) -> Tuple[torch.Tensor, Handle]:
         """offload_param: stage the host shard H2D on the side stream and all-gather from there (the RCCL work
-        is ordered after the copy, not after the compute queued so far)."""
-        host = self._shard16(g)
+        is ordered after the copy, not after the compute queued so far). NVMe: the shard is first read from the
+        file into a pinned ring slot (C++ AIO), which is released once its H2D copy has run."""
+        slot = None
+        if self.param_nvme is not None:
+            slot, host = self.param_nvme.read(g.shard_off, g.shard_numel)
+        else:
+            host = self._shard16(g)
         if not self.is_cuda:
             stage = host.clone()
             if g.P == 1:
@@ -535,6 +566,10 @@ class ZeroEngine:
                 self._h2d.wait_event(self._p16_ready)
             stage = torch.empty(g.shard_numel, dtype=self.dtype, device=self.device)
             stage.copy_(host, non_blocking=True)
+            if slot is not None:
+                done = torch.cuda.Event()
+                done.record(self._h2d)
+                self.param_nvme.release_after(slot, done)
             if g.P == 1:
                 ev = torch.cuda.Event()
                 ev.record(self._h2d)
@@ -1116,6 +1151,8 @@ class ZeroEngine:
             "grad_shard_GiB": self.shard_total * 4 / gb,
             "param_shard_GiB": 0.0 if self.param_host else self.shard_total * 2 / gb,
             "param_shard_host_GiB": self.shard_total * 2 / gb if self.param_host else 0.0,
+            "param_nvme_ring_GiB": (sum(t.numel() * t.element_size() for t in self.param_nvme.slots) / gb
+                                    if self.param_nvme is not None else 0.0),
             "param_full_GiB": (self.full_total * 2 / gb) if self.p16_full is not None else 0.0,
             "grad_full_GiB": (self.gfull_total * 4 / gb) if self.grad_full is not None else 0.0,
             "weight_T_cache_GiB": sum(t.numel() * t.element_size() for _, c in self._tcache.values()

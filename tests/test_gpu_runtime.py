@@ -101,25 +101,32 @@ def test_trainer_runs_ahead_and_nan_latch_keeps_pre_nan_state(tmp_path):
     assert torch.equal(bad.engine.master, ref.engine.master)
 
 
-def test_offload_param_on_gpu_matches_device_params():
-    """offload_param=cpu: the bf16 partition in pinned host memory, H2D-staged gathers on a side stream."""
+def test_offload_param_on_gpu_matches_device_params(tmp_path):
+    """offload_param=cpu: the bf16 partition in pinned host memory, H2D-staged gathers on a side stream;
+    offload_param=nvme: the partition in a file, read per gather by the C++ AIO engine into pinned ring slots
+    (released by the H2D copy's event) and written back after each device AdamW step."""
     from distributed_llm_training_gpu_manager_amd.models import get_config
     from distributed_llm_training_gpu_manager_amd.parallel.zero import EngineConfig, ZeroEngine
 
     res = {}
-    for name, off in (("dev", "none"), ("host", "cpu")):
+    for name, off in (("dev", "none"), ("host", "cpu"), ("nvme", "nvme")):
         torch.cuda.empty_cache()
         e = ZeroEngine(get_config("llama-small"), EngineConfig(zero_stage=3, seq_len=512, micro_batch_size=1,
-                                                               grad_accum=2, scheduler="constant", offload_param=off),
+                                                               grad_accum=2, scheduler="constant", offload_param=off,
+                                                               nvme_path=str(tmp_path / "nvme")),
                        torch.device("cuda", 0))
         g = torch.Generator(device="cuda").manual_seed(0)
         for _ in range(2):
             mb = [torch.randint(0, 32768, (1, 513), device="cuda", generator=g) for _ in range(2)]
             m = e.train_step([(t[:, :-1], t[:, 1:]) for t in mb])
         torch.cuda.synchronize()
-        res[name] = (float(m["loss"]), e.master.clone(), e.p16_shard.device.type, e.memory_report())
+        res[name] = (float(m["loss"]), e.master.clone(), e.p16_shard.device.type, e.memory_report(),
+                     dict(e.param_nvme.stats) if e.param_nvme is not None else None)
         del e
     assert res["host"][2] == "cpu" and res["dev"][2] == "cuda"
     assert res["host"][3]["param_shard_host_GiB"] > 0 and res["host"][3]["param_shard_GiB"] == 0
-    assert abs(res["host"][0] - res["dev"][0]) < 1e-3
-    assert torch.equal(res["host"][1], res["dev"][1])
+    st = res["nvme"][4]
+    assert st is not None and st["read_GiB"] > 0 and st["write_GiB"] > 0, st
+    for name in ("host", "nvme"):
+        assert abs(res[name][0] - res["dev"][0]) < 1e-3, name
+        assert torch.equal(res[name][1], res["dev"][1]), name

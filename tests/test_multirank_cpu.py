@@ -518,8 +518,11 @@ def _knob_worker(rank, world, port, kw, out):
     comm_mod.Comm.all_gather = orig_ag
     params = eng.full_params()
     if rank == 0:
+        nv = getattr(eng, "param_nvme", None)
         torch.save({"params": params, "grads0": grads0, "ops": ops_seen, "gathers": gathers,
-                    "groups": [(g.name, g.kind, g.P, [s.name for s in g.specs]) for g in eng.groups]}, out)
+                    "groups": [(g.name, g.kind, g.P, [s.name for s in g.specs]) for g in eng.groups],
+                    "nvme": dict(nv.stats, path=nv.path, size=os.path.getsize(nv.path)) if nv is not None else None},
+                   out)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -597,14 +600,26 @@ def test_param_persistence_threshold_keeps_small_tensors_replicated(tmp_path):
 
 def test_offload_param_matches_device_params(tmp_path):
     """offload_param=cpu (ZeRO-Infinity): the bf16 partition is host memory, gathers stage it first; the
-    training is the same as with device-resident parameters, with and without optimizer offload."""
+    training is the same as with device-resident parameters, with and without optimizer offload.
+    offload_param=nvme: the partition is a file read per gather through the C++ AIO engine (and written back
+    after every optimizer step) -- again the same training, alone and with the NVMe optimizer swap."""
     res = {}
+    nv = str(tmp_path / "nvme")
     for name, kw in (("dev", {}), ("par", {"offload_param": "cpu"}),
-                     ("both", {"offload_param": "cpu", "offload_optimizer": "cpu"})):
+                     ("both", {"offload_param": "cpu", "offload_optimizer": "cpu"}),
+                     ("nvme", {"offload_param": "nvme", "nvme_path": nv}),
+                     ("nvme_both", {"offload_param": "nvme", "offload_optimizer": "nvme", "nvme_path": nv})):
         out = str(tmp_path / f"{name}.pt")
         mp.spawn(_knob_worker, args=(2, _port(), kw, out), nprocs=2, join=True)
         res[name] = torch.load(out, weights_only=True)
-    for name in ("par", "both"):
+    for name in ("nvme", "nvme_both"):
+        st = res[name]["nvme"]
+        assert st is not None and st["read_GiB"] > 0, (name, st)  # every gather read the file through AIO
+        assert st["path"].startswith(nv) and st["size"] > 0
+    # device AdamW: the new 16-bit values stream back through AIO (with the host optimizer they are written
+    # in place through the file mapping by the NVMe optimizer swap)
+    assert res["nvme"]["nvme"]["write_GiB"] > 0
+    for name in ("par", "both", "nvme", "nvme_both"):
         for k, v in res["dev"]["grads0"].items():
             assert torch.allclose(res[name]["grads0"][k], v, atol=1e-6, rtol=1e-4), (name, k)
         _compare(res[name], res["dev"]["params"], res["dev"]["grads0"], 2)
