@@ -34,6 +34,7 @@
 #include <torch/all.h>
 #include <c10/hip/HIPStream.h>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 #include "dlgm_common.h"
 
@@ -442,7 +443,8 @@ struct BwdParams {
   const E* v;
   const E* dout;
   const float* lse;    // [B, Hq, S], natural log of sum exp(scale * s)
-  const float* delta;  // [2, B, Hq, S]: -delta, then -lse / scale (flash_bwd_delta_kernel)
+  const float* delta;  // [2, B, Hq, S]: -delta, then -lse / scale (flash_bwd_delta_kernel, or the dQ pass itself)
+  const E* o;          // forward output [B, S, Hq, D] contiguous (read by the dQ pass that computes delta)
   E* dq;            // [B, S, Hq, D]
   float* dk_part;      // [group, B, S, Hkv, D] fp32 partials (one per q head of the GQA group)
   float* dv_part;
@@ -744,8 +746,12 @@ constexpr int kDqThreads = 256;
 constexpr int kDqBQ = 128;
 constexpr int kDqBKV = 64;
 
-template <typename E, int D, bool TAIL, bool FROM_DS = false>
+// DELTA: this pass also computes delta = rowsum(dO * O) for its query rows (it holds dO in registers already)
+// and writes the [-delta, -lse/scale] rows the dK/dV pass reads -- no separate delta launch; the dQ pass then
+// runs first.
+template <typename E, int D, bool TAIL, bool FROM_DS = false, bool DELTA = false>
 __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams<E> p) {
+  static_assert(!(FROM_DS && DELTA), "the stored-dS dQ pass runs after dK/dV");
   constexpr int KK = D / 16;
   constexpr int DT = D / 32;
   constexpr int TILE = kDqBKV * D;
@@ -786,7 +792,27 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams<E
     }
     const int64_t rowc = ((int64_t)b * p.Hq + hq) * p.S;
     lse2 = qcol < p.S ? p.lse[rowc + qcol] * kLog2e : INFINITY;
-    nd = qcol < p.S ? p.delta[rowc + qcol] : 0.f;  // -delta
+    if constexpr (DELTA) {
+      // this lane holds dO[qcol][16kk + 8h .. +7]: the matching O chunks, a 64-term dot, the other half-wave's 64
+      float acc = 0.f;
+      if (qcol < p.S) {
+        const E* orow = p.o + (((int64_t)b * p.S + qcol) * p.Hq + hq) * D + 8 * h;
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+          const vec8_t<E> ov = *reinterpret_cast<const vec8_t<E>*>(orow + 16 * kk);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc += (float)dof[kk][j] * (float)ov[j];
+        }
+      }
+      nd = -(acc + swap_halves(acc));
+      if (qcol < p.S && h == 0) {
+        float* dl = const_cast<float*>(p.delta);
+        dl[rowc + qcol] = nd;
+        dl[(int64_t)p.B * p.Hq * p.S + rowc + qcol] = p.lse[rowc + qcol] * p.neg_inv_scale;
+      }
+    } else {
+      nd = qcol < p.S ? p.delta[rowc + qcol] : 0.f;  // -delta
+    }
   }
 
   f32x16 dqt[DT];
@@ -947,6 +973,12 @@ bool dq_from_ds() {
   return e != nullptr && std::atoi(e) != 0;
 }
 
+// DLGM_ATTN_DELTA_IN_DQ=0: the separate delta launch before dK/dV (default 1: the dQ pass computes delta)
+bool delta_in_dq() {
+  const char* e = std::getenv("DLGM_ATTN_DELTA_IN_DQ");
+  return e == nullptr || std::atoi(e) != 0;
+}
+
 bool bwd_two_streams() {
   static const bool on = [] {
     const char* e = std::getenv("DLGM_ATTN_BWD_STREAMS");
@@ -1076,18 +1108,25 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
   DLGM_DISPATCH_16(q.scalar_type(), E, {
     auto dop = reinterpret_cast<const E*>(dout.data_ptr());
     auto outp = reinterpret_cast<const E*>(out.data_ptr());
-    if (D == 128)
-      flash_bwd_delta_kernel<E, 128><<<(rows + 15) / 16, 256, 0, stream>>>(
-          dop, outp, lse.data_ptr<float>(), delta.data_ptr<float>(), (float)(-1.0 / softmax_scale), B, S, Hq,
-          dout.stride(1), dout.stride(2), dout.stride(0));
-    else
-      flash_bwd_delta_kernel<E, 64><<<(rows + 31) / 32, 256, 0, stream>>>(
-          dop, outp, lse.data_ptr<float>(), delta.data_ptr<float>(), (float)(-1.0 / softmax_scale), B, S, Hq,
-          dout.stride(1), dout.stride(2), dout.stride(0));
-    DLGM_CHECK_HIP(hipGetLastError());
+    // dK/dV and dQ are independent passes over the same inputs: optionally the dQ pass runs on a side stream
+    // (forked and joined with events, so it also works under HIP graph capture)
+    const bool fork = bwd_two_streams() && !from_ds;
+    // default: the dQ pass computes delta itself and runs first (no delta launch)
+    const bool fused = !from_ds && !fork && delta_in_dq();
+    if (!fused) {
+      if (D == 128)
+        flash_bwd_delta_kernel<E, 128><<<(rows + 15) / 16, 256, 0, stream>>>(
+            dop, outp, lse.data_ptr<float>(), delta.data_ptr<float>(), (float)(-1.0 / softmax_scale), B, S, Hq,
+            dout.stride(1), dout.stride(2), dout.stride(0));
+      else
+        flash_bwd_delta_kernel<E, 64><<<(rows + 31) / 32, 256, 0, stream>>>(
+            dop, outp, lse.data_ptr<float>(), delta.data_ptr<float>(), (float)(-1.0 / softmax_scale), B, S, Hq,
+            dout.stride(1), dout.stride(2), dout.stride(0));
+      DLGM_CHECK_HIP(hipGetLastError());
+    }
     BwdParams<E> p{reinterpret_cast<const E*>(q.data_ptr()), reinterpret_cast<const E*>(k.data_ptr()),
                    reinterpret_cast<const E*>(v.data_ptr()), dop, lse.data_ptr<float>(), delta.data_ptr<float>(),
-                   reinterpret_cast<E*>(dq.data_ptr()), nparts > 1 ? dk_part.data_ptr<float>() : nullptr,
+                   outp, reinterpret_cast<E*>(dq.data_ptr()), nparts > 1 ? dk_part.data_ptr<float>() : nullptr,
                    nparts > 1 ? dv_part.data_ptr<float>() : nullptr, /*ds=*/nullptr, reinterpret_cast<E*>(dk.data_ptr()),
                    reinterpret_cast<E*>(dv.data_ptr()), q.stride(0), q.stride(1), q.stride(2), k.stride(0),
                    k.stride(1), k.stride(2), v.stride(0), v.stride(1), v.stride(2), dout.stride(0), dout.stride(1),
@@ -1098,41 +1137,37 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
       dsT = at::empty({B, Hq, S, S}, q.options());
       p.ds = reinterpret_cast<E*>(dsT.data_ptr());
     }
-    // dK/dV and dQ are independent passes over the same inputs: optionally the dQ pass runs on a side stream
-    // (forked and joined with events, so it also works under HIP graph capture)
-    const bool fork = bwd_two_streams() && !from_ds;
     hipStream_t qs = stream;
     if (fork) {
       qs = c10::hip::getStreamFromPool(false, q.get_device()).stream();
       DLGM_CHECK_HIP(hipEventRecord(bwd_event(0), stream));
       DLGM_CHECK_HIP(hipStreamWaitEvent(qs, bwd_event(0), 0));
     }
+    // one (dK/dV, dQ) pair of launches per head dim / tail instantiation
+    auto run = [&](auto dc, auto tc) {
+      constexpr int DD = decltype(dc)::value;
+      constexpr bool TT = decltype(tc)::value;
+      auto dkdv = [&]() {
+        if (hp == 2) flash_bwd_dkdv_kernel<E, DD, TT, false, 2><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+        else flash_bwd_dkdv_kernel<E, DD, TT><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+      };
+      if (fused) {
+        flash_bwd_dq_kernel<E, DD, TT, false, true><<<dq_blocks, kDqThreads, 0, stream>>>(p);
+        dkdv();
+      } else if (from_ds && !TT) {
+        flash_bwd_dkdv_kernel<E, DD, false, true><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+        flash_bwd_dq_kernel<E, DD, false, true><<<dq_blocks, kDqThreads, 0, stream>>>(p);
+      } else {
+        dkdv();
+        flash_bwd_dq_kernel<E, DD, TT><<<dq_blocks, kDqThreads, 0, qs>>>(p);
+      }
+    };
     if (D == 128) {
-      if (tail) {
-        if (hp == 2) flash_bwd_dkdv_kernel<E, 128, true, false, 2><<<kv_blocks, kKvThreads, 0, stream>>>(p);
-        else flash_bwd_dkdv_kernel<E, 128, true><<<kv_blocks, kKvThreads, 0, stream>>>(p);
-        flash_bwd_dq_kernel<E, 128, true><<<dq_blocks, kDqThreads, 0, qs>>>(p);
-      } else if (from_ds) {
-        flash_bwd_dkdv_kernel<E, 128, false, true><<<kv_blocks, kKvThreads, 0, stream>>>(p);
-        flash_bwd_dq_kernel<E, 128, false, true><<<dq_blocks, kDqThreads, 0, stream>>>(p);
-      } else {
-        if (hp == 2) flash_bwd_dkdv_kernel<E, 128, false, false, 2><<<kv_blocks, kKvThreads, 0, stream>>>(p);
-        else flash_bwd_dkdv_kernel<E, 128, false><<<kv_blocks, kKvThreads, 0, stream>>>(p);
-        flash_bwd_dq_kernel<E, 128, false><<<dq_blocks, kDqThreads, 0, qs>>>(p);
-      }
+      if (tail) run(std::integral_constant<int, 128>{}, std::true_type{});
+      else run(std::integral_constant<int, 128>{}, std::false_type{});
     } else {
-      if (tail) {
-        if (hp == 2) flash_bwd_dkdv_kernel<E, 64, true, false, 2><<<kv_blocks, kKvThreads, 0, stream>>>(p);
-        else flash_bwd_dkdv_kernel<E, 64, true><<<kv_blocks, kKvThreads, 0, stream>>>(p);
-        flash_bwd_dq_kernel<E, 64, true><<<dq_blocks, kDqThreads, 0, qs>>>(p);
-      } else if (from_ds) {
-        flash_bwd_dkdv_kernel<E, 64, false, true><<<kv_blocks, kKvThreads, 0, stream>>>(p);
-        flash_bwd_dq_kernel<E, 64, false, true><<<dq_blocks, kDqThreads, 0, stream>>>(p);
-      } else {
-        if (hp == 2) flash_bwd_dkdv_kernel<E, 64, false, false, 2><<<kv_blocks, kKvThreads, 0, stream>>>(p);
-        else flash_bwd_dkdv_kernel<E, 64, false><<<kv_blocks, kKvThreads, 0, stream>>>(p);
-        flash_bwd_dq_kernel<E, 64, false><<<dq_blocks, kDqThreads, 0, qs>>>(p);
-      }
+      if (tail) run(std::integral_constant<int, 64>{}, std::true_type{});
+      else run(std::integral_constant<int, 64>{}, std::false_type{});
     }
     DLGM_CHECK_HIP(hipGetLastError());
     if (fork) {

@@ -203,6 +203,26 @@ def test_flash_attention_bwd_dq_from_stored_ds(monkeypatch, S, Hq, Hkv, D):
         assert rel_err(got, b.cpu()) < 1e-2, rel_err(got, b.cpu())
 
 
+@pytest.mark.parametrize("S,Hq,Hkv,D", [(256, 4, 4, 128), (512, 8, 2, 128), (200, 4, 1, 128), (192, 4, 2, 64)])
+def test_flash_attention_bwd_delta_in_dq(monkeypatch, S, Hq, Hkv, D):
+    """Default backward: the dQ pass computes delta = rowsum(dO * O) itself and runs before dK/dV (no separate
+    delta launch). Same gradients as the separate-delta order (DLGM_ATTN_DELTA_IN_DQ=0) and the fp32 reference."""
+    torch.manual_seed(0)
+    B = 1
+    q, k, v = (torch.randn(B, S, h, D, dtype=torch.bfloat16, device=DEV) for h in (Hq, Hkv, Hkv))
+    do = torch.randn(B, S, Hq, D, dtype=torch.bfloat16, device=DEV)
+    scale = 1 / math.sqrt(D)
+    o, lse = ops.flash_attn_fwd(q, k, v, scale, True)
+    monkeypatch.setenv("DLGM_ATTN_DELTA_IN_DQ", "0")
+    sep = ops.flash_attn_bwd(do, q, k, v, o, lse, scale, True)
+    monkeypatch.setenv("DLGM_ATTN_DELTA_IN_DQ", "1")
+    fused = ops.flash_attn_bwd(do, q, k, v, o, lse, scale, True)
+    ref = attn_ops._ref_bwd(do.cpu(), q.cpu(), k.cpu(), v.cpu(), o.cpu(), lse.cpu(), scale, True)
+    for name, g, s0, want in zip("qkv", fused, sep, ref):
+        assert rel_err(g, want) < 3e-2, (name, rel_err(g, want))
+        assert float((g.float() - s0.float()).abs().max()) <= 1e-2 * float(s0.float().abs().max()), name
+
+
 def test_flash_attention_rescale_branch():
     """Force the online-softmax rescale: one huge key late in the sequence for one query."""
     torch.manual_seed(1)
