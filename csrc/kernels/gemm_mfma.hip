@@ -226,19 +226,22 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
   if constexpr (MODE == kDense) {
     grouped_tile(id, p.tiles_m, tm, tn);
   } else if constexpr (MODE == kGroupM) {
-    tn = id % p.tiles_n;
-    int j = id / p.tiles_n;
+    // expert by expert; within an expert the row tiles run fastest, so the ~32 blocks resident on one XCD
+    // (consecutive ids after the remap) share each weight column panel across all the expert's row tiles
+    // (one HBM read of the panel, the rest L2 hits) instead of streaming every panel once per row tile
+    int j = id;
     grp = -1;
     for (int e = 0; e < p.G; ++e) {
       const int lo = p.offsets[e], hi = p.offsets[e + 1];
       const int te = (hi - lo + BM - 1) / BM;
-      if (j < te) {
+      if (j < te * p.tiles_n) {
         grp = e;
-        m_lo = lo + j * BM;  // this block's first row (absolute)
+        tn = j / te;
+        m_lo = lo + (j - tn * te) * BM;  // this block's first row (absolute)
         m_hi = hi;
         break;
       }
-      j -= te;
+      j -= te * p.tiles_n;
     }
     if (grp < 0) return;  // spare block: the grid is sized for the worst case
   } else {  // grouped-K
