@@ -65,6 +65,8 @@ int64_t dlgm_gemm_lt_version();
 void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bool accumulate,
                     const c10::optional<at::Tensor>& offsets, int64_t mode, int64_t M, int64_t N, int64_t K,
                     int64_t G, int64_t b_gstride);
+void dlgm_gemm_mfma_seg(at::Tensor out, const std::vector<at::Tensor>& a, const std::vector<at::Tensor>& b,
+                        const at::Tensor& offsets, bool accumulate);
 
 TORCH_LIBRARY(dlgm, m) {
   m.def("rmsnorm_fwd(Tensor x, Tensor? residual, Tensor w, float eps) -> (Tensor, Tensor, Tensor)");
@@ -91,6 +93,7 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("gemm_lt_tune(Tensor out, Tensor a, Tensor b, float beta, int n_heuristic, bool all_algos, int reps) -> Tensor");
   m.def("gemm_lt_version() -> int", &dlgm_gemm_lt_version);
   m.def("gemm_mfma(Tensor(a!) out, Tensor a, Tensor b, bool accumulate, Tensor? offsets, int mode, int M, int N, int K, int G, int b_gstride) -> ()");
+  m.def("gemm_mfma_seg(Tensor(a!) out, Tensor[] a, Tensor[] b, Tensor offsets, bool accumulate) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dlgm, CUDA, m) {
@@ -117,4 +120,5 @@ TORCH_LIBRARY_IMPL(dlgm, CUDA, m) {
   m.impl("gemm_lt", &dlgm_gemm_lt);
   m.impl("gemm_lt_tune", &dlgm_gemm_lt_tune);
   m.impl("gemm_mfma", &dlgm_gemm_mfma);
+  m.impl("gemm_mfma_seg", &dlgm_gemm_mfma_seg);
 }

@@ -43,12 +43,18 @@ typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 typedef __attribute__((address_space(3))) void* lptr_t;
 
 enum Epi { kStoreBf16 = 0, kStoreF32 = 1, kAccF32 = 2 };
-enum Mode { kDense = 0, kGroupM = 1, kGroupK = 2 };
+enum Mode { kDense = 0, kGroupM = 1, kGroupK = 2, kGroupKSeg = 3 };
+constexpr int kMaxSeg = 16;  // grouped-K over segments: at most this many (micro-batch) row sets per launch
 
 struct GemmArgs {
   const bf16* a;
   const bf16* b;
   void* c;
+  // kGroupKSeg: segment s has its own token-major operands (a_seg[s] [R_s, M], b_seg[s] [R_s, N]) and
+  // offsets[s * (G + 1) ..] split its rows by group; group g reduces over its rows of every segment
+  const bf16* a_seg[kMaxSeg];
+  const bf16* b_seg[kMaxSeg];
+  int nseg;
   int64_t lda, ldb, ldc;           // leading (non-unit) strides in elements
   int64_t a_gstride, b_gstride, c_gstride;  // per-group pointer steps (elements) for grouped modes
   const int* offsets;              // [G + 1] exclusive prefix over the grouped dimension (device)
@@ -244,16 +250,32 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
       j -= te * p.tiles_n;
     }
     if (grp < 0) return;  // spare block: the grid is sized for the worst case
-  } else {  // grouped-K
+  } else {  // grouped-K (one segment, or kGroupKSeg: the group's rows of every segment)
     const int per = p.tiles_m * p.tiles_n;
     grp = id / per;
     grouped_tile(id - grp * per, p.tiles_m, tm, tn);
-    k_lo = p.offsets[grp];
-    k_hi = p.offsets[grp + 1];
+    if constexpr (MODE == kGroupK) {
+      k_lo = p.offsets[grp];
+      k_hi = p.offsets[grp + 1];
+    }
   }
-  const bf16* A = p.a;
-  const bf16* B = p.b + (MODE == kGroupM ? (int64_t)grp * p.b_gstride : 0);
-  char* C = (char*)p.c + (MODE == kGroupK ? (int64_t)grp * p.c_gstride * CES : 0);
+  // kGroupKSeg: cumulative K-tile counts over the segments (seg_cum[s] = first K-tile of segment s)
+  int seg_cum[kMaxSeg + 1];
+  seg_cum[0] = 0;
+  if constexpr (MODE == kGroupKSeg) {
+#pragma unroll
+    for (int sg = 0; sg < kMaxSeg; ++sg) {
+      int n = 0;
+      if (sg < p.nseg) {
+        const int lo = p.offsets[sg * (p.G + 1) + grp], hi = p.offsets[sg * (p.G + 1) + grp + 1];
+        n = (hi - lo + BK - 1) / BK;
+      }
+      seg_cum[sg + 1] = seg_cum[sg] + n;
+    }
+  }
+  const bf16* A0 = p.a;
+  const bf16* B0 = p.b + (MODE == kGroupM ? (int64_t)grp * p.b_gstride : 0);
+  char* C = (char*)p.c + (MODE == kGroupK || MODE == kGroupKSeg ? (int64_t)grp * p.c_gstride * CES : 0);
   const int m0 = MODE == kGroupM ? m_lo : tm * BM;
   const int n0 = tn * BN;
   const int rows_valid = min(BM, m_hi - m0);
@@ -265,9 +287,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4)(0.f);
 
-  const int nk = (k_hi - k_lo + BK - 1) / BK;
+  const int nk = MODE == kGroupKSeg ? seg_cum[kMaxSeg] : (k_hi - k_lo + BK - 1) / BK;
   // partial tiles: K (grouped-K group ends), M rows (K-contiguous A: grouped-M group ends / M % 256 != 0)
-  constexpr bool PK = MODE == kGroupK, PM = AK;
+  constexpr bool PK = MODE == kGroupK || MODE == kGroupKSeg, PM = AK;
   if (nk > 0) {
     const HalfStager<AK, 0> sa(p.lda, w, lane);
     const HalfStager<BKM, 1> sb(p.ldb, w, lane);
@@ -275,8 +297,26 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
     // stage half h of operand op for K-tile t (skipped past the end); returns whether anything was issued
     auto stage = [&](int op, int h, int t) -> bool {
       if (t >= nk) return false;
-      const int k0 = k_lo + t * BK;
-      const int kv = min(BK, k_hi - k0);
+      int k0, kv;
+      const bf16* A = A0;
+      const bf16* B = B0;
+      if constexpr (MODE == kGroupKSeg) {
+        int sg = 0;  // the segment holding K-tile t (empty segments are stepped over)
+#pragma unroll
+        for (int q = 1; q < kMaxSeg; ++q) sg += t >= seg_cum[q] ? 1 : 0;
+        sg = __builtin_amdgcn_readfirstlane(sg);
+        int cum = 0;
+#pragma unroll
+        for (int q = 0; q < kMaxSeg; ++q) cum = q == sg ? seg_cum[q] : cum;
+        const int lo = p.offsets[sg * (p.G + 1) + grp], hi = p.offsets[sg * (p.G + 1) + grp + 1];
+        k0 = lo + (t - cum) * BK;
+        kv = min(BK, hi - k0);
+        A = p.a_seg[sg];
+        B = p.b_seg[sg];
+      } else {
+        k0 = k_lo + t * BK;
+        kv = min(BK, k_hi - k0);
+      }
       char* img = region(t & 1, op, h);
       if (op == 0) {
         if constexpr (AK)
@@ -488,5 +528,61 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
   } else {  // token-major operands (checked above)
     launch_epi<kGroupK, false, false>(epi, grid, st, p);
   }
+  DLGM_CHECK_HIP(hipGetLastError());
+}
+
+// Grouped-K over segments: out[g] (+)= sum over s of a[s][rows of g in s]^T @ b[s][rows of g in s], with
+// a[s] [R_s, M] and b[s] [R_s, N] token-major (row-major) bf16 and offsets [nseg, G + 1] int32 on the device
+// (offsets[s] splits segment s's rows by group). One launch reduces each group over all its rows of every
+// segment -- e.g. an expert's weight gradient over the step's micro-batches -- without concatenating them.
+void dlgm_gemm_mfma_seg(at::Tensor out, const std::vector<at::Tensor>& a, const std::vector<at::Tensor>& b,
+                        const at::Tensor& offsets, bool accumulate) {
+  const int nseg = (int)a.size();
+  TORCH_CHECK(nseg >= 1 && nseg <= kMaxSeg && (int)b.size() == nseg, "gemm_mfma_seg: 1..16 segments, a/b paired");
+  TORCH_CHECK(out.is_cuda() && out.dim() == 3 && out.is_contiguous() && out.scalar_type() == at::kFloat,
+              "gemm_mfma_seg: out [G, M, N] contiguous fp32");
+  const int64_t G = out.size(0), M = out.size(1), N = out.size(2);
+  TORCH_CHECK(M % BM == 0 && N % BN == 0, "gemm_mfma_seg: M and N must be multiples of 256");
+  TORCH_CHECK(offsets.is_cuda() && offsets.scalar_type() == at::kInt && offsets.is_contiguous() &&
+                  offsets.dim() == 2 && offsets.size(0) == nseg && offsets.size(1) == G + 1,
+              "gemm_mfma_seg: offsets [nseg, G + 1] int32 on the GPU");
+  GemmArgs p{};
+  for (int s = 0; s < nseg; ++s) {
+    const at::Tensor& x = a[s];
+    const at::Tensor& y = b[s];
+    TORCH_CHECK(x.is_cuda() && y.is_cuda() && x.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16,
+                "gemm_mfma_seg: bf16 GPU operands");
+    TORCH_CHECK(x.dim() == 2 && y.dim() == 2 && x.size(1) == M && y.size(1) == N && x.size(0) == y.size(0) &&
+                    x.stride(1) == 1 && y.stride(1) == 1,
+                "gemm_mfma_seg: a[s] [R_s, M] and b[s] [R_s, N] row-major");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0,
+                "gemm_mfma_seg: operands 16-byte aligned");
+    if (s == 0) {
+      p.lda = x.stride(0);
+      p.ldb = y.stride(0);
+    }
+    TORCH_CHECK(x.stride(0) == p.lda && y.stride(0) == p.ldb && p.lda % 8 == 0 && p.ldb % 8 == 0,
+                "gemm_mfma_seg: one row stride per operand across segments, 16-byte rows");
+    p.a_seg[s] = reinterpret_cast<const bf16*>(x.data_ptr());
+    p.b_seg[s] = reinterpret_cast<const bf16*>(y.data_ptr());
+  }
+  p.a = p.a_seg[0];
+  p.b = p.b_seg[0];
+  p.c = out.data_ptr();
+  p.ldc = N;
+  p.nseg = nseg;
+  p.offsets = offsets.data_ptr<int>();
+  p.M = (int)M;
+  p.N = (int)N;
+  p.K = 0;
+  p.G = (int)G;
+  p.mode = kGroupKSeg;
+  p.c_gstride = out.stride(0);
+  p.tiles_n = (int)(N / BN);
+  p.tiles_m = (int)(M / BM);
+  const int64_t nblk = G * (int64_t)p.tiles_m * p.tiles_n;
+  if (nblk == 0) return;
+  launch_epi<kGroupKSeg, false, false>(accumulate ? kAccF32 : kStoreF32, dim3((unsigned)nblk),
+                                       c10::hip::getCurrentHIPStream(), p);
   DLGM_CHECK_HIP(hipGetLastError());
 }

@@ -223,42 +223,17 @@ class MixtralBlock(LlamaBlock):
         self._wstash, self._wflushed, self._wbytes = [], True, 0
 
     def _flush_wgrad_grouped(self, g: Params) -> None:
-        """Deferred expert dW with device offsets: every stashed micro-batch's rows are scattered into one
-        expert-major tensor per operand (positions computed on the device from the routing counts; no host
-        read), then ONE grouped GEMM per weight reduces each expert over all its rows of the step."""
+        """Deferred expert dW with device offsets: ONE segmented grouped GEMM per weight reduces each expert over
+        its rows of every stashed micro-batch (segment = micro-batch, its offsets row = that micro-batch's
+        routing; no host read, no concatenation of the rows)."""
         stash, acc = self._wstash, self._wflushed
         self._wstash, self._wflushed, self._wbytes = [], True, 0
-        if len(stash) == 1:
-            dy, a, dgu, x, offs = stash[0]
-            gm.grouped_wgrad(g["w_down"], dy, a, offs, acc)
-            gm.grouped_wgrad(g["w_gate_up"], dgu, x, offs, acc)
-            return
-        dev = stash[0][0].device
-        counts = torch.stack([o[1:] - o[:-1] for *_, o in stash]).to(torch.long)  # [micro-batches, experts]
-        tot = counts.sum(0)
-        new_off = torch.zeros(self.E_local + 1, dtype=torch.int32, device=dev)
-        new_off[1:] = tot.cumsum(0)
-        # destination of micro-batch m's first row of expert e: the expert's start + rows of earlier micro-batches
-        dst0 = new_off[:-1].to(torch.long).unsqueeze(0) + (counts.cumsum(0) - counts)
-        rows = [t[0].shape[0] for t in stash]
-        R = sum(rows)
-        idx = []
-        for m, (*_, o) in enumerate(stash):
-            shift = dst0[m] - o[:-1].to(torch.long)
-            idx.append(torch.arange(rows[m], device=dev) +
-                       torch.repeat_interleave(shift, counts[m], output_size=rows[m]))
-
-        def merged(k: int) -> torch.Tensor:
-            t0 = stash[0][k]
-            out = t0.new_empty((R, t0.shape[1]))
-            for m in range(len(stash)):
-                out.index_copy_(0, idx[m], stash[m][k])
-            return out
-        dy_m, a_m = merged(0), merged(1)
-        gm.grouped_wgrad(g["w_down"], dy_m, a_m, new_off, acc)
-        del dy_m, a_m
-        dgu_m, x_m = merged(2), merged(3)
-        gm.grouped_wgrad(g["w_gate_up"], dgu_m, x_m, new_off, acc)
+        for i in range(0, len(stash), gm.MAX_SEGMENTS):
+            part = stash[i:i + gm.MAX_SEGMENTS]
+            offs = torch.stack([o for *_, o in part])  # [segments, experts + 1] int32, on the device
+            gm.grouped_wgrad_segments(g["w_down"], [t[0] for t in part], [t[1] for t in part], offs, acc or i > 0)
+            gm.grouped_wgrad_segments(g["w_gate_up"], [t[2] for t in part], [t[3] for t in part], offs,
+                                      acc or i > 0)
 
     def moe_backward(self, p: Params, g: Params, hn2: torch.Tensor, saved, dout: torch.Tensor, ctx: StepContext):
         c = self.cfg

@@ -3,6 +3,7 @@
 ``mfma_mm(out, a, b, acc)``   out (+)= a @ b for bf16 operand views of any unit-stride layout (gemm_mfma.hip)
 ``grouped_mm(x, w, offsets)`` expert-grouped forward / input-gradient GEMM (rows split by offsets)
 ``grouped_wgrad(out, a, b, offsets)`` expert-grouped weight gradient (reduction rows split by offsets)
+``grouped_wgrad_segments(out, a_list, b_list, offsets)`` the same over several row sets (micro-batches) at once
 
 The group offsets are an int32 device tensor, so an MoE layer launches its expert GEMMs without
 reading the routing counts on the host (graph-capture safe). CPU tensors take an fp32 reference path
@@ -111,6 +112,35 @@ def grouped_wgrad(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, offsets: 
     for e in range(G):
         lo, hi = offs[e], offs[e + 1]
         r = a[lo:hi].float().t() @ b[lo:hi].float()
+        if acc:
+            out[e].add_(r.to(out.dtype))
+        else:
+            out[e].copy_(r.to(out.dtype))
+    return out
+
+
+MAX_SEGMENTS = 16
+
+
+def grouped_wgrad_segments(out: torch.Tensor, a: list, b: list, offsets: torch.Tensor,
+                           acc: bool = False) -> torch.Tensor:
+    """out[e] (+)= sum_s a[s][rows of e in s]^T @ b[s][rows of e in s]: a[s] [R_s, M], b[s] [R_s, N] row-major,
+    offsets [S, G + 1] int32 (row s splits segment s by group), out [G, M, N] fp32. One launch reduces every
+    group over its rows of all the segments (the step's micro-batches) without concatenating them."""
+    G, M, N = out.shape
+    if use_native(out):
+        assert len(a) <= MAX_SEGMENTS
+        hip_ops().gemm_mfma_seg(out, list(a), list(b), offsets, acc)
+        return out
+    offs = offsets.tolist()
+    for e in range(G):
+        r = None
+        for s, (x, y) in enumerate(zip(a, b)):
+            lo, hi = offs[s][e], offs[s][e + 1]
+            part = x[lo:hi].float().t() @ y[lo:hi].float()
+            r = part if r is None else r + part
+        if r is None:
+            r = torch.zeros(M, N)
         if acc:
             out[e].add_(r.to(out.dtype))
         else:

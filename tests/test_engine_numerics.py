@@ -308,8 +308,8 @@ def test_llama_chunked_head_matches_autograd_gpu(monkeypatch):
 
 def test_mixtral_grouped_deferred_wgrad_matches_per_micro_batch_cpu(monkeypatch):
     """The grouped expert path (device offsets) with the weight gradients deferred to the step's last
-    micro-batch -- every micro-batch's rows scattered expert-major on the device, one grouped dW GEMM per
-    weight -- equals the per-micro-batch grouped dW. CPU run of the same code (grouped ops' reference path)."""
+    micro-batch -- one segmented grouped dW GEMM per weight over every stashed micro-batch's rows -- equals the
+    per-micro-batch grouped dW. CPU run of the same code (grouped ops' reference path)."""
     from distributed_llm_training_gpu_manager_amd.models.mixtral import MixtralBlock
     from distributed_llm_training_gpu_manager_amd.parallel.zero import EngineConfig, ZeroEngine
     monkeypatch.setattr(MixtralBlock, "_grouped", lambda self, x, wgrad=False: True)

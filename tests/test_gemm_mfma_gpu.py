@@ -109,6 +109,35 @@ def test_grouped_weight_gradient_uneven_and_empty_groups():
         lo += n
 
 
+@pytest.mark.parametrize("nseg", [1, 3, 16])
+def test_grouped_weight_gradient_over_segments(nseg):
+    """Segmented grouped-K (the deferred expert dW over a step's micro-batches): every group reduces over its
+    rows of all segments; segments route differently (uneven, empty groups, a segment with no rows for a
+    group, partial K tiles at every segment end); store and accumulate epilogues."""
+    g = torch.Generator(device=dev).manual_seed(4 + nseg)
+    G, M, N = 4, 256, 512
+    segs = []
+    for s in range(nseg):
+        sizes = [int(x) for x in torch.randint(0, 200, (G,), generator=torch.Generator().manual_seed(s))]
+        sizes[s % G] = 0  # a group with no rows in this segment
+        R = sum(sizes)
+        offs = [0] + list(torch.tensor(sizes).cumsum(0).tolist())
+        segs.append((torch.randn(R, M, device=dev, generator=g).to(torch.bfloat16),
+                     torch.randn(R, N, device=dev, generator=g).to(torch.bfloat16), offs))
+    offsets = torch.tensor([o for *_, o in segs], dtype=torch.int32, device=dev)
+    ref = torch.zeros(G, M, N, device=dev)
+    for a, b, o in segs:
+        for e in range(G):
+            ref[e] += a[o[e]:o[e + 1]].float().t() @ b[o[e]:o[e + 1]].float()
+    out = torch.full((G, M, N), 5.0, device=dev)
+    gm.grouped_wgrad_segments(out, [s[0] for s in segs], [s[1] for s in segs], offsets)
+    assert _rel(out, ref) < 1e-5
+    base = torch.randn(G, M, N, device=dev, generator=g)
+    out2 = base.clone()
+    gm.grouped_wgrad_segments(out2, [s[0] for s in segs], [s[1] for s in segs], offsets, acc=True)
+    assert _rel(out2, ref + base) < 1e-5
+
+
 def test_grouped_forward_reads_nothing_on_the_host(monkeypatch):
     """The grouped MFMA expert GEMM takes the routing offsets on the device only: run it inside a HIP graph
     capture (which fails on any synchronising call) with offsets that differ from the warm-up call.
