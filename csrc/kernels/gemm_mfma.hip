@@ -44,7 +44,7 @@ typedef __attribute__((address_space(3))) void* lptr_t;
 
 enum Epi { kStoreBf16 = 0, kStoreF32 = 1, kAccF32 = 2 };
 enum Mode { kDense = 0, kGroupM = 1, kGroupK = 2, kGroupKSeg = 3 };
-constexpr int kMaxSeg = 16;  // grouped-K over segments: at most this many (micro-batch) row sets per launch
+constexpr int kMaxSeg = 8;  // grouped-K over segments: at most this many (micro-batch) row sets per launch
 
 struct GemmArgs {
   const bf16* a;
@@ -259,18 +259,22 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
       k_hi = p.offsets[grp + 1];
     }
   }
-  // kGroupKSeg: cumulative K-tile counts over the segments (seg_cum[s] = first K-tile of segment s)
-  int seg_cum[kMaxSeg + 1];
+  // kGroupKSeg: this group's row range in every segment and the cumulative K-tile counts (seg_cum[s] = first
+  // K-tile of segment s), loaded once: the stage calls inside the pipelined loop then select among registers
+  // (a scalar load there would add an lgkmcnt wait, which also drains the in-flight LDS fragment reads)
+  int seg_cum[kMaxSeg + 1], seg_lo[kMaxSeg], seg_hi[kMaxSeg];
   seg_cum[0] = 0;
   if constexpr (MODE == kGroupKSeg) {
 #pragma unroll
     for (int sg = 0; sg < kMaxSeg; ++sg) {
-      int n = 0;
+      int lo = 0, hi = 0;
       if (sg < p.nseg) {
-        const int lo = p.offsets[sg * (p.G + 1) + grp], hi = p.offsets[sg * (p.G + 1) + grp + 1];
-        n = (hi - lo + BK - 1) / BK;
+        lo = p.offsets[sg * (p.G + 1) + grp];
+        hi = p.offsets[sg * (p.G + 1) + grp + 1];
       }
-      seg_cum[sg + 1] = seg_cum[sg] + n;
+      seg_lo[sg] = __builtin_amdgcn_readfirstlane(lo);
+      seg_hi[sg] = __builtin_amdgcn_readfirstlane(hi);
+      seg_cum[sg + 1] = seg_cum[sg] + (seg_hi[sg] - seg_lo[sg] + BK - 1) / BK;
     }
   }
   const bf16* A0 = p.a;
@@ -301,18 +305,19 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
       const bf16* A = A0;
       const bf16* B = B0;
       if constexpr (MODE == kGroupKSeg) {
-        int sg = 0;  // the segment holding K-tile t (empty segments are stepped over)
+        // the segment holding K-tile t (empty segments are stepped over), selected among registers
+        int cum = 0, lo = 0, hi = 0;
 #pragma unroll
-        for (int q = 1; q < kMaxSeg; ++q) sg += t >= seg_cum[q] ? 1 : 0;
-        sg = __builtin_amdgcn_readfirstlane(sg);
-        int cum = 0;
-#pragma unroll
-        for (int q = 0; q < kMaxSeg; ++q) cum = q == sg ? seg_cum[q] : cum;
-        const int lo = p.offsets[sg * (p.G + 1) + grp], hi = p.offsets[sg * (p.G + 1) + grp + 1];
+        for (int q = 0; q < kMaxSeg; ++q) {
+          const bool in = t >= seg_cum[q];
+          cum = in ? seg_cum[q] : cum;
+          lo = in ? seg_lo[q] : lo;
+          hi = in ? seg_hi[q] : hi;
+          A = in ? p.a_seg[q] : A;
+          B = in ? p.b_seg[q] : B;
+        }
         k0 = lo + (t - cum) * BK;
         kv = min(BK, hi - k0);
-        A = p.a_seg[sg];
-        B = p.b_seg[sg];
       } else {
         k0 = k_lo + t * BK;
         kv = min(BK, k_hi - k0);
@@ -538,7 +543,7 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
 void dlgm_gemm_mfma_seg(at::Tensor out, const std::vector<at::Tensor>& a, const std::vector<at::Tensor>& b,
                         const at::Tensor& offsets, bool accumulate) {
   const int nseg = (int)a.size();
-  TORCH_CHECK(nseg >= 1 && nseg <= kMaxSeg && (int)b.size() == nseg, "gemm_mfma_seg: 1..16 segments, a/b paired");
+  TORCH_CHECK(nseg >= 1 && nseg <= kMaxSeg && (int)b.size() == nseg, "gemm_mfma_seg: 1..8 segments, a/b paired");
   TORCH_CHECK(out.is_cuda() && out.dim() == 3 && out.is_contiguous() && out.scalar_type() == at::kFloat,
               "gemm_mfma_seg: out [G, M, N] contiguous fp32");
   const int64_t G = out.size(0), M = out.size(1), N = out.size(2);

@@ -52,10 +52,12 @@ class MixtralBlock(LlamaBlock):
         c = self.cfg
         out_std = c.init_std / (2 * c.n_layers) ** 0.5
         off = self.ep_rank * self.E_local
+        # tcache: the engine keeps [E, in, out] transposes (budgeted), so the expert dX GEMMs read K-contiguous
+        # weights (the layout both the grouped MFMA kernel and hipBLASLt run fastest)
         return [ParamSpec("w_gate_up", (self.E_local, 2 * c.ffn_dim, c.d_model), std=c.init_std,
-                          experts=self.E_local, expert_offset=off),
+                          experts=self.E_local, expert_offset=off, tcache=True),
                 ParamSpec("w_down", (self.E_local, c.d_model, c.ffn_dim), std=out_std,
-                          experts=self.E_local, expert_offset=off)]
+                          experts=self.E_local, expert_offset=off, tcache=True)]
 
     def dispatcher(self, ctx: StepContext) -> ExpertDispatcher:
         if self._dispatcher is None:
@@ -112,15 +114,31 @@ class MixtralBlock(LlamaBlock):
             off += n
         return y, (gu_all, a_all, dctx)
 
+    @staticmethod
+    def _grouped_dx(dy: torch.Tensor, p: Params, name: str, offs: torch.Tensor) -> torch.Tensor:
+        """dy @ W[e] per expert rows; through the cached [E, in, out] transpose when the engine keeps one."""
+        wt = p.get(name + ".T")
+        if wt is not None:
+            return gm.grouped_mm(dy, wt, offs, transpose_w=True)
+        return gm.grouped_mm(dy, p[name], offs, transpose_w=False)
+
+    @staticmethod
+    def _expert_dx(dy: torch.Tensor, p: Params, name: str, e: int, out: torch.Tensor) -> None:
+        wt = p.get(name + ".T")
+        if wt is not None:
+            torch.mm(dy, wt[e].t(), out=out)
+        else:
+            torch.mm(dy, p[name][e], out=out)
+
     def _experts_bwd(self, p: Params, g: Params, x: torch.Tensor, dy: torch.Tensor, saved, acc: bool, ctx=None):
         gu_all, a_all, dctx = saved
         if self._grouped(x):
             offs = dctx.local_offsets
             dy = dy.contiguous()
-            da_all = gm.grouped_mm(dy, p["w_down"], offs, transpose_w=False)
+            da_all = self._grouped_dx(dy, p, "w_down", offs)
             dgu_all = ops.swiglu_bwd(da_all, gu_all)
             del da_all
-            dx = gm.grouped_mm(dgu_all, p["w_gate_up"], offs, transpose_w=False)
+            dx = self._grouped_dx(dgu_all, p, "w_gate_up", offs)
             if ctx is not None and ctx.defer_wgrad:
                 # dW once per step over the micro-batches' rows regrouped expert-major on the device
                 if ctx.micro_index == 0:
@@ -153,7 +171,7 @@ class MixtralBlock(LlamaBlock):
             dye = dy.narrow(0, off, n)
             if not gw:
                 grad_mm(g["w_down"][e], dye.t(), a_all.narrow(0, off, n), acc)
-            torch.mm(dye, p["w_down"][e], out=da_all.narrow(0, off, n))
+            self._expert_dx(dye, p, "w_down", e, da_all.narrow(0, off, n))
             off += n
         dgu_all = ops.swiglu_bwd(da_all, gu_all)  # one launch over every expert's rows
         del da_all
@@ -165,7 +183,7 @@ class MixtralBlock(LlamaBlock):
                 dgu = dgu_all.narrow(0, off, n)
                 if not gw:
                     grad_mm(g["w_gate_up"][e], dgu.t(), x.narrow(0, off, n), acc)
-                torch.mm(dgu, p["w_gate_up"][e], out=dx.narrow(0, off, n))
+                self._expert_dx(dgu, p, "w_gate_up", e, dx.narrow(0, off, n))
             off += n
         return dx
 
@@ -184,14 +202,14 @@ class MixtralBlock(LlamaBlock):
         off = 0
         for e, n in enumerate(counts):
             if n:
-                torch.mm(dy.narrow(0, off, n), p["w_down"][e], out=da_all.narrow(0, off, n))
+                self._expert_dx(dy.narrow(0, off, n), p, "w_down", e, da_all.narrow(0, off, n))
             off += n
         dgu_all = ops.swiglu_bwd(da_all, gu_all)
         del da_all
         off = 0
         for e, n in enumerate(counts):
             if n:
-                torch.mm(dgu_all.narrow(0, off, n), p["w_gate_up"][e], out=dx.narrow(0, off, n))
+                self._expert_dx(dgu_all.narrow(0, off, n), p, "w_gate_up", e, dx.narrow(0, off, n))
             off += n
         self._wstash.append((dy, a_all, dgu_all, x, list(counts)))
         self._wbytes += sum(t.numel() * t.element_size() for t in (dy, a_all, dgu_all, x))

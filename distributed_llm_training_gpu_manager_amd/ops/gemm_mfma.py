@@ -27,13 +27,16 @@ from .._native import hip_ops, use_native
 
 DENSE, GROUP_M, GROUP_K = 0, 1, 2
 # Expert GEMM strategy (DLGM_MOE_GROUPED):
-#   "0"     (default) the per-expert hipBLASLt loop: reads the routing counts on the host once per layer and
-#           micro-batch (the forward's read is reused by the backward);
-#   "1"     every expert GEMM as one grouped MFMA launch with the device offsets: no host read at all;
+#   "1"     (default) every expert GEMM as one grouped MFMA launch with the device offsets: no host read of the
+#           routing counts at all (graph-capture safe); the input-gradient GEMMs read the engine's cached
+#           [E, in, out] weight transposes, the deferred weight gradients run as ONE segmented launch per weight
+#           over the step's micro-batches;
+#   "0"     the per-expert hipBLASLt loop: reads the routing counts on the host once per layer and micro-batch;
 #   "wgrad" only the weight gradients grouped (MFMA), forward / dX per expert through hipBLASLt.
-# Mixtral-8x7B (2 layers, seq 4096, GA 4, one MI355X, round 3): loop 128.3k tok/s (MFU 0.294), all-grouped
-# MFMA 115.1k (0.263) -- the host read costs less than the grouped kernel's gap to hipBLASLt.
-_MODE = os.environ.get("DLGM_MOE_GROUPED", "0")
+# Mixtral-8x7B (2 layers, seq 4096, GA 4, one MI355X, round 3): grouped 120.0k tok/s (MFU 0.27) vs loop 125.0k
+# (0.29) -- 4 % for no host synchronisation in the micro-batch loop (was 115.1k vs 128.3k before the grouped-M
+# tile order, the segmented dW and the expert W^T cache; profiles/moe_experiments_r01.md).
+_MODE = os.environ.get("DLGM_MOE_GROUPED", "1")
 GROUPED = _MODE == "1"
 GROUPED_WGRAD = _MODE in ("1", "wgrad") and os.environ.get("DLGM_MOE_GROUPED_WGRAD", "1") != "0"
 
@@ -119,7 +122,7 @@ def grouped_wgrad(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, offsets: 
     return out
 
 
-MAX_SEGMENTS = 16
+MAX_SEGMENTS = 8
 
 
 def grouped_wgrad_segments(out: torch.Tensor, a: list, b: list, offsets: torch.Tensor,

@@ -114,6 +114,7 @@ def plan_rank(m: ModelConfig, *, world: int, zero_stage: int = 3, micro_batch: i
               local_grad_accum="hbm", local_grad_hbm_fraction: float = 0.15, max_live_parameters="hbm",
               max_reuse_distance="hbm", live_hbm_fraction: float = 0.12, prefetch_bucket_size: float = 5e8,
               transposed_weight_cache: bool = True, tcache_hbm_fraction: float = 0.08,
+              expert_weight_cache: bool = True,
               defer_expert_wgrad="auto", defer_wgrad_budget_gb: float = 48.0,
               offload_optimizer: str = "none", offload_param: str = "none",
               hbm_bytes: float = MI355X_HBM, headroom: float = 0.10) -> RankPlan:
@@ -182,6 +183,16 @@ def plan_rank(m: ModelConfig, *, world: int, zero_stage: int = 3, micro_batch: i
             plan.notes.append(f"parameters on {offload_param}: {2.0 * shard / GiB:.1f} GiB host")
     parts["runtime_reserve"] = runtime_reserve(sum(parts.values()))
     tc_names = lambda g: [sp for sp in g.specs if sp.tcache and len(sp.shape) == 2]  # noqa: E731
+    # expert-stacked [E, out, in] weights of groups that are never gathered (ZeroEngine.__init__: within
+    # tcache_hbm_fraction of the device, in group order)
+    stacked, sused = 0.0, 0.0
+    if transposed_weight_cache and expert_weight_cache:
+        for g in groups:
+            if zero_stage < 3 or g.P == 1:
+                nb = 2.0 * sum(sp.numel for sp in g.specs if sp.tcache and len(sp.shape) == 3)
+                if nb and sused + nb <= tcache_hbm_fraction * hbm_bytes:
+                    sused += nb
+        stacked = sused
     if zero_stage == 3 and not host_par:
         committed = sum(parts.values())
         live_params, tc_budget = zero3_budgets(hbm_bytes, committed, live_hbm_fraction, tcache_hbm_fraction,
@@ -204,9 +215,9 @@ def plan_rank(m: ModelConfig, *, world: int, zero_stage: int = 3, micro_batch: i
                 if nb and g.P > 1 and rp.held_through_step(g.idx) and used + nb <= budget:
                     used += nb
             tc += used
-        parts["bf16_weight_T_cache"] = tc
+        parts["bf16_weight_T_cache"] = tc + stacked
     elif transposed_weight_cache and zero_stage < 3:
-        parts["bf16_weight_T_cache"] = 2.0 * sum(sp.numel for g in groups for sp in tc_names(g))
+        parts["bf16_weight_T_cache"] = 2.0 * sum(sp.numel for g in groups for sp in tc_names(g)) + stacked
     return plan
 
 

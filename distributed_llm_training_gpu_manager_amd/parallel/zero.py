@@ -42,6 +42,7 @@ Schedule (one micro-batch)
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence, Tuple
@@ -140,6 +141,9 @@ class EngineConfig:
     # ZeRO-3 (P > 1): groups the residency plan holds gathered for the whole step get the W^T cache too,
     # while the caches fit in this fraction of HBM (Llama-3-8B: 14 GiB) and in what the HBM plan leaves
     tcache_hbm_fraction: float = 0.08
+    # W^T cache also for expert-stacked [E, out, in] weights of never-gathered groups (expert dX GEMMs read
+    # K-contiguous weights), within tcache_hbm_fraction of the device (env DLGM_EXPERT_WT=0 turns it off)
+    expert_weight_cache: bool = True
     init_device: str = "auto"  # "cpu" gives bit-identical init on any device (tests); auto: cpu below 1e9 params
     # replay the GA micro-batches of a step (forward + backward + gradient accumulation) as ONE captured
     # HIP graph: one launch instead of ~30 kernel launches per layer per micro-batch, for models whose
@@ -339,10 +343,21 @@ class ZeroEngine:
         self._pver = 0  # bumped whenever the bf16 compute copy changes
         self._tcache: Dict[int, Tuple[int, Dict[str, torch.Tensor]]] = {}
         self._tnames: Dict[int, List[Tuple[str, Tuple[int, ...]]]] = {}
+        self._expert_wt = cfg.expert_weight_cache and os.environ.get("DLGM_EXPERT_WT", "1") != "0"
         if cfg.transposed_weight_cache:
+            # 2-D weights always; expert-stacked [E, out, in] weights within tcache_hbm_fraction of the device
+            budget = (cfg.tcache_hbm_fraction * torch.cuda.get_device_properties(device).total_memory
+                      if device.type == "cuda" else math.inf)
+            used = 0
             for g in self.groups:
                 if self.stage < 3 or g.P == 1:
                     names = [(sp.name, tuple(sp.shape)) for sp in g.specs if sp.tcache and len(sp.shape) == 2]
+                    stacked = [(sp.name, tuple(sp.shape)) for sp in g.specs
+                               if sp.tcache and len(sp.shape) == 3 and self._expert_wt]
+                    nbytes = sum(math.prod(shp) for _, shp in stacked) * 2
+                    if stacked and used + nbytes <= budget:
+                        names += stacked
+                        used += nbytes
                     if names:
                         self._tnames[g.idx] = names
         self.step_count = 0
@@ -620,15 +635,20 @@ class ZeroEngine:
         return out
 
     def _transposed(self, gi: int, views: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
-        """name + ".T" -> cached [in, out] copy of the stationary compute weight (rebuilt per step)."""
+        """name + ".T" -> cached [in, out] copy of the stationary compute weight (rebuilt per step); expert-stacked
+        [E, out, in] weights get [E, in, out] (one transpose per expert)."""
         ver, cache = self._tcache.get(gi, (-1, None))
         if cache is None:
-            cache = {n: torch.empty((shp[1], shp[0]), dtype=self.dtype, device=self.device)
+            cache = {n: torch.empty(shp[:-2] + (shp[-1], shp[-2]), dtype=self.dtype, device=self.device)
                      for n, shp in self._tnames[gi]}
         if ver != self._pver:
             from ..ops.gemm import transpose
-            for n, _ in self._tnames[gi]:
-                transpose(views[n], out=cache[n])
+            for n, shp in self._tnames[gi]:
+                if len(shp) == 3:
+                    for e in range(shp[0]):
+                        transpose(views[n][e], out=cache[n][e])
+                else:
+                    transpose(views[n], out=cache[n])
             self._tcache[gi] = (self._pver, cache)
         return {n + ".T": t for n, t in cache.items()}
 
@@ -1037,12 +1057,15 @@ class ZeroEngine:
     def graph_capturable(self) -> bool:
         """Is the micro-batch loop free of collectives and host synchronisation (so it can be captured)?
 
-        Single rank (every group P == 1: gradients land directly in the fp32 shard, no gather), dense
-        model (MoE dispatch sizes are read on the host), no optimizer / activation offload (host
-        copies), no per-phase timers (host-side event bookkeeping). The fp16 loss scale is a device word
+        Single rank (every group P == 1: gradients land directly in the fp32 shard, no gather), a dense
+        model or an MoE model on the grouped expert path at EP = 1 (the routing offsets stay on the device;
+        the per-expert loop reads them on the host), no optimizer / activation offload (host copies), no
+        per-phase timers (host-side event bookkeeping). The fp16 loss scale is a device word
         (LossScaler.state), so the fp16 path replays the same graph at every scale."""
         c = self.cfg
-        return (c.hip_graphs and self.is_cuda and self.W == 1 and not self.has_experts and self.offload is None
+        from ..ops import gemm_mfma as gm
+        moe_ok = not self.has_experts or (self.ep_size == 1 and gm.GROUPED)
+        return (c.hip_graphs and self.is_cuda and self.W == 1 and moe_ok and self.offload is None
                 and not self.param_host
                 and not c.cpu_checkpointing and not self.timers.enabled
                 and self.sp_size == 1 and self._graph_state != "failed")
