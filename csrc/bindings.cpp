@@ -20,8 +20,8 @@ void dlgm_rope_(at::Tensor qkv, const at::Tensor& cos_t, const at::Tensor& sin_t
                 const c10::optional<at::Tensor>& pos_ids, int64_t n_rope_heads, int64_t head_dim, int64_t seq_len,
                 bool inverse);
 // swiglu.hip
-at::Tensor dlgm_swiglu_fwd(const at::Tensor& gu);
-at::Tensor dlgm_swiglu_bwd(const at::Tensor& dy, const at::Tensor& gu);
+at::Tensor dlgm_swiglu_fwd(const at::Tensor& gu, const c10::optional<at::Tensor>& nrows);
+at::Tensor dlgm_swiglu_bwd(const at::Tensor& dy, const at::Tensor& gu, const c10::optional<at::Tensor>& nrows);
 // cross_entropy.hip
 std::tuple<at::Tensor, at::Tensor> dlgm_cross_entropy_(at::Tensor logits, const at::Tensor& labels,
                                                        int64_t ignore_index, double grad_scale, bool compute_grad,
@@ -50,6 +50,10 @@ at::Tensor dlgm_moe_combine_fwd(const at::Tensor& y, const at::Tensor& pos, cons
 std::tuple<at::Tensor, at::Tensor> dlgm_moe_combine_bwd(const at::Tensor& dout, const at::Tensor& y,
                                                         const at::Tensor& pos, const at::Tensor& gates);
 std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_moe_permute(const at::Tensor& topi, int64_t n_experts);
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dlgm_moe_capacity_plan(const at::Tensor& offsets,
+                                                                                   int64_t rows, int64_t capacity);
+at::Tensor dlgm_gather_rows(const at::Tensor& src, const at::Tensor& idx, const c10::optional<at::Tensor>& idx2,
+                            const c10::optional<at::Tensor>& nrows);
 // transpose.hip
 at::Tensor dlgm_transpose(const at::Tensor& x, const c10::optional<at::Tensor>& out);
 // embedding.hip
@@ -72,8 +76,8 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("rmsnorm_fwd(Tensor x, Tensor? residual, Tensor w, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("rmsnorm_bwd(Tensor dy, Tensor h, Tensor w, Tensor rstd, Tensor? dres, Tensor(a!) dw, bool accumulate_dw) -> Tensor");
   m.def("rope_(Tensor(a!) qkv, Tensor cos, Tensor sin, Tensor? pos_ids, int n_rope_heads, int head_dim, int seq_len, bool inverse) -> ()");
-  m.def("swiglu_fwd(Tensor gu) -> Tensor");
-  m.def("swiglu_bwd(Tensor dy, Tensor gu) -> Tensor");
+  m.def("swiglu_fwd(Tensor gu, Tensor? nrows=None) -> Tensor");
+  m.def("swiglu_bwd(Tensor dy, Tensor gu, Tensor? nrows=None) -> Tensor");
   m.def("cross_entropy_(Tensor(a!) logits, Tensor labels, int ignore_index, float grad_scale, bool compute_grad, Tensor? scale=None) -> (Tensor, Tensor)");
   m.def("grad_stats(Tensor[] grads, Tensor(a!) out, bool accumulate) -> ()");
   m.def("adamw_step_(Tensor(a!) p, Tensor(b!) m, Tensor(c!) v, Tensor g, Tensor(d!)? p16, Tensor? stats, float lr, float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2, float grad_scale, float max_norm, Tensor? scale_state=None) -> ()");
@@ -84,6 +88,8 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("moe_combine_fwd(Tensor y, Tensor pos, Tensor? gates) -> Tensor");
   m.def("moe_combine_bwd(Tensor dout, Tensor y, Tensor pos, Tensor gates) -> (Tensor, Tensor)");
   m.def("moe_permute(Tensor topi, int n_experts) -> (Tensor, Tensor, Tensor)");
+  m.def("moe_capacity_plan(Tensor offsets, int rows, int capacity) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("gather_rows(Tensor src, Tensor idx, Tensor? idx2=None, Tensor? nrows=None) -> Tensor");
   m.def("transpose(Tensor x, Tensor(a!)? out=None) -> Tensor");
   m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, float softmax_scale, bool causal, Tensor? dqkv=None) -> (Tensor, Tensor, Tensor)");
   m.def("embedding_fwd(Tensor table, Tensor ids) -> Tensor");
@@ -113,6 +119,8 @@ TORCH_LIBRARY_IMPL(dlgm, CUDA, m) {
   m.impl("moe_combine_fwd", &dlgm_moe_combine_fwd);
   m.impl("moe_combine_bwd", &dlgm_moe_combine_bwd);
   m.impl("moe_permute", &dlgm_moe_permute);
+  m.impl("moe_capacity_plan", &dlgm_moe_capacity_plan);
+  m.impl("gather_rows", &dlgm_gather_rows);
   m.impl("transpose", &dlgm_transpose);
   m.impl("embedding_fwd", &dlgm_embedding_fwd);
   m.impl("embedding_bwd_", &dlgm_embedding_bwd_);

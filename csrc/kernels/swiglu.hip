@@ -15,9 +15,10 @@ namespace {
 
 template <typename T>
 __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const T* __restrict__ gu, T* __restrict__ y,
-                                                         int64_t T_, int64_t F, int64_t gu_stride) {
+                                                         int64_t T_, int64_t F, int64_t gu_stride,
+                                                         const int* __restrict__ nrows) {
   const int64_t fch = F >> 3;
-  const int64_t total = T_ * fch;
+  const int64_t total = (nrows != nullptr ? min(T_, (int64_t)nrows[0]) : T_) * fch;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t t = i / fch, c = (i - t * fch) * 8;
@@ -33,9 +34,9 @@ __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const T* __restrict__ g
 template <typename T>
 __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ gu,
                                                          T* __restrict__ dgu, int64_t T_, int64_t F,
-                                                         int64_t gu_stride) {
+                                                         int64_t gu_stride, const int* __restrict__ nrows) {
   const int64_t fch = F >> 3;
-  const int64_t total = T_ * fch;
+  const int64_t total = (nrows != nullptr ? min(T_, (int64_t)nrows[0]) : T_) * fch;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t t = i / fch, c = (i - t * fch) * 8;
@@ -62,7 +63,15 @@ int64_t grid_for(int64_t work) {
 
 }  // namespace
 
-at::Tensor dlgm_swiglu_fwd(const at::Tensor& gu) {
+static const int* rows_ptr(const c10::optional<at::Tensor>& nrows) {
+  if (!nrows.has_value() || !nrows->defined()) return nullptr;
+  TORCH_CHECK(nrows->is_cuda() && nrows->scalar_type() == at::kInt && nrows->numel() == 1, "swiglu: nrows int32 [1]");
+  return nrows->data_ptr<int>();
+}
+
+// nrows (optional, int32 [1] on the device): only rows [0, nrows) are computed; the rest of the output is left
+// uninitialised (the MoE capacity layout's unused overflow rows, whose count is known only on the device)
+at::Tensor dlgm_swiglu_fwd(const at::Tensor& gu, const c10::optional<at::Tensor>& nrows) {
   TORCH_CHECK(gu.is_cuda() && DLGM_IS16(gu) && gu.dim() == 2 && gu.stride(1) == 1,
               "swiglu: gu must be a [T, 2F] bf16/fp16 GPU tensor");
   const int64_t T = gu.size(0), F = gu.size(1) / 2;
@@ -71,12 +80,12 @@ at::Tensor dlgm_swiglu_fwd(const at::Tensor& gu) {
   if (T == 0) return y;
   auto stream = c10::hip::getCurrentHIPStream();
   DLGM_DISPATCH_16(gu.scalar_type(), E, swiglu_fwd_kernel<E><<<grid_for(T * F / 8), 256, 0, stream>>>(
-      reinterpret_cast<const E*>(gu.data_ptr()), reinterpret_cast<E*>(y.data_ptr()), T, F, gu.stride(0)));
+      reinterpret_cast<const E*>(gu.data_ptr()), reinterpret_cast<E*>(y.data_ptr()), T, F, gu.stride(0), rows_ptr(nrows)));
   DLGM_CHECK_HIP(hipGetLastError());
   return y;
 }
 
-at::Tensor dlgm_swiglu_bwd(const at::Tensor& dy, const at::Tensor& gu) {
+at::Tensor dlgm_swiglu_bwd(const at::Tensor& dy, const at::Tensor& gu, const c10::optional<at::Tensor>& nrows) {
   TORCH_CHECK(gu.is_cuda() && DLGM_IS16(gu) && gu.dim() == 2 && gu.stride(1) == 1,
               "swiglu_bwd: gu must be a [T, 2F] bf16/fp16 GPU tensor");
   const int64_t T = gu.size(0), F = gu.size(1) / 2;
@@ -87,7 +96,7 @@ at::Tensor dlgm_swiglu_bwd(const at::Tensor& dy, const at::Tensor& gu) {
   auto stream = c10::hip::getCurrentHIPStream();
   DLGM_DISPATCH_16(gu.scalar_type(), E, swiglu_bwd_kernel<E><<<grid_for(T * F / 8), 256, 0, stream>>>(
       reinterpret_cast<const E*>(dy.data_ptr()), reinterpret_cast<const E*>(gu.data_ptr()),
-      reinterpret_cast<E*>(dgu.data_ptr()), T, F, gu.stride(0)));
+      reinterpret_cast<E*>(dgu.data_ptr()), T, F, gu.stride(0), rows_ptr(nrows)));
   DLGM_CHECK_HIP(hipGetLastError());
   return dgu;
 }

@@ -29,7 +29,7 @@ import torch
 from .. import ops
 from ..ops.gemm import grad_mm
 from ..ops import gemm_mfma as gm
-from ..ops.moe import moe_combine, moe_combine_bwd, moe_permute
+from ..ops.moe import capacity_plan, capacity_rows, gather_rows, moe_combine, moe_combine_bwd, moe_permute
 from ..parallel.ep import ExpertDispatcher
 from .common import ParamSpec, Params, StepContext, Unit
 from .config import ModelConfig
@@ -52,12 +52,13 @@ class MixtralBlock(LlamaBlock):
         c = self.cfg
         out_std = c.init_std / (2 * c.n_layers) ** 0.5
         off = self.ep_rank * self.E_local
-        # tcache: the engine keeps [E, in, out] transposes (budgeted), so the expert dX GEMMs read K-contiguous
-        # weights (the layout both the grouped MFMA kernel and hipBLASLt run fastest)
+        # tcache: the engine keeps [E, in, out] transposes (budgeted), so the grouped MFMA dX GEMMs read
+        # K-contiguous weights; the capacity layout's batched hipBLASLt GEMMs take either layout at speed
+        tc = not gm.CAPACITY
         return [ParamSpec("w_gate_up", (self.E_local, 2 * c.ffn_dim, c.d_model), std=c.init_std,
-                          experts=self.E_local, expert_offset=off, tcache=True),
+                          experts=self.E_local, expert_offset=off, tcache=tc),
                 ParamSpec("w_down", (self.E_local, c.d_model, c.ffn_dim), std=out_std,
-                          experts=self.E_local, expert_offset=off, tcache=True)]
+                          experts=self.E_local, expert_offset=off, tcache=tc)]
 
     def dispatcher(self, ctx: StepContext) -> ExpertDispatcher:
         if self._dispatcher is None:
@@ -65,12 +66,20 @@ class MixtralBlock(LlamaBlock):
         return self._dispatcher
 
     # ---------------------------------------------------------------- MoE FFN
+    def _cap_mode(self, x: torch.Tensor) -> bool:
+        """Expert GEMMs over the capacity layout (static-shape batched hipBLASLt + grouped overflow)?"""
+        c = self.cfg
+        return gm.CAPACITY and (not x.is_cuda or gm.grouped_supported(x, capacity=True)) and \
+            (2 * c.ffn_dim) % 256 == 0 and c.d_model % 256 == 0 and c.ffn_dim % 256 == 0
+
     def moe_forward(self, p: Params, hn2: torch.Tensor, ctx: StepContext):
         c = self.cfg
         T, E, K = hn2.shape[0], c.n_experts, c.top_k
         probs, topi, gates = ops.router_topk(torch.mm(hn2, p["router"].t()), K)  # [K9]
         offsets, pos, tok = moe_permute(topi, E)  # expert sort on the device, no host read
         counts = (offsets[1:] - offsets[:-1]).long()
+        if self._cap_mode(hn2):
+            return self._moe_forward_cap(p, hn2, ctx, probs, topi, gates, offsets, pos, tok, counts)
         x_sorted = hn2.index_select(0, tok)
         disp = self.dispatcher(ctx)
         x_local, dctx = disp.dispatch(x_sorted, counts, offsets)
@@ -80,6 +89,83 @@ class MixtralBlock(LlamaBlock):
         f = counts.float() / float(T * K) * K  # fraction of tokens choosing each expert (summed over k)
         ctx.aux.setdefault("moe_aux", []).append(float(E) * (f * probs.mean(0)).sum())
         return out, (probs, topi, gates, pos, f, x_local, dctx, exp_saved, y_sorted)
+
+    def _moe_forward_cap(self, p: Params, hn2, ctx, probs, topi, gates, offsets, pos, tok, counts):
+        """Capacity-layout MoE forward (ops.moe.CapacityPlan): at EP = 1 the expert rows are gathered straight
+        from the tokens into the expanded layout and the combine reads the expert outputs through the slot ->
+        expanded-row map; at EP > 1 the all-to-all carries expert-sorted rows and the layout is entered /
+        left on the expert rank."""
+        c = self.cfg
+        T, E, K = hn2.shape[0], c.n_experts, c.top_k
+        disp = self.dispatcher(ctx)
+        if disp.W == 1:
+            plan = capacity_plan(offsets, T * K, capacity_rows(T * K, E, gm.CAPACITY_FACTOR, gm.CAPACITY_ALIGN))
+            x_exp = gather_rows(hn2, plan.exp_src, tok, plan.nrows)
+            dctx = None
+        else:
+            x_local, dctx = disp.dispatch(hn2.index_select(0, tok), counts, offsets)
+            R = x_local.shape[0]
+            C = capacity_rows(T * K * disp.W, E, gm.CAPACITY_FACTOR, gm.CAPACITY_ALIGN)  # balanced share x factor
+            plan = capacity_plan(dctx.local_offsets, R, C)
+            x_exp = gather_rows(x_local, plan.exp_src, None, plan.nrows)
+        y_exp, exp_saved = self._experts_fwd_cap(p, x_exp, plan)
+        if dctx is None:
+            y_src, pos_y = y_exp, plan.row_map.index_select(0, pos.reshape(-1)).view_as(pos)
+        else:
+            y_src, pos_y = disp.combine(y_exp.index_select(0, plan.row_map), dctx), pos
+        out = moe_combine(y_src, pos_y, gates)
+        f = counts.float() / float(T * K) * K
+        ctx.aux.setdefault("moe_aux", []).append(float(E) * (f * probs.mean(0)).sum())
+        return out, ("cap", probs, topi, gates, pos, f, dctx, x_exp, plan, exp_saved, y_src, pos_y)
+
+    def _experts_fwd_cap(self, p: Params, x: torch.Tensor, plan):
+        gu = gm.capacity_mm(x, p["w_gate_up"], plan)
+        a = ops.swiglu_fwd(gu, plan.nrows)
+        y = gm.capacity_mm(a, p["w_down"], plan)
+        return y, (gu, a)
+
+    def _experts_bwd_cap(self, p: Params, g: Params, x: torch.Tensor, dy: torch.Tensor, saved, plan, ctx):
+        gu, a = saved
+        da = gm.capacity_mm(dy, p["w_down"], plan, transpose_w=False)
+        dgu = ops.swiglu_bwd(da, gu, plan.nrows)
+        del da
+        dx = gm.capacity_mm(dgu, p["w_gate_up"], plan, transpose_w=False)
+        if ctx.defer_wgrad:
+            # dW once per step: each expert's capacity rows of every micro-batch in ONE batched GEMM (K = GA x C)
+            if ctx.micro_index == 0:
+                self._wstash, self._wflushed, self._wbytes = [], False, 0
+            self._wstash.append((dy, a, dgu, x, plan))
+            self._wbytes += sum(t.numel() * t.element_size() for t in (dy, a, dgu, x))
+            if ctx.last_micro or self._wbytes > getattr(ctx, "defer_budget_bytes", 48 << 30):
+                self._flush_wgrad_cap(g)
+            return dx
+        gm.capacity_wgrad(g["w_down"], [dy], [a], [plan], ctx.grad_acc)
+        gm.capacity_wgrad(g["w_gate_up"], [dgu], [x], [plan], ctx.grad_acc)
+        return dx
+
+    def _flush_wgrad_cap(self, g: Params) -> None:
+        stash, acc = self._wstash, self._wflushed
+        self._wstash, self._wflushed, self._wbytes = [], True, 0
+        plans = [s[4] for s in stash]
+        gm.capacity_wgrad(g["w_down"], [s[0] for s in stash], [s[1] for s in stash], plans, acc)
+        gm.capacity_wgrad(g["w_gate_up"], [s[2] for s in stash], [s[3] for s in stash], plans, acc)
+
+    def _moe_backward_cap(self, p: Params, g: Params, hn2: torch.Tensor, saved, dout: torch.Tensor, ctx):
+        _, probs, topi, gates, pos, f, dctx, x_exp, plan, exp_saved, y_src, pos_y = saved
+        disp = self.dispatcher(ctx)
+        dy_src, dgates = moe_combine_bwd(dout.contiguous(), y_src, pos_y, gates)
+        if dctx is None:
+            dy_exp = dy_src  # rows no slot references (capacity padding, unused overflow) are zero
+        else:
+            dy_local = disp.redispatch(dy_src, dctx)
+            dy_exp = dy_local.new_zeros((plan.rows, dy_local.shape[1]))
+            dy_exp.index_copy_(0, plan.row_map, dy_local)
+        dx_exp = self._experts_bwd_cap(p, g, x_exp, dy_exp, exp_saved, plan, ctx)
+        if dctx is None:
+            dhn2 = moe_combine(dx_exp, pos_y, None)  # adjoint of the dispatch gather: sum the K slots per token
+        else:
+            dhn2 = moe_combine(disp.combine(dx_exp.index_select(0, plan.row_map), dctx), pos, None)
+        return self._router_backward(p, g, hn2, probs, topi, gates, f, dgates, dhn2, dout, ctx)
 
     def _grouped(self, x: torch.Tensor, wgrad: bool = False) -> bool:
         """Expert GEMMs as single grouped MFMA launches (csrc/kernels/gemm_mfma.hip) with the device
@@ -254,15 +340,20 @@ class MixtralBlock(LlamaBlock):
                                       acc or i > 0)
 
     def moe_backward(self, p: Params, g: Params, hn2: torch.Tensor, saved, dout: torch.Tensor, ctx: StepContext):
-        c = self.cfg
+        if saved[0] == "cap":
+            return self._moe_backward_cap(p, g, hn2, saved, dout, ctx)
         probs, topi, gates, pos, f, x_local, dctx, exp_saved, y_sorted = saved
-        T, E = probs.shape
         disp = self.dispatcher(ctx)
         dy_sorted, dgates = moe_combine_bwd(dout.contiguous(), y_sorted, pos, gates)
         dy_local = disp.redispatch(dy_sorted, dctx)
         dx_local = self._experts_bwd(p, g, x_local, dy_local, exp_saved, ctx.grad_acc, ctx)
         dx_sorted = disp.combine(dx_local, dctx)
         dhn2 = moe_combine(dx_sorted, pos, None)  # adjoint of the dispatch gather: sum the K slots per token
+        return self._router_backward(p, g, hn2, probs, topi, gates, f, dgates, dhn2, dout, ctx)
+
+    def _router_backward(self, p: Params, g: Params, hn2, probs, topi, gates, f, dgates, dhn2, dout, ctx):
+        c = self.cfg
+        T, E = probs.shape
         dtop = gates * (dgates - (gates * dgates).sum(-1, keepdim=True))
         dlogits = torch.zeros(T, E, dtype=torch.float32, device=dout.device).scatter_(1, topi, dtop)
         if c.router_aux_coef > 0:

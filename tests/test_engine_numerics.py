@@ -78,6 +78,7 @@ def test_mixtral_expert_gemm_modes_match_autograd_gpu(monkeypatch, grouped, wgra
     the deferred grouped dW over both micro-batches), the grouped weight gradients only, and the per-expert
     hipBLASLt loop."""
     from distributed_llm_training_gpu_manager_amd.ops import gemm_mfma as gm
+    monkeypatch.setattr(gm, "CAPACITY", False)
     monkeypatch.setattr(gm, "GROUPED", grouped)
     monkeypatch.setattr(gm, "GROUPED_WGRAD", wgrad)
     _check("cuda", "mixtral-tiny", tol=1e-1)
@@ -314,6 +315,8 @@ def test_mixtral_grouped_deferred_wgrad_matches_per_micro_batch_cpu(monkeypatch)
     per-micro-batch grouped dW. CPU run of the same code (grouped ops' reference path)."""
     from distributed_llm_training_gpu_manager_amd.models.mixtral import MixtralBlock
     from distributed_llm_training_gpu_manager_amd.parallel.zero import EngineConfig, ZeroEngine
+    from distributed_llm_training_gpu_manager_amd.ops import gemm_mfma as gm
+    monkeypatch.setattr(gm, "CAPACITY", False)
     monkeypatch.setattr(MixtralBlock, "_grouped", lambda self, x, wgrad=False: True)
     mc = get_config("mixtral-tiny")
     g = torch.Generator().manual_seed(4)

@@ -206,12 +206,15 @@ def _defer_worker(rank, world, port, model, dw, out):
     """EP = W with GA 3; counts the expert-dW flushes so the deferred path is known to have run."""
     from distributed_llm_training_gpu_manager_amd.models import mixtral
     flushes = [0]
-    orig = mixtral.MixtralBlock._flush_wgrad
 
-    def spy(self, g):
-        flushes[0] += 1
-        return orig(self, g)
-    mixtral.MixtralBlock._flush_wgrad = spy
+    def counted(orig):
+        def spy(self, g):
+            flushes[0] += 1
+            return orig(self, g)
+        return spy
+    # the per-expert path's flush, or the capacity layout's (DLGM_MOE_GROUPED=cap)
+    mixtral.MixtralBlock._flush_wgrad = counted(mixtral.MixtralBlock._flush_wgrad)
+    mixtral.MixtralBlock._flush_wgrad_cap = counted(mixtral.MixtralBlock._flush_wgrad_cap)
     _init(rank, world, port)
     eng = ZeroEngine(_model(model), _cfg(3, 3, expert_parallel_size=world, defer_expert_wgrad=dw),
                      torch.device("cpu"), Comm())
