@@ -52,10 +52,12 @@ std::tuple<at::Tensor, at::Tensor> dlgm_moe_combine_bwd(const at::Tensor& dout, 
 std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_moe_permute(const at::Tensor& topi, int64_t n_experts);
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dlgm_moe_capacity_plan(const at::Tensor& offsets,
                                                                                    int64_t rows, int64_t capacity);
+std::tuple<at::Tensor, at::Tensor> dlgm_moe_pad_plan(const at::Tensor& offsets, int64_t padded_rows, int64_t align);
 at::Tensor dlgm_gather_rows(const at::Tensor& src, const at::Tensor& idx, const c10::optional<at::Tensor>& idx2,
                             const c10::optional<at::Tensor>& nrows);
 // transpose.hip
-at::Tensor dlgm_transpose(const at::Tensor& x, const c10::optional<at::Tensor>& out);
+at::Tensor dlgm_transpose(const at::Tensor& x, const c10::optional<at::Tensor>& out,
+                          const c10::optional<at::Tensor>& rows);
 // embedding.hip
 at::Tensor dlgm_embedding_fwd(const at::Tensor& table, const at::Tensor& ids);
 void dlgm_embedding_bwd_(at::Tensor grad, const at::Tensor& dy, const at::Tensor& sorted_ids, const at::Tensor& order);
@@ -70,7 +72,7 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
                     const c10::optional<at::Tensor>& offsets, int64_t mode, int64_t M, int64_t N, int64_t K,
                     int64_t G, int64_t b_gstride);
 void dlgm_gemm_mfma_seg(at::Tensor out, const std::vector<at::Tensor>& a, const std::vector<at::Tensor>& b,
-                        const at::Tensor& offsets, bool accumulate);
+                        const at::Tensor& offsets, bool accumulate, bool kmajor);
 
 TORCH_LIBRARY(dlgm, m) {
   m.def("rmsnorm_fwd(Tensor x, Tensor? residual, Tensor w, float eps) -> (Tensor, Tensor, Tensor)");
@@ -89,8 +91,9 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("moe_combine_bwd(Tensor dout, Tensor y, Tensor pos, Tensor gates) -> (Tensor, Tensor)");
   m.def("moe_permute(Tensor topi, int n_experts) -> (Tensor, Tensor, Tensor)");
   m.def("moe_capacity_plan(Tensor offsets, int rows, int capacity) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("moe_pad_plan(Tensor offsets, int padded_rows, int align) -> (Tensor, Tensor)");
   m.def("gather_rows(Tensor src, Tensor idx, Tensor? idx2=None, Tensor? nrows=None) -> Tensor");
-  m.def("transpose(Tensor x, Tensor(a!)? out=None) -> Tensor");
+  m.def("transpose(Tensor x, Tensor(a!)? out=None, Tensor? rows=None) -> Tensor");
   m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, float softmax_scale, bool causal, Tensor? dqkv=None) -> (Tensor, Tensor, Tensor)");
   m.def("embedding_fwd(Tensor table, Tensor ids) -> Tensor");
   m.def("embedding_bwd_(Tensor(a!) grad, Tensor dy, Tensor sorted_ids, Tensor order) -> ()");
@@ -99,7 +102,7 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("gemm_lt_tune(Tensor out, Tensor a, Tensor b, float beta, int n_heuristic, bool all_algos, int reps) -> Tensor");
   m.def("gemm_lt_version() -> int", &dlgm_gemm_lt_version);
   m.def("gemm_mfma(Tensor(a!) out, Tensor a, Tensor b, bool accumulate, Tensor? offsets, int mode, int M, int N, int K, int G, int b_gstride) -> ()");
-  m.def("gemm_mfma_seg(Tensor(a!) out, Tensor[] a, Tensor[] b, Tensor offsets, bool accumulate) -> ()");
+  m.def("gemm_mfma_seg(Tensor(a!) out, Tensor[] a, Tensor[] b, Tensor offsets, bool accumulate, bool kmajor=False) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dlgm, CUDA, m) {
@@ -121,6 +124,7 @@ TORCH_LIBRARY_IMPL(dlgm, CUDA, m) {
   m.impl("moe_permute", &dlgm_moe_permute);
   m.impl("moe_capacity_plan", &dlgm_moe_capacity_plan);
   m.impl("gather_rows", &dlgm_gather_rows);
+  m.impl("moe_pad_plan", &dlgm_moe_pad_plan);
   m.impl("transpose", &dlgm_transpose);
   m.impl("embedding_fwd", &dlgm_embedding_fwd);
   m.impl("embedding_bwd_", &dlgm_embedding_bwd_);

@@ -292,6 +292,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4)(0.f);
 
   const int nk = MODE == kGroupKSeg ? seg_cum[kMaxSeg] : (k_hi - k_lo + BK - 1) / BK;
+  // an empty reduction that accumulates leaves C as it is: skip the read-modify-write of the tile (the MoE
+  // capacity layout's overflow dW launches cover every expert and usually find no rows at all)
+  if (EPI == kAccF32 && nk <= 0) return;
   // partial tiles: K (grouped-K group ends), M rows (K-contiguous A: grouped-M group ends / M % 256 != 0)
   constexpr bool PK = MODE == kGroupK || MODE == kGroupKSeg, PM = AK;
   if (nk > 0) {
@@ -540,8 +543,13 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
 // a[s] [R_s, M] and b[s] [R_s, N] token-major (row-major) bf16 and offsets [nseg, G + 1] int32 on the device
 // (offsets[s] splits segment s's rows by group). One launch reduces each group over all its rows of every
 // segment -- e.g. an expert's weight gradient over the step's micro-batches -- without concatenating them.
+//
+// kmajor: the operands are given transposed, a[s] [M, P] and b[s] [N, P] row-major (the reduction dim contiguous,
+// one P for all segments), with every group's range [offsets[s][g], offsets[s][g + 1]) a whole number of 64-wide
+// K tiles (zero padded: ops.moe.pad_plan + the row-remapped transpose). Both images are then K-contiguous --
+// the layout the kernel runs fastest (ds_read_b128 fragments, no transposed LDS reads).
 void dlgm_gemm_mfma_seg(at::Tensor out, const std::vector<at::Tensor>& a, const std::vector<at::Tensor>& b,
-                        const at::Tensor& offsets, bool accumulate) {
+                        const at::Tensor& offsets, bool accumulate, bool kmajor) {
   const int nseg = (int)a.size();
   TORCH_CHECK(nseg >= 1 && nseg <= kMaxSeg && (int)b.size() == nseg, "gemm_mfma_seg: 1..8 segments, a/b paired");
   TORCH_CHECK(out.is_cuda() && out.dim() == 3 && out.is_contiguous() && out.scalar_type() == at::kFloat,
@@ -557,9 +565,15 @@ void dlgm_gemm_mfma_seg(at::Tensor out, const std::vector<at::Tensor>& a, const 
     const at::Tensor& y = b[s];
     TORCH_CHECK(x.is_cuda() && y.is_cuda() && x.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16,
                 "gemm_mfma_seg: bf16 GPU operands");
-    TORCH_CHECK(x.dim() == 2 && y.dim() == 2 && x.size(1) == M && y.size(1) == N && x.size(0) == y.size(0) &&
-                    x.stride(1) == 1 && y.stride(1) == 1,
-                "gemm_mfma_seg: a[s] [R_s, M] and b[s] [R_s, N] row-major");
+    if (kmajor) {
+      TORCH_CHECK(x.dim() == 2 && y.dim() == 2 && x.size(0) == M && y.size(0) == N && x.size(1) == y.size(1) &&
+                      x.stride(1) == 1 && y.stride(1) == 1,
+                  "gemm_mfma_seg(kmajor): a[s] [M, P] and b[s] [N, P] row-major");
+    } else {
+      TORCH_CHECK(x.dim() == 2 && y.dim() == 2 && x.size(1) == M && y.size(1) == N && x.size(0) == y.size(0) &&
+                      x.stride(1) == 1 && y.stride(1) == 1,
+                  "gemm_mfma_seg: a[s] [R_s, M] and b[s] [R_s, N] row-major");
+    }
     TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0,
                 "gemm_mfma_seg: operands 16-byte aligned");
     if (s == 0) {
@@ -587,7 +601,11 @@ void dlgm_gemm_mfma_seg(at::Tensor out, const std::vector<at::Tensor>& a, const 
   p.tiles_m = (int)(M / BM);
   const int64_t nblk = G * (int64_t)p.tiles_m * p.tiles_n;
   if (nblk == 0) return;
-  launch_epi<kGroupKSeg, false, false>(accumulate ? kAccF32 : kStoreF32, dim3((unsigned)nblk),
+  if (kmajor)
+    launch_epi<kGroupKSeg, true, true>(accumulate ? kAccF32 : kStoreF32, dim3((unsigned)nblk),
                                        c10::hip::getCurrentHIPStream(), p);
+  else
+    launch_epi<kGroupKSeg, false, false>(accumulate ? kAccF32 : kStoreF32, dim3((unsigned)nblk),
+                                         c10::hip::getCurrentHIPStream(), p);
   DLGM_CHECK_HIP(hipGetLastError());
 }

@@ -172,6 +172,36 @@ __global__ __launch_bounds__(256) void moe_capacity_plan_kernel(const int* __res
   }
 }
 
+// Aligned re-layout of expert-sorted rows: expert e's rows start at padded row poff[e] (a multiple of `align`,
+// poff[e+1] - poff[e] = count rounded up to align). rows[p] = the sorted row at padded row p, or -1 (padding; also
+// every p past poff[G]). With it a transposed [D, P] image has every expert's reduction range on whole K tiles.
+__global__ __launch_bounds__(256) void moe_pad_plan_kernel(const int* __restrict__ offsets, int G, int64_t P,
+                                                           int align, int* __restrict__ rows, int* __restrict__ poff) {
+  __shared__ int s_off[kMaxCapGroups + 1], s_pad[kMaxCapGroups + 1];
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int e = 0; e < G; ++e) {
+      s_off[e] = offsets[e];
+      s_pad[e] = acc;
+      acc += (offsets[e + 1] - offsets[e] + align - 1) / align * align;
+    }
+    s_off[G] = offsets[G];
+    s_pad[G] = acc;
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && (int)threadIdx.x <= G) poff[threadIdx.x] = s_pad[threadIdx.x];
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < P; p += (int64_t)gridDim.x * blockDim.x) {
+    int src = -1;
+    if (p < s_pad[G]) {
+      int e = 0;
+      while (s_pad[e + 1] <= p) ++e;
+      const int r = (int)p - s_pad[e];
+      if (r < s_off[e + 1] - s_off[e]) src = s_off[e] + r;
+    }
+    rows[p] = src;
+  }
+}
+
 // out[r] = src[idx2 ? idx2[idx[r]] : idx[r]] for idx[r] >= 0, zeros for idx[r] < 0; rows at or past *nrows (when
 // given) are left untouched. One wave per row, 16 B per lane.
 template <typename E>
@@ -266,6 +296,21 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dlgm_moe_capacity_pla
       ovf.data_ptr<int>(), nrows.data_ptr<int>());
   DLGM_CHECK_HIP(hipGetLastError());
   return {exp_src, row_map, ovf, nrows};
+}
+
+std::tuple<at::Tensor, at::Tensor> dlgm_moe_pad_plan(const at::Tensor& offsets, int64_t padded_rows, int64_t align) {
+  TORCH_CHECK(offsets.is_cuda() && offsets.scalar_type() == at::kInt && offsets.is_contiguous() && offsets.dim() == 1,
+              "moe_pad_plan: offsets must be a contiguous int32 [G + 1] GPU tensor");
+  const int64_t G = offsets.numel() - 1;
+  TORCH_CHECK(G >= 1 && G <= kMaxCapGroups && align >= 1 && padded_rows >= 0 && padded_rows < (1ll << 31),
+              "moe_pad_plan: 1..64 groups, align >= 1");
+  auto rows = at::empty({padded_rows}, offsets.options());
+  auto poff = at::empty({G + 1}, offsets.options());
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((padded_rows + 255) / 256, 2048));
+  moe_pad_plan_kernel<<<(unsigned)blocks, 256, 0, c10::hip::getCurrentHIPStream()>>>(
+      offsets.data_ptr<int>(), (int)G, padded_rows, (int)align, rows.data_ptr<int>(), poff.data_ptr<int>());
+  DLGM_CHECK_HIP(hipGetLastError());
+  return {rows, poff};
 }
 
 at::Tensor dlgm_gather_rows(const at::Tensor& src, const at::Tensor& idx, const c10::optional<at::Tensor>& idx2,

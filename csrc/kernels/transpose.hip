@@ -14,8 +14,10 @@ using namespace dlgm;
 
 namespace {
 
+// rows (optional): output column r of y takes source row rows[r] of x, or zeros when rows[r] < 0 (R = len(rows))
 __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
-                                                             int64_t R, int64_t C, int64_t ldx, int64_t ldy) {
+                                                             int64_t R, int64_t C, int64_t ldx, int64_t ldy,
+                                                             const int* __restrict__ rows) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -26,7 +28,14 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restr
     if (r0 >= R || c0 >= C) continue;  // R, C are multiples of 8: a chunk is wholly in or out
     short8 v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const short8*>(x + (r0 + j) * ldx + c0);
+    for (int j = 0; j < 8; ++j) {
+      if (rows == nullptr) {
+        v[j] = *reinterpret_cast<const short8*>(x + (r0 + j) * ldx + c0);
+      } else {
+        const int src = rows[r0 + j];
+        v[j] = src >= 0 ? *reinterpret_cast<const short8*>(x + (int64_t)src * ldx + c0) : (short8)(0);
+      }
+    }
     short8 o[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -39,12 +48,19 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restr
 
 }  // namespace
 
-// out[C, R] (contiguous) = x[R, C]^T; x may be a row-strided view (stride(1) == 1).
-at::Tensor dlgm_transpose(const at::Tensor& x, const c10::optional<at::Tensor>& out_opt) {
+// out[C, R] (contiguous) = x[R, C]^T; x may be a row-strided view (stride(1) == 1). With `rows` (int32 [R'],
+// R' % 8 == 0) the transpose runs over a remapped row space: out[C, R'] with column r = x[rows[r]] (zeros for
+// rows[r] < 0) -- e.g. expert-sorted rows re-laid with every expert starting on an aligned column.
+at::Tensor dlgm_transpose(const at::Tensor& x, const c10::optional<at::Tensor>& out_opt,
+                          const c10::optional<at::Tensor>& rows_opt) {
   // 16-bit payload moved bit-exactly: serves bf16 and fp16
   TORCH_CHECK(x.is_cuda() && DLGM_IS16(x) && x.dim() == 2, "transpose: bf16/fp16 2-D GPU tensor");
   TORCH_CHECK(x.stride(1) == 1, "transpose: rows must be contiguous");
-  const int64_t R = x.size(0), C = x.size(1);
+  const bool remap = rows_opt.has_value() && rows_opt->defined();
+  if (remap)
+    TORCH_CHECK(rows_opt->is_cuda() && rows_opt->scalar_type() == at::kInt && rows_opt->is_contiguous() &&
+                    rows_opt->dim() == 1, "transpose: rows must be a contiguous int32 GPU vector");
+  const int64_t R = remap ? rows_opt->numel() : x.size(0), C = x.size(1);
   TORCH_CHECK(R % 8 == 0 && C % 8 == 0 && x.stride(0) % 8 == 0, "transpose: dims and row stride must be multiples of 8");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "transpose: input must be 16-byte aligned");
   at::Tensor y = out_opt.has_value() ? *out_opt : at::empty({C, R}, x.options());
@@ -54,7 +70,8 @@ at::Tensor dlgm_transpose(const at::Tensor& x, const c10::optional<at::Tensor>& 
   const int64_t tiles = ((R + 63) / 64) * ((C + 63) / 64);
   const int64_t grid = std::min<int64_t>((tiles + 3) / 4, 256 * 16);
   transpose_bf16_kernel<<<grid, 256, 0, c10::hip::getCurrentHIPStream()>>>(
-      reinterpret_cast<const bf16*>(x.data_ptr()), reinterpret_cast<bf16*>(y.data_ptr()), R, C, x.stride(0), R);
+      reinterpret_cast<const bf16*>(x.data_ptr()), reinterpret_cast<bf16*>(y.data_ptr()), R, C, x.stride(0), R,
+      remap ? rows_opt->data_ptr<int>() : nullptr);
   DLGM_CHECK_HIP(hipGetLastError());
   return y;
 }

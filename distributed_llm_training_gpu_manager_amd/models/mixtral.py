@@ -27,9 +27,10 @@ from typing import Any, List, Tuple
 import torch
 
 from .. import ops
-from ..ops.gemm import grad_mm
+from ..ops.gemm import grad_mm, transpose
 from ..ops import gemm_mfma as gm
-from ..ops.moe import capacity_plan, capacity_rows, gather_rows, moe_combine, moe_combine_bwd, moe_permute
+from ..ops.moe import (capacity_plan, capacity_rows, gather_rows, moe_combine, moe_combine_bwd, moe_permute,
+                       pad_plan)
 from ..parallel.ep import ExpertDispatcher
 from .common import ParamSpec, Params, StepContext, Unit
 from .config import ModelConfig
@@ -229,8 +230,16 @@ class MixtralBlock(LlamaBlock):
                 # dW once per step over the micro-batches' rows regrouped expert-major on the device
                 if ctx.micro_index == 0:
                     self._wstash, self._wflushed, self._wbytes = [], False, 0
-                self._wstash.append((dy, a_all, dgu_all, x, offs))
-                self._wbytes += sum(t.numel() * t.element_size() for t in (dy, a_all, dgu_all, x))
+                if gm.KMAJOR_DW and self.dispatcher(ctx).W == 1:
+                    # K-contiguous operands for the deferred dW: each stashed tensor transposed into an aligned
+                    # re-layout (every expert's rows start on a 64-column boundary, zero padded), so the segmented
+                    # kernel reads ds_read_b128 fragments on whole K tiles instead of transposed LDS reads
+                    src, poff = pad_plan(offs, x.shape[0])
+                    item = tuple(transpose(t, rows=src) for t in (dy, a_all, dgu_all, x)) + (poff, True)
+                else:
+                    item = (dy, a_all, dgu_all, x, offs, False)
+                self._wstash.append(item)
+                self._wbytes += sum(t.numel() * t.element_size() for t in item[:4])
                 if ctx.last_micro or self._wbytes > getattr(ctx, "defer_budget_bytes", 48 << 30):
                     self._flush_wgrad_grouped(g)
                 return dx
@@ -334,10 +343,13 @@ class MixtralBlock(LlamaBlock):
         self._wstash, self._wflushed, self._wbytes = [], True, 0
         for i in range(0, len(stash), gm.MAX_SEGMENTS):
             part = stash[i:i + gm.MAX_SEGMENTS]
-            offs = torch.stack([o for *_, o in part])  # [segments, experts + 1] int32, on the device
-            gm.grouped_wgrad_segments(g["w_down"], [t[0] for t in part], [t[1] for t in part], offs, acc or i > 0)
+            km = part[0][5]
+            assert all(t[5] == km for t in part)
+            offs = torch.stack([t[4] for t in part])  # [segments, experts + 1] int32, on the device
+            gm.grouped_wgrad_segments(g["w_down"], [t[0] for t in part], [t[1] for t in part], offs, acc or i > 0,
+                                      kmajor=km)
             gm.grouped_wgrad_segments(g["w_gate_up"], [t[2] for t in part], [t[3] for t in part], offs,
-                                      acc or i > 0)
+                                      acc or i > 0, kmajor=km)
 
     def moe_backward(self, p: Params, g: Params, hn2: torch.Tensor, saved, dout: torch.Tensor, ctx: StepContext):
         if saved[0] == "cap":

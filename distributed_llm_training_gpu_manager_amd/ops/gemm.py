@@ -159,8 +159,16 @@ def grad_copy(out: torch.Tensor, src: torch.Tensor, acc: bool) -> None:
         out.copy_(src)
 
 
-def transpose(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Contiguous x^T for a 2-D bf16 tensor (register-blocked HIP kernel on the GPU)."""
+def transpose(x: torch.Tensor, out: Optional[torch.Tensor] = None, rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Contiguous x^T for a 2-D bf16 tensor (register-blocked HIP kernel on the GPU). rows (int32 [R'], optional):
+    transpose a re-laid row space instead -- column r of the result is x[rows[r]], zeros where rows[r] < 0."""
+    if rows is not None:
+        if use_native(x):
+            return hip_ops().transpose(x, out, rows)
+        s = rows.long()
+        xr = x.index_select(0, s.clamp(min=0)) * (s >= 0).unsqueeze(1).to(x.dtype)
+        y = xr.t().contiguous()
+        return out.copy_(y) if out is not None else y
     if use_native(x) and x.dtype in (torch.bfloat16, torch.float16) and x.shape[0] % 8 == 0 and x.shape[1] % 8 == 0 \
             and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0:
         return hip_ops().transpose(x, out)

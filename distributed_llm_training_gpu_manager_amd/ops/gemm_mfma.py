@@ -43,6 +43,9 @@ DENSE, GROUP_M, GROUP_K = 0, 1, 2
 _MODE = os.environ.get("DLGM_MOE_GROUPED", "1")
 CAPACITY = _MODE == "cap"
 CAPACITY_FACTOR = float(os.environ.get("DLGM_MOE_CAPACITY_FACTOR", "1.125"))
+# deferred grouped dW over K-contiguous operands (each stashed micro-batch transposed into an aligned re-layout);
+# EP = 1 (one static row count); DLGM_MOE_KMAJOR_DW=0 keeps the token-major (transposed-LDS-read) kernel
+KMAJOR_DW = os.environ.get("DLGM_MOE_KMAJOR_DW", "1") != "0"
 CAPACITY_ALIGN = 64  # capacity rows per expert are a multiple of this
 # the capacity region as ONE torch.bmm per weight (opt-in): on MI355X / this torch build the bf16 batched GEMM at the
 # Mixtral-8x7B shape ([8, 1024, 4096] x [8, 4096, 28672]) faulted with an illegal address inside the library
@@ -205,21 +208,26 @@ MAX_SEGMENTS = 8
 
 
 def grouped_wgrad_segments(out: torch.Tensor, a: list, b: list, offsets: torch.Tensor,
-                           acc: bool = False) -> torch.Tensor:
+                           acc: bool = False, kmajor: bool = False) -> torch.Tensor:
     """out[e] (+)= sum_s a[s][rows of e in s]^T @ b[s][rows of e in s]: a[s] [R_s, M], b[s] [R_s, N] row-major,
     offsets [S, G + 1] int32 (row s splits segment s by group), out [G, M, N] fp32. One launch reduces every
-    group over its rows of all the segments (the step's micro-batches) without concatenating them."""
+    group over its rows of all the segments (the step's micro-batches) without concatenating them.
+    kmajor: the operands come transposed, a[s] [M, P], b[s] [N, P] (one P), every group range a multiple of 64
+    columns with zero padding (ops.moe.pad_plan + the row-remapped transpose): the K-contiguous kernel."""
     G, M, N = out.shape
     if use_native(out):
         assert len(a) <= MAX_SEGMENTS
-        hip_ops().gemm_mfma_seg(out, list(a), list(b), offsets, acc)
+        hip_ops().gemm_mfma_seg(out, list(a), list(b), offsets, acc, kmajor)
         return out
     offs = offsets.tolist()
     for e in range(G):
         r = None
         for s, (x, y) in enumerate(zip(a, b)):
             lo, hi = offs[s][e], offs[s][e + 1]
-            part = x[lo:hi].float().t() @ y[lo:hi].float()
+            if kmajor:
+                part = x[:, lo:hi].float() @ y[:, lo:hi].float().t()
+            else:
+                part = x[lo:hi].float().t() @ y[lo:hi].float()
             r = part if r is None else r + part
         if r is None:
             r = torch.zeros(M, N)

@@ -96,6 +96,31 @@ def capacity_plan(offsets: torch.Tensor, rows: int, capacity: int) -> CapacityPl
     return CapacityPlan(G, capacity, rows, exp_src, row_map, ovf.to(torch.int32), nrows)
 
 
+def padded_rows(rows: int, groups: int, align: int = 64) -> int:
+    """Static upper bound of the aligned re-layout's length (:func:`pad_plan`), a multiple of 8."""
+    return (rows + groups * (align - 1) + 7) // 8 * 8
+
+
+def pad_plan(offsets: torch.Tensor, rows: int, align: int = 64) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Aligned re-layout of `rows` expert-sorted rows (offsets int32 [G + 1]): every expert starts on a multiple of
+    `align`. Returns (src int32 [padded_rows(rows, G, align)]: padded row -> sorted row or -1, poff int32 [G + 1]:
+    the padded offsets, each range a multiple of align). Device-side, no host read."""
+    G = offsets.numel() - 1
+    P = padded_rows(rows, G, align)
+    if use_native(offsets):
+        return hip_ops().moe_pad_plan(offsets.contiguous(), P, align)
+    off = offsets.long()
+    cnt = off[1:] - off[:-1]
+    padc = (cnt + align - 1) // align * align
+    poff = torch.zeros(G + 1, dtype=torch.long, device=offsets.device)
+    poff[1:] = padc.cumsum(0)
+    src = torch.full((P,), -1, dtype=torch.int32, device=offsets.device)
+    j = torch.arange(rows, device=offsets.device)
+    e = torch.bucketize(j, off[1:], right=True)
+    src[poff[e] + (j - off[e])] = j.to(torch.int32)
+    return src, poff.to(torch.int32)
+
+
 def gather_rows(src: torch.Tensor, idx: torch.Tensor, idx2: Optional[torch.Tensor] = None,
                 nrows: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out[r] = src[idx2[idx[r]] if idx2 is given else idx[r]], zero rows where idx[r] < 0 (int32 idx). On the

@@ -309,7 +309,8 @@ def test_llama_chunked_head_matches_autograd_gpu(monkeypatch):
     _check("cuda")
 
 
-def test_mixtral_grouped_deferred_wgrad_matches_per_micro_batch_cpu(monkeypatch):
+@pytest.mark.parametrize("kmajor", [False, True])
+def test_mixtral_grouped_deferred_wgrad_matches_per_micro_batch_cpu(monkeypatch, kmajor):
     """The grouped expert path (device offsets) with the weight gradients deferred to the step's last
     micro-batch -- one segmented grouped dW GEMM per weight over every stashed micro-batch's rows -- equals the
     per-micro-batch grouped dW. CPU run of the same code (grouped ops' reference path)."""
@@ -317,6 +318,7 @@ def test_mixtral_grouped_deferred_wgrad_matches_per_micro_batch_cpu(monkeypatch)
     from distributed_llm_training_gpu_manager_amd.parallel.zero import EngineConfig, ZeroEngine
     from distributed_llm_training_gpu_manager_amd.ops import gemm_mfma as gm
     monkeypatch.setattr(gm, "CAPACITY", False)
+    monkeypatch.setattr(gm, "KMAJOR_DW", kmajor)  # stash transposed into the aligned re-layout, or token-major
     monkeypatch.setattr(MixtralBlock, "_grouped", lambda self, x, wgrad=False: True)
     mc = get_config("mixtral-tiny")
     g = torch.Generator().manual_seed(4)

@@ -166,3 +166,62 @@ def test_capacity_mode_hip_graph_replay_matches_eager_gpu(monkeypatch):
         assert abs(a - b) <= 1e-4 * max(1.0, abs(b)), (lg, le)
     err = float((eg.master - ee.master).abs().max() / ee.master.abs().max())
     assert err < 1e-4, err
+
+
+@pytest.mark.parametrize("counts", [[5, 0, 9, 70], [64, 1, 0, 0], [0, 0, 0, 3]])
+def test_pad_plan_and_remapped_transpose(counts):
+    from distributed_llm_training_gpu_manager_amd.ops.gemm import transpose
+    from distributed_llm_training_gpu_manager_amd.ops.moe import pad_plan, padded_rows
+    R = sum(counts)
+    src, poff = pad_plan(_offsets(counts), R, 64)
+    assert src.numel() == padded_rows(R, len(counts), 64)
+    assert all((b - a) % 64 == 0 for a, b in zip(poff.tolist()[:-1], poff.tolist()[1:]))
+    x = torch.randn(R, 24)
+    xt = transpose(x, rows=src)
+    off = 0
+    for e, n in enumerate(counts):
+        p0 = int(poff[e])
+        assert torch.equal(xt[:, p0:p0 + n], x[off:off + n].t())
+        assert float(xt[:, p0 + n:int(poff[e + 1])].abs().sum()) == 0.0
+        off += n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("counts", [[5, 0, 9, 70], [700, 1300, 0, 1048]])
+def test_pad_plan_and_remapped_transpose_gpu(counts):
+    from distributed_llm_training_gpu_manager_amd.ops.gemm import transpose
+    from distributed_llm_training_gpu_manager_amd.ops.moe import pad_plan
+    R = sum(counts)
+    src_c, poff_c = pad_plan(_offsets(counts), R, 64)
+    src_g, poff_g = pad_plan(_offsets(counts, "cuda"), R, 64)
+    assert torch.equal(src_g.cpu(), src_c) and torch.equal(poff_g.cpu(), poff_c)
+    x = torch.randn(R, 136).to(torch.bfloat16)
+    assert torch.equal(transpose(x.cuda(), rows=src_g).cpu(), transpose(x, rows=src_c))
+
+
+@pytest.mark.gpu
+def test_kmajor_segmented_wgrad_gpu_matches_fp32():
+    """The K-contiguous segmented grouped dW (aligned re-layout, two segments, uneven and empty experts) against
+    an fp32 reference."""
+    from distributed_llm_training_gpu_manager_amd.ops.gemm import transpose
+    from distributed_llm_training_gpu_manager_amd.ops.moe import pad_plan
+    G, M, N = 4, 256, 512
+    torch.manual_seed(0)
+    segs = [[130, 0, 300, 77], [5, 250, 0, 190]]
+    a_t, b_t, offs, ref = [], [], [], torch.zeros(G, M, N)
+    for counts in segs:
+        R = sum(counts)
+        a = torch.randn(R, M).to(torch.bfloat16)
+        b = torch.randn(R, N).to(torch.bfloat16)
+        src, poff = pad_plan(_offsets(counts, "cuda"), R, 64)
+        a_t.append(transpose(a.cuda(), rows=src))
+        b_t.append(transpose(b.cuda(), rows=src))
+        offs.append(poff)
+        o = 0
+        for e, n in enumerate(counts):
+            ref[e] += a[o:o + n].float().t() @ b[o:o + n].float()
+            o += n
+    out = torch.zeros(G, M, N, device="cuda")
+    gm.grouped_wgrad_segments(out, a_t, b_t, torch.stack(offs), acc=False, kmajor=True)
+    err = float((out.cpu() - ref).abs().max() / ref.abs().max())
+    assert err < 1e-5, err

@@ -11,3 +11,5 @@ for M in 1 cap; do
   echo "mode=$M"; [ $rc -eq 0 ] || { tail -15 gpurun_out/bench_mixtral_$M.err; exit $rc; }
   python -c "import json;d=json.load(open('gpurun_out/bench_mixtral_$M.json'));print(d['value'],d['ms_per_step'],d['extra']['mfu_vs_2.5PF_dense_bf16'],d['extra']['peak_GiB_max_over_ranks'])"
 done
+timeout -k 10 240 python -u tools/diag/fill_sources.py > gpurun_out/fill_sources.log 2>&1; rc=$?
+tail -25 gpurun_out/fill_sources.log; exit $rc
