@@ -207,7 +207,7 @@ def test_kmajor_segmented_wgrad_gpu_matches_fp32():
     from distributed_llm_training_gpu_manager_amd.ops.moe import pad_plan
     G, M, N = 4, 256, 512
     torch.manual_seed(0)
-    segs = [[130, 0, 300, 77], [5, 250, 0, 190]]
+    segs = [[130, 0, 300, 77], [5, 250, 0, 252]]  # one row count: one padded stride
     a_t, b_t, offs, ref = [], [], [], torch.zeros(G, M, N)
     for counts in segs:
         R = sum(counts)
