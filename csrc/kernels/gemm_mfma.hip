@@ -61,7 +61,16 @@ struct GemmArgs {
   int M, N, K;                     // K: dense / grouped-M reduction length; M: rows for dense/grouped-K
   int G, mode;
   int tiles_n, tiles_m;
+  int qskip;  // skip the MFMAs of row quadrants wholly past the valid rows (DLGM_GEMM_QSKIP=0: A/B off)
 };
+
+int qskip_env() {
+  static const int v = [] {
+    const char* e = std::getenv("DLGM_GEMM_QSKIP");
+    return (e != nullptr && e[0] == '0') ? 0 : 1;
+  }();
+  return v;
+}
 
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -358,11 +367,15 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
             acc[4 * mq + i][2 * nq + j] = mfma16(nq ? bq1[j][s2] : bq0[j][s2], af[i][s2], acc[4 * mq + i][2 * nq + j]);
       __builtin_amdgcn_s_setprio(0);
     };
+    // a partial M tile (a group's last row tile, or M % 256): a wave skips the MFMAs of its 64-row quadrants that
+    // lie wholly past the valid rows (their outputs are never stored) -- the SIMD's MFMA pipe then serves the
+    // partner wave alone. Barriers and DMA are unchanged, so the phase structure holds for every wave.
+    const int rv = p.qskip ? __builtin_amdgcn_readfirstlane(rows_valid) : BM;
     auto phase_end = [&](bool issued, int mq, int nq) {
       wait(issued);
       raw_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      mma(mq, nq);
+      if (wr * 128 + mq * 64 < rv) mma(mq, nq);
       raw_barrier();
     };
     auto ktile = [&](auto bufc, int t) {
@@ -503,6 +516,7 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
   p.c_gstride = mode == kGroupK ? out.stride(0) : 0;
   p.tiles_n = (int)(N / BN);
   p.tiles_m = (int)((M + BM - 1) / BM);
+  p.qskip = qskip_env();
   int64_t nblk;
   if (mode == kDense) {
     nblk = (int64_t)p.tiles_m * p.tiles_n;
