@@ -271,7 +271,10 @@ def main() -> int:
         dog = threading.Timer(args.comm_sweep_timeout, _stalled)
         dog.daemon = True
         dog.start()
-        rows = sweep(comm, env.device, sizes_mb=(16, 64, 256) if env.device.type == "cuda" else (1,))
+        try:  # a failing collective must never cost the result line
+            rows = sweep(comm, env.device, sizes_mb=(16, 64, 256) if env.device.type == "cuda" else (1,))
+        except Exception as e:  # noqa: BLE001
+            rows = f"sweep failed: {type(e).__name__}: {e}"[:400]
         dog.cancel()
         if out is not None:
             out["extra"]["comm_busbw"] = rows

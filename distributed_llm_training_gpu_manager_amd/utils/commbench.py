@@ -66,7 +66,11 @@ def sweep(comm: Comm, device,
     for op in ops:
         for mb in sizes_mb:
             nbytes = int(mb * (1 << 20))
-            dt = run(op, comm, nbytes, device, dtype, iters, warmup)
+            try:
+                dt = run(op, comm, nbytes, device, dtype, iters, warmup)
+            except Exception as e:  # noqa: BLE001 -- record it; the caller's watchdog covers a rank left behind
+                rows.append({"op": op, "MiB": mb, "error": f"{type(e).__name__}: {e}"[:200], "world": comm.world})
+                continue
             algbw = nbytes / dt / 1e9
             rows.append({"op": op, "MiB": mb, "time_us": round(dt * 1e6, 1), "algbw_GBps": round(algbw, 1),
                          "busbw_GBps": round(algbw * FACTOR[op](comm.world), 1), "world": comm.world})
