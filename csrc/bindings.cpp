@@ -74,6 +74,13 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
 void dlgm_gemm_mfma_seg(at::Tensor out, const std::vector<at::Tensor>& a, const std::vector<at::Tensor>& b,
                         const at::Tensor& offsets, bool accumulate, bool kmajor);
 
+// xgmi_mesh.hip
+at::Tensor dlgm_ipc_alloc(int64_t nbytes);
+at::Tensor dlgm_ipc_handle(const at::Tensor& buf);
+int64_t dlgm_ipc_open(const at::Tensor& handle);
+void dlgm_ipc_close(int64_t ptr);
+void dlgm_mesh_push(const at::Tensor& src, const at::Tensor& peers, int64_t dst_off, int64_t cap);
+
 TORCH_LIBRARY(dlgm, m) {
   m.def("rmsnorm_fwd(Tensor x, Tensor? residual, Tensor w, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("rmsnorm_bwd(Tensor dy, Tensor h, Tensor w, Tensor rstd, Tensor? dres, Tensor(a!) dw, bool accumulate_dw) -> Tensor");
@@ -101,6 +108,11 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("gemm_lt(Tensor(a!) out, Tensor a, Tensor b, float beta, int algo) -> int");
   m.def("gemm_lt_tune(Tensor out, Tensor a, Tensor b, float beta, int n_heuristic, bool all_algos, int reps) -> Tensor");
   m.def("gemm_lt_version() -> int", &dlgm_gemm_lt_version);
+  m.def("ipc_alloc(int nbytes) -> Tensor", &dlgm_ipc_alloc);
+  m.def("ipc_handle(Tensor buf) -> Tensor", &dlgm_ipc_handle);
+  m.def("ipc_open(Tensor handle) -> int", &dlgm_ipc_open);
+  m.def("ipc_close(int ptr) -> ()", &dlgm_ipc_close);
+  m.def("mesh_push(Tensor src, Tensor peers, int dst_off, int cap) -> ()");
   m.def("gemm_mfma(Tensor(a!) out, Tensor a, Tensor b, bool accumulate, Tensor? offsets, int mode, int M, int N, int K, int G, int b_gstride) -> ()");
   m.def("gemm_mfma_seg(Tensor(a!) out, Tensor[] a, Tensor[] b, Tensor offsets, bool accumulate, bool kmajor=False) -> ()");
 }
@@ -133,4 +145,5 @@ TORCH_LIBRARY_IMPL(dlgm, CUDA, m) {
   m.impl("gemm_lt_tune", &dlgm_gemm_lt_tune);
   m.impl("gemm_mfma", &dlgm_gemm_mfma);
   m.impl("gemm_mfma_seg", &dlgm_gemm_mfma_seg);
+  m.impl("mesh_push", &dlgm_mesh_push);
 }

@@ -11,13 +11,23 @@ from typing import Dict, List, Sequence
 
 import torch
 
-from ..parallel.comm import Comm
+from ..parallel.comm import DONE, Comm
 
-FACTOR = {"all_gather": lambda w: (w - 1) / w, "mesh_all_gather": lambda w: (w - 1) / w, "reduce_scatter": lambda w: (w - 1) / w,
+FACTOR = {"all_gather": lambda w: (w - 1) / w, "mesh_all_gather": lambda w: (w - 1) / w,
+          "ipc_mesh_all_gather": lambda w: (w - 1) / w, "reduce_scatter": lambda w: (w - 1) / w,
           "all_to_all": lambda w: (w - 1) / w, "all_reduce": lambda w: 2 * (w - 1) / w}
 
 
 def run(op: str, comm: Comm, nbytes: int, device, dtype, iters: int, warmup: int) -> float:
+    mesh_ref: list = []
+    try:
+        return _run(op, comm, nbytes, device, dtype, iters, warmup, mesh_ref)
+    finally:
+        for m in mesh_ref:
+            m.close()
+
+
+def _run(op: str, comm: Comm, nbytes: int, device, dtype, iters: int, warmup: int, mesh_ref: list) -> float:
     W = comm.world
     esz = torch.tensor([], dtype=dtype).element_size()
     n = max(W, nbytes // esz // W * W)
@@ -29,6 +39,14 @@ def run(op: str, comm: Comm, nbytes: int, device, dtype, iters: int, warmup: int
         inp = torch.randn(n // W, device=device).to(dtype)
         out = torch.empty(n, device=device, dtype=dtype)
         fn = lambda: comm.all_gather_mesh(out, inp, async_op=True)  # noqa: E731
+    elif op == "ipc_mesh_all_gather":
+        # peer-write mesh over HIP IPC symmetric buffers (parallel/xgmi_mesh.py); opt-in, GPU only: not part of
+        # bench.py's default post-timing sweep (a new transport must not put the result line at risk)
+        from ..parallel.xgmi_mesh import XgmiMesh
+        inp = torch.randn(n // W, device=device).to(dtype)
+        mesh = XgmiMesh(comm, n * esz, device)
+        mesh_ref.append(mesh)
+        fn = lambda: (mesh.all_gather(inp), DONE)[1]  # noqa: E731
     elif op == "reduce_scatter":
         inp = torch.randn(n, device=device).to(dtype)
         out = torch.empty(n // W, device=device, dtype=dtype)
