@@ -7,7 +7,11 @@ Attention is the Llama block's (GQA, RoPE theta 1e6). The FFN is a routed mixtur
     sort (token, k) slots by expert       one-workgroup HIP counting sort (moe_permute), one gather
     EP all-to-all                          rows to the rank owning the expert (RCCL)
     local experts: SwiGLU MLP              grouped MFMA GEMMs, one launch for all experts, group
-                                           offsets read on the device (no host sync at EP = 1)
+                                           offsets read on the device (no host sync at EP = 1); the
+                                           expert dW deferred to the step's last micro-batch as one
+                                           segmented launch per weight over K-contiguous operands
+                                           (each micro-batch transposed into an aligned re-layout);
+                                           opt-in alternative: the capacity layout (ops.moe.CapacityPlan)
     EP all-to-all back, combine            out[t] = sum_k gate * y[slot]  (HIP gather kernel)
 
 Backward is hand-written: the combine adjoint gives d(expert outputs) and d(gates),
