@@ -62,7 +62,9 @@ struct GemmArgs {
   int G, mode;
   int tiles_n, tiles_m;
   int qskip;  // skip the MFMAs of row quadrants wholly past the valid rows (DLGM_GEMM_QSKIP=0: A/B off)
-  int chunk;  // grouped-M: chunked round-robin XCD remap (DLGM_GEMM_CHUNK_REMAP=0: the XCD-contiguous remap)
+  int chunk;  // grouped-M: balanced remap over the real tiles (DLGM_GEMM_CHUNK_REMAP=0: contiguous over the grid)
+  int splitk;          // grouped-M split-K: each tile's K range in this many parts, fp32 partials
+  int64_t c_sstride;   // elements between the partial slices of C (split-K)
 };
 
 int env_flag(const char* name) {
@@ -203,14 +205,6 @@ __device__ __forceinline__ int xcd_remap(int id, int total) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + id / 8;
 }
 
-constexpr int kChunk = 32;  // consecutive ids kept on one XCD (an expert's row tiles of ~7 column panels)
-
-// block b runs on XCD b % 8 as its (b / 8)-th block; chunk c of kChunk consecutive ids goes to XCD c % 8
-__device__ __forceinline__ int chunk_remap(int b) {
-  const int x = b & 7, k = b >> 3;
-  return (k / kChunk) * (8 * kChunk) + x * kChunk + (k % kChunk);
-}
-
 __device__ __forceinline__ void raw_barrier() {
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
@@ -238,14 +232,30 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
 
   // ---- which tile (and group) this block computes. The mode is a template parameter: each
   // instantiation has straight-line pointer setup (no mode-dependent phis for the operand bases).
-  // grouped-M grids are sized for the worst case and their tail is spare blocks: an XCD-contiguous remap hands
-  // every spare id to the last XCD(s) and leaves them idle (the real tiles are the low ids), so wide grouped-M
-  // grids are remapped in chunks of kChunk consecutive ids dealt round-robin to the XCDs (a chunk still shares its
-  // weight panels inside one L2; Mixtral w13 forward 1.92 -> 1.77 ms); the grid is a multiple of 8 * kChunk
-  const int id = MODE == kGroupM && p.chunk ? chunk_remap(blockIdx.x) : xcd_remap(blockIdx.x, gridDim.x);
+  // grouped-M grids are sized for the worst case and their tail is spare blocks: the XCD-contiguous remap over the
+  // whole grid hands every spare id to the last XCD(s) and leaves them idle (the real tiles are the low ids)
+  int id;
+  if constexpr (MODE == kGroupM) {
+    if (p.chunk) {
+      // balanced XCD-contiguous order over the REAL tiles (counted from the device offsets): XCD x runs ids
+      // [x*q, (x+1)*q) first and its spare blocks last, so every XCD gets 1/8 of the work and each keeps the
+      // contiguous, L2-sharing run of an expert's tiles
+      int real = 0;
+      for (int e = 0; e < p.G; ++e) real += (p.offsets[e + 1] - p.offsets[e] + BM - 1) / BM;
+      real *= p.tiles_n * p.splitk;
+      const int q = (real + 7) / 8, x = blockIdx.x & 7, k = blockIdx.x >> 3;
+      id = x * q + k;
+      if (k >= q || id >= real) return;  // spare block (grid sized for the worst case)
+    } else {
+      id = xcd_remap(blockIdx.x, gridDim.x);
+    }
+  } else {
+    id = xcd_remap(blockIdx.x, gridDim.x);
+  }
   int tm = 0, tn, grp = 0;
   int m_lo = 0, m_hi = p.M;  // valid rows of A / C for this block
   int k_lo = 0, k_hi = p.K;  // reduction range
+  int64_t split_off = 0;     // grouped-M split-K: this block's partial slice of C (elements)
   constexpr int CES = EPI == kStoreBf16 ? 2 : 4;
   // tile order: GM output rows x all columns per group, walked down the GM rows first, so the ~32 blocks
   // resident on one XCD (consecutive ids after the XCD remap) cover a GM x (32/GM) patch: per K-step they
@@ -265,6 +275,14 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
     // (consecutive ids after the remap) share each weight column panel across all the expert's row tiles
     // (one HBM read of the panel, the rest L2 hits) instead of streaming every panel once per row tile
     int j = id;
+    if (p.splitk > 1) {  // adjacent ids = the K parts of one tile (same XCD: their A / B panels share L2 lines)
+      const int part = j % p.splitk;
+      j /= p.splitk;
+      const int ks = ((p.K + p.splitk - 1) / p.splitk + BK - 1) / BK * BK;
+      k_lo = part * ks;
+      k_hi = min(p.K, k_lo + ks);
+      split_off = (int64_t)part * p.c_sstride;
+    }
     grp = -1;
     for (int e = 0; e < p.G; ++e) {
       const int lo = p.offsets[e], hi = p.offsets[e + 1];
@@ -308,7 +326,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
   }
   const bf16* A0 = p.a;
   const bf16* B0 = p.b + (MODE == kGroupM ? (int64_t)grp * p.b_gstride : 0);
-  char* C = (char*)p.c + (MODE == kGroupK || MODE == kGroupKSeg ? (int64_t)grp * p.c_gstride * CES : 0);
+  char* C = (char*)p.c + (MODE == kGroupK || MODE == kGroupKSeg ? (int64_t)grp * p.c_gstride * CES : 0) +
+            split_off * CES;
   const int m0 = MODE == kGroupM ? m_lo : tm * BM;
   const int n0 = tn * BN;
   const int rows_valid = min(BM, m_hi - m0);
@@ -475,6 +494,26 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
   }
 }
 
+// out[i] = sum over the split-K partial slices (fp32, `parts` x n) -> bf16; 8 elements per thread
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, bf16* __restrict__ out,
+                                                            int parts, int64_t n) {
+  const int64_t n8 = n >> 3;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    f32x4 a0 = *reinterpret_cast<const f32x4*>(part + i * 8), a1 = *reinterpret_cast<const f32x4*>(part + i * 8 + 4);
+    for (int s2 = 1; s2 < parts; ++s2) {
+      a0 += *reinterpret_cast<const f32x4*>(part + s2 * n + i * 8);
+      a1 += *reinterpret_cast<const f32x4*>(part + s2 * n + i * 8 + 4);
+    }
+    const f32x8 acc = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    store8f(out + i * 8, acc);
+  }
+}
+
+int splitk_env() {
+  static const int v = env_flag("DLGM_GEMM_SPLITK");
+  return v;
+}
+
 template <int MODE, bool AK, bool BKM>
 void launch_epi(int epi, dim3 grid, hipStream_t st, const GemmArgs& a) {
   if (epi == kStoreBf16)
@@ -537,9 +576,19 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
   p.tiles_n = (int)(N / BN);
   p.tiles_m = (int)((M + BM - 1) / BM);
   p.qskip = qskip_env();
-  // wide outputs only: with 16 column tiles and a long K (the expert dX / down projections) the XCD-contiguous
-  // order keeps each expert's row panels (up to 15 MB each) on one L2 and measured 7.5 % faster than chunks
-  p.chunk = chunk_env() && p.tiles_n >= 32;
+  p.chunk = chunk_env();
+  p.splitk = 1;
+  // narrow grouped-M problems (<= 16 column tiles: the expert down projection and input gradients) fill only ~2.2
+  // rounds of 256 CUs, so a third round runs ~20 % full: split the long K in two (fp32 partials + one reduce)
+  at::Tensor part;
+  at::Tensor out_final = out;
+  if (mode == kGroupM && !out32 && p.tiles_n <= 16 && K >= 16384 && splitk_env()) {
+    p.splitk = 2;
+    part = at::empty({p.splitk, M, N}, out.options().dtype(at::kFloat));
+    p.c = part.data_ptr();
+    p.ldc = N;
+    p.c_sstride = M * N;
+  }
   int64_t nblk;
   if (mode == kDense) {
     nblk = (int64_t)p.tiles_m * p.tiles_n;
@@ -548,14 +597,14 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
                     offsets->numel() == G + 1, "gemm_mfma: grouped modes need int32 offsets[G+1] on the GPU");
     p.offsets = offsets->data_ptr<int>();
     if (mode == kGroupM) {
-      nblk = ((M + BM - 1) / BM + G) * p.tiles_n;  // M = total rows: worst-case tiles over all groups
-      nblk = (nblk + 8 * kChunk - 1) / (8 * kChunk) * (8 * kChunk);  // chunk_remap's period
+      nblk = ((M + BM - 1) / BM + G) * p.tiles_n * p.splitk;  // M = total rows: worst-case tiles over all groups
+      nblk = (nblk + 7) / 8 * 8;  // whole rounds of the 8 XCDs (the balanced remap's block -> XCD mapping)
     } else {
       nblk = G * (int64_t)p.tiles_m * p.tiles_n;
     }
   }
   if (nblk == 0) return;
-  const int epi = !out32 ? kStoreBf16 : accumulate ? kAccF32 : kStoreF32;
+  const int epi = p.splitk > 1 ? kStoreF32 : !out32 ? kStoreBf16 : accumulate ? kAccF32 : kStoreF32;
   auto st = c10::hip::getCurrentHIPStream();
   dim3 grid((unsigned)nblk);
   if (mode == kDense) {
@@ -576,6 +625,15 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
     launch_epi<kGroupK, false, false>(epi, grid, st, p);
   }
   DLGM_CHECK_HIP(hipGetLastError());
+  if (p.splitk > 1) {
+    TORCH_CHECK(out_final.is_contiguous() && out_final.size(-1) == N && (N % 8) == 0, "gemm_mfma: split-K out layout");
+    const int64_t n = M * N;
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n / 8 + 255) / 256, 4096));
+    splitk_reduce_kernel<<<(unsigned)blocks, 256, 0, st>>>(part.data_ptr<float>(),
+                                                           reinterpret_cast<bf16*>(out_final.data_ptr()),
+                                                           p.splitk, n);
+    DLGM_CHECK_HIP(hipGetLastError());
+  }
 }
 
 // Grouped-K over segments: out[g] (+)= sum over s of a[s][rows of g in s]^T @ b[s][rows of g in s], with

@@ -85,6 +85,26 @@ def test_grouped_rows_forward_uneven_and_empty_groups():
         lo += n
 
 
+@pytest.mark.parametrize("transpose_w", [True, False])
+def test_grouped_rows_narrow_long_k_split_k(transpose_w):
+    """Narrow output (<= 16 column tiles) with a long K: the grouped-M launch splits K in two (fp32 partials + a
+    reduce kernel), uneven / empty / single-row groups; also the balanced XCD remap over the real tiles."""
+    g = torch.Generator(device=dev).manual_seed(7)
+    sizes = [700, 0, 1, 513, 1300, 77, 256, 33]
+    R, K, N, G = sum(sizes), 16384, 512, len(sizes)
+    offs = torch.tensor([0] + list(torch.tensor(sizes).cumsum(0)), dtype=torch.int32, device=dev)
+    x = torch.randn(R, K, device=dev, generator=g).to(torch.bfloat16)
+    w = (torch.randn(G, N, K, device=dev, generator=g) if transpose_w else
+         torch.randn(G, K, N, device=dev, generator=g)).to(torch.bfloat16)
+    out = gm.grouped_mm(x, w, offs, transpose_w=transpose_w)
+    lo = 0
+    for e, n in enumerate(sizes):
+        if n:
+            we = w[e].float().t() if transpose_w else w[e].float()
+            assert _rel(out[lo:lo + n], x[lo:lo + n].float() @ we) < 1e-2, e
+        lo += n
+
+
 def test_grouped_weight_gradient_uneven_and_empty_groups():
     g = torch.Generator(device=dev).manual_seed(3)
     sizes = [130, 0, 700, 1]
