@@ -53,11 +53,14 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_moe_permute(const at::Tensor
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dlgm_moe_capacity_plan(const at::Tensor& offsets,
                                                                                    int64_t rows, int64_t capacity);
 std::tuple<at::Tensor, at::Tensor> dlgm_moe_pad_plan(const at::Tensor& offsets, int64_t padded_rows, int64_t align);
+std::tuple<at::Tensor, at::Tensor> dlgm_moe_pad_plan_multi(const at::Tensor& offsets, int64_t padded_rows,
+                                                            int64_t align);
 at::Tensor dlgm_gather_rows(const at::Tensor& src, const at::Tensor& idx, const c10::optional<at::Tensor>& idx2,
                             const c10::optional<at::Tensor>& nrows);
 // transpose.hip
 at::Tensor dlgm_transpose(const at::Tensor& x, const c10::optional<at::Tensor>& out,
                           const c10::optional<at::Tensor>& rows);
+at::Tensor dlgm_transpose_multi(const std::vector<at::Tensor>& xs, const at::Tensor& rows);
 // embedding.hip
 at::Tensor dlgm_embedding_fwd(const at::Tensor& table, const at::Tensor& ids);
 void dlgm_embedding_bwd_(at::Tensor grad, const at::Tensor& dy, const at::Tensor& sorted_ids, const at::Tensor& order);
@@ -99,6 +102,8 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("moe_permute(Tensor topi, int n_experts) -> (Tensor, Tensor, Tensor)");
   m.def("moe_capacity_plan(Tensor offsets, int rows, int capacity) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("moe_pad_plan(Tensor offsets, int padded_rows, int align) -> (Tensor, Tensor)");
+  m.def("moe_pad_plan_multi(Tensor offsets, int padded_rows, int align) -> (Tensor, Tensor)");
+  m.def("transpose_multi(Tensor[] xs, Tensor rows) -> Tensor");
   m.def("gather_rows(Tensor src, Tensor idx, Tensor? idx2=None, Tensor? nrows=None) -> Tensor");
   m.def("transpose(Tensor x, Tensor(a!)? out=None, Tensor? rows=None) -> Tensor");
   m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, float softmax_scale, bool causal, Tensor? dqkv=None) -> (Tensor, Tensor, Tensor)");
@@ -137,6 +142,8 @@ TORCH_LIBRARY_IMPL(dlgm, CUDA, m) {
   m.impl("moe_capacity_plan", &dlgm_moe_capacity_plan);
   m.impl("gather_rows", &dlgm_gather_rows);
   m.impl("moe_pad_plan", &dlgm_moe_pad_plan);
+  m.impl("moe_pad_plan_multi", &dlgm_moe_pad_plan_multi);
+  m.impl("transpose_multi", &dlgm_transpose_multi);
   m.impl("transpose", &dlgm_transpose);
   m.impl("embedding_fwd", &dlgm_embedding_fwd);
   m.impl("embedding_bwd_", &dlgm_embedding_bwd_);

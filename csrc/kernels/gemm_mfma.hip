@@ -552,7 +552,9 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
   TORCH_CHECK(mode == kGroupM || M % BM == 0 || ak, "gemm_mfma: M-contiguous a needs M % 256 == 0");
   TORCH_CHECK(mode == kGroupK || K % BK == 0, "gemm_mfma: K must be a multiple of 64");
   // a group's reduction range ends anywhere: only the MN-contiguous images mask partial k tiles
-  TORCH_CHECK(mode != kGroupK || (!ak && !bk), "gemm_mfma: grouped-K needs token-major (row = k) operands");
+  // grouped-K: token-major operands (row = k; partial K tiles at group ends are zero-filled in LDS), or both
+  // K-contiguous with every group's K range on whole 64-wide tiles (the aligned re-layout, ops.moe.pad_plan_multi)
+  TORCH_CHECK(mode != kGroupK || (!ak && !bk) || (ak && bk), "gemm_mfma: grouped-K operands both token-major or both K-major");
   TORCH_CHECK(mode != kGroupM || ak, "gemm_mfma: grouped-M needs row-major (K-contiguous) rows");
   TORCH_CHECK(mode == kDense || mode == kGroupM || mode == kGroupK, "gemm_mfma: bad mode");
   for (const at::Tensor* t : {&a, &b2}) {
@@ -621,6 +623,8 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
       launch_epi<kGroupM, true, true>(epi, grid, st, p);
     else
       launch_epi<kGroupM, true, false>(epi, grid, st, p);
+  } else if (ak && bk) {  // K-major, tile-aligned group ranges
+    launch_epi<kGroupK, true, true>(epi, grid, st, p);
   } else {  // token-major operands (checked above)
     launch_epi<kGroupK, false, false>(epi, grid, st, p);
   }

@@ -202,6 +202,50 @@ __global__ __launch_bounds__(256) void moe_pad_plan_kernel(const int* __restrict
   }
 }
 
+// The same re-layout over S row sets (micro-batches) at once: expert e's rows of set 0, then of set 1, ... are
+// contiguous from padded row poff[e] (a multiple of align). rows[p] = (set << 24) | row within the set, or -1.
+// offsets [S, G + 1]: set s's expert split. One grouped-K launch then reduces each expert over all its rows with
+// contiguous, tile-aligned K ranges (no per-segment selection inside the GEMM's pipelined loop).
+constexpr int kMaxSets = 8;
+
+__global__ __launch_bounds__(256) void moe_pad_plan_multi_kernel(const int* __restrict__ offsets, int S, int G,
+                                                                 int64_t P, int align, int* __restrict__ rows,
+                                                                 int* __restrict__ poff) {
+  __shared__ int s_off[kMaxSets][kMaxCapGroups + 1], s_cum[kMaxSets + 1][kMaxCapGroups], s_pad[kMaxCapGroups + 1];
+  for (int i = threadIdx.x; i < S * (G + 1); i += blockDim.x) s_off[i / (G + 1)][i % (G + 1)] = offsets[i];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int e = 0; e < G; ++e) {
+      int c = 0;
+      for (int t = 0; t < S; ++t) {
+        s_cum[t][e] = c;
+        c += s_off[t][e + 1] - s_off[t][e];
+      }
+      s_cum[S][e] = c;
+      s_pad[e] = acc;
+      acc += (c + align - 1) / align * align;
+    }
+    s_pad[G] = acc;
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && (int)threadIdx.x <= G) poff[threadIdx.x] = s_pad[threadIdx.x];
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < P; p += (int64_t)gridDim.x * blockDim.x) {
+    int src = -1;
+    if (p < s_pad[G]) {
+      int e = 0;
+      while (s_pad[e + 1] <= p) ++e;
+      const int r = (int)p - s_pad[e];
+      if (r < s_cum[S][e]) {
+        int t = 0;
+        while (s_cum[t + 1][e] <= r) ++t;
+        src = (t << 24) | (s_off[t][e] + r - s_cum[t][e]);
+      }
+    }
+    rows[p] = src;
+  }
+}
+
 // out[r] = src[idx2 ? idx2[idx[r]] : idx[r]] for idx[r] >= 0, zeros for idx[r] < 0; rows at or past *nrows (when
 // given) are left untouched. One wave per row, 16 B per lane.
 template <typename E>
@@ -309,6 +353,22 @@ std::tuple<at::Tensor, at::Tensor> dlgm_moe_pad_plan(const at::Tensor& offsets, 
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((padded_rows + 255) / 256, 2048));
   moe_pad_plan_kernel<<<(unsigned)blocks, 256, 0, c10::hip::getCurrentHIPStream()>>>(
       offsets.data_ptr<int>(), (int)G, padded_rows, (int)align, rows.data_ptr<int>(), poff.data_ptr<int>());
+  DLGM_CHECK_HIP(hipGetLastError());
+  return {rows, poff};
+}
+
+std::tuple<at::Tensor, at::Tensor> dlgm_moe_pad_plan_multi(const at::Tensor& offsets, int64_t padded_rows,
+                                                            int64_t align) {
+  TORCH_CHECK(offsets.is_cuda() && offsets.scalar_type() == at::kInt && offsets.is_contiguous() && offsets.dim() == 2,
+              "moe_pad_plan_multi: offsets must be a contiguous int32 [S, G + 1] GPU tensor");
+  const int64_t S = offsets.size(0), G = offsets.size(1) - 1;
+  TORCH_CHECK(S >= 1 && S <= kMaxSets && G >= 1 && G <= kMaxCapGroups && align >= 1 && padded_rows >= 0 &&
+                  padded_rows < (1ll << 31), "moe_pad_plan_multi: 1..8 sets, 1..64 groups, align >= 1");
+  auto rows = at::empty({padded_rows}, offsets.options());
+  auto poff = at::empty({G + 1}, offsets.options());
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((padded_rows + 255) / 256, 2048));
+  moe_pad_plan_multi_kernel<<<(unsigned)blocks, 256, 0, c10::hip::getCurrentHIPStream()>>>(
+      offsets.data_ptr<int>(), (int)S, (int)G, padded_rows, (int)align, rows.data_ptr<int>(), poff.data_ptr<int>());
   DLGM_CHECK_HIP(hipGetLastError());
   return {rows, poff};
 }

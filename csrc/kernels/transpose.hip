@@ -15,9 +15,14 @@ using namespace dlgm;
 namespace {
 
 // rows (optional): output column r of y takes source row rows[r] of x, or zeros when rows[r] < 0 (R = len(rows))
+struct Sources {  // up to 8 row-major sources of one row stride, passed by value (no host-to-device copy)
+  const bf16* p[8];
+  int n;
+};
+
 __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
                                                              int64_t R, int64_t C, int64_t ldx, int64_t ldy,
-                                                             const int* __restrict__ rows) {
+                                                             const int* __restrict__ rows, Sources srcs) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -33,7 +38,16 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restr
         v[j] = *reinterpret_cast<const short8*>(x + (r0 + j) * ldx + c0);
       } else {
         const int src = rows[r0 + j];
-        v[j] = src >= 0 ? *reinterpret_cast<const short8*>(x + (int64_t)src * ldx + c0) : (short8)(0);
+        if (srcs.n == 0) {
+          v[j] = src >= 0 ? *reinterpret_cast<const short8*>(x + (int64_t)src * ldx + c0) : (short8)(0);
+        } else {  // several sources: rows[] = (source << 24) | row; the source is picked among kernel arguments
+          const int si = src >= 0 ? (src >> 24) : 0;
+          const bf16* xs = srcs.p[0];
+#pragma unroll
+          for (int q = 1; q < 8; ++q) xs = si == q ? srcs.p[q] : xs;
+          v[j] = src >= 0 ? *reinterpret_cast<const short8*>(xs + (int64_t)(src & 0xFFFFFF) * ldx + c0)
+                          : (short8)(0);
+        }
       }
     }
     short8 o[8];
@@ -71,7 +85,36 @@ at::Tensor dlgm_transpose(const at::Tensor& x, const c10::optional<at::Tensor>& 
   const int64_t grid = std::min<int64_t>((tiles + 3) / 4, 256 * 16);
   transpose_bf16_kernel<<<grid, 256, 0, c10::hip::getCurrentHIPStream()>>>(
       reinterpret_cast<const bf16*>(x.data_ptr()), reinterpret_cast<bf16*>(y.data_ptr()), R, C, x.stride(0), R,
-      remap ? rows_opt->data_ptr<int>() : nullptr);
+      remap ? rows_opt->data_ptr<int>() : nullptr, Sources{{}, 0});
+  DLGM_CHECK_HIP(hipGetLastError());
+  return y;
+}
+
+// out[C, P] = the columns of several row-major sources x_s [R_s, C] (one row stride), laid out by `rows` (int32 [P],
+// P % 8 == 0: (s << 24) | row, or -1 for a zero column): the deferred expert dW's K-contiguous operand with every
+// expert's rows of all micro-batches contiguous (ops.moe.pad_plan_multi).
+at::Tensor dlgm_transpose_multi(const std::vector<at::Tensor>& xs, const at::Tensor& rows) {
+  TORCH_CHECK(!xs.empty() && xs.size() <= 8, "transpose_multi: 1..8 sources");
+  const at::Tensor& x0 = xs[0];
+  TORCH_CHECK(rows.is_cuda() && rows.scalar_type() == at::kInt && rows.is_contiguous() && rows.dim() == 1,
+              "transpose_multi: rows must be a contiguous int32 GPU vector");
+  const int64_t P = rows.numel(), C = x0.size(1);
+  Sources srcs{{}, (int)xs.size()};
+  for (const at::Tensor& x : xs) {
+    TORCH_CHECK(x.is_cuda() && DLGM_IS16(x) && x.dim() == 2 && x.stride(1) == 1 && x.size(1) == C &&
+                    x.stride(0) == x0.stride(0) && x.scalar_type() == x0.scalar_type() && x.size(0) < (1 << 24),
+                "transpose_multi: sources [R_s, C] of one dtype and row stride, R_s < 2^24");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "transpose_multi: 16-byte aligned sources");
+    srcs.p[&x - &xs[0]] = reinterpret_cast<const bf16*>(x.data_ptr());
+  }
+  TORCH_CHECK(P % 8 == 0 && C % 8 == 0 && x0.stride(0) % 8 == 0, "transpose_multi: P, C and the row stride % 8");
+  at::Tensor y = at::empty({C, P}, x0.options());
+  if (P == 0 || C == 0) return y;
+  const int64_t tiles = ((P + 63) / 64) * ((C + 63) / 64);
+  const int64_t grid = std::min<int64_t>((tiles + 3) / 4, 256 * 16);
+  transpose_bf16_kernel<<<grid, 256, 0, c10::hip::getCurrentHIPStream()>>>(
+      reinterpret_cast<const bf16*>(x0.data_ptr()), reinterpret_cast<bf16*>(y.data_ptr()), P, C, x0.stride(0), P,
+      rows.data_ptr<int>(), srcs);
   DLGM_CHECK_HIP(hipGetLastError());
   return y;
 }

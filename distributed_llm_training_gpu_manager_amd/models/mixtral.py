@@ -9,8 +9,9 @@ Attention is the Llama block's (GQA, RoPE theta 1e6). The FFN is a routed mixtur
     local experts: SwiGLU MLP              grouped MFMA GEMMs, one launch for all experts, group
                                            offsets read on the device (no host sync at EP = 1); the
                                            expert dW deferred to the step's last micro-batch as one
-                                           segmented launch per weight over K-contiguous operands
-                                           (each micro-batch transposed into an aligned re-layout);
+                                           grouped-K launch per weight over K-contiguous operands (the
+                                           stashed micro-batches transposed once into an aligned re-layout,
+                                           each expert's rows of all micro-batches contiguous);
                                            opt-in alternative: the capacity layout (ops.moe.CapacityPlan)
     EP all-to-all back, combine            out[t] = sum_k gate * y[slot]  (HIP gather kernel)
 
@@ -31,10 +32,10 @@ from typing import Any, List, Tuple
 import torch
 
 from .. import ops
-from ..ops.gemm import grad_mm, transpose
+from ..ops.gemm import grad_mm, transpose_multi
 from ..ops import gemm_mfma as gm
 from ..ops.moe import (capacity_plan, capacity_rows, gather_rows, moe_combine, moe_combine_bwd, moe_permute,
-                       pad_plan)
+                       pad_plan_multi)
 from ..parallel.ep import ExpertDispatcher
 from .common import ParamSpec, Params, StepContext, Unit
 from .config import ModelConfig
@@ -234,14 +235,11 @@ class MixtralBlock(LlamaBlock):
                 # dW once per step over the micro-batches' rows regrouped expert-major on the device
                 if ctx.micro_index == 0:
                     self._wstash, self._wflushed, self._wbytes = [], False, 0
-                if gm.KMAJOR_DW and self.dispatcher(ctx).W == 1:
-                    # K-contiguous operands for the deferred dW: each stashed tensor transposed into an aligned
-                    # re-layout (every expert's rows start on a 64-column boundary, zero padded), so the segmented
-                    # kernel reads ds_read_b128 fragments on whole K tiles instead of transposed LDS reads
-                    src, poff = pad_plan(offs, x.shape[0])
-                    item = tuple(transpose(t, rows=src) for t in (dy, a_all, dgu_all, x)) + (poff, True)
-                else:
-                    item = (dy, a_all, dgu_all, x, offs, False)
+                # K-major flush (gm.KMAJOR_DW): the rows stay row-major until the step's last micro-batch, then
+                # each operand of all stashed micro-batches is transposed ONCE into an aligned re-layout where every
+                # expert's rows of all micro-batches are contiguous and start on a 64-column boundary -> one plain
+                # grouped-K launch per weight (K-contiguous fragments, no per-segment selection in its loop)
+                item = (dy, a_all, dgu_all, x, offs, gm.KMAJOR_DW)
                 self._wstash.append(item)
                 self._wbytes += sum(t.numel() * t.element_size() for t in item[:4])
                 if ctx.last_micro or self._wbytes > getattr(ctx, "defer_budget_bytes", 48 << 30):
@@ -347,13 +345,18 @@ class MixtralBlock(LlamaBlock):
         self._wstash, self._wflushed, self._wbytes = [], True, 0
         for i in range(0, len(stash), gm.MAX_SEGMENTS):
             part = stash[i:i + gm.MAX_SEGMENTS]
-            km = part[0][5]
-            assert all(t[5] == km for t in part)
             offs = torch.stack([t[4] for t in part])  # [segments, experts + 1] int32, on the device
-            gm.grouped_wgrad_segments(g["w_down"], [t[0] for t in part], [t[1] for t in part], offs, acc or i > 0,
-                                      kmajor=km)
+            if part[0][5]:
+                src, poff = pad_plan_multi(offs, sum(int(t[0].shape[0]) for t in part))
+                for wname, ia, ib in (("w_down", 0, 1), ("w_gate_up", 2, 3)):
+                    at_ = transpose_multi([t[ia] for t in part], src)
+                    bt_ = transpose_multi([t[ib] for t in part], src)
+                    gm.grouped_wgrad(g[wname], at_, bt_, poff, acc or i > 0, kmajor=True)
+                    del at_, bt_
+                continue
+            gm.grouped_wgrad_segments(g["w_down"], [t[0] for t in part], [t[1] for t in part], offs, acc or i > 0)
             gm.grouped_wgrad_segments(g["w_gate_up"], [t[2] for t in part], [t[3] for t in part], offs,
-                                      acc or i > 0, kmajor=km)
+                                      acc or i > 0)
 
     def moe_backward(self, p: Params, g: Params, hn2: torch.Tensor, saved, dout: torch.Tensor, ctx: StepContext):
         if saved[0] == "cap":

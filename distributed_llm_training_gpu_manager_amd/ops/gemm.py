@@ -179,6 +179,22 @@ def transpose(x: torch.Tensor, out: Optional[torch.Tensor] = None, rows: Optiona
     return y
 
 
+def transpose_multi(xs: list, rows: torch.Tensor) -> torch.Tensor:
+    """out[C, P]: column p = xs[rows[p] >> 24][rows[p] & 0xFFFFFF] (zeros where rows[p] < 0); xs row-major [R_s, C]
+    of one dtype / row stride, at most 8 (csrc/kernels/transpose.hip, one launch)."""
+    if use_native(xs[0]):
+        return hip_ops().transpose_multi(list(xs), rows)
+    r = rows.long()
+    valid = r >= 0
+    s, i = (r >> 24).clamp(min=0), (r & 0xFFFFFF)
+    C = xs[0].shape[1]
+    out = torch.zeros(C, r.numel(), dtype=xs[0].dtype)
+    for t, x in enumerate(xs):
+        m = valid & (s == t)
+        out[:, m] = x[i[m]].t()
+    return out
+
+
 def dx_mm(dy: torch.Tensor, p: dict, name: str) -> torch.Tensor:
     """Input gradient dy @ W for a weight stored [out, in]. When the engine supplies the cached
     transpose ``p[name + ".T"]`` ([in, out], refreshed once per optimizer step) the GEMM runs as

@@ -120,16 +120,24 @@ def grouped_mm(x: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, transpos
 
 
 def grouped_wgrad(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, offsets: torch.Tensor,
-                  acc: bool = False) -> torch.Tensor:
-    """out[e] (+)= a[rows of e]^T @ b[rows of e]: a [R, M], b [R, N] row-major (token rows), out [G, M, N]."""
+                  acc: bool = False, kmajor: bool = False) -> torch.Tensor:
+    """out[e] (+)= a[rows of e]^T @ b[rows of e]: a [R, M], b [R, N] row-major (token rows), out [G, M, N].
+    kmajor: a [M, P] and b [N, P] come transposed (K contiguous) with every group's column range a whole number
+    of 64-wide tiles, zero padded (ops.moe.pad_plan_multi + ops.gemm.transpose_multi)."""
     G, M, N = out.shape
     if use_native(out):
-        hip_ops().gemm_mfma(out, a.t(), b, acc, offsets, GROUP_K, M, N, a.shape[0], G, 0)
+        if kmajor:
+            hip_ops().gemm_mfma(out, a, b.t(), acc, offsets, GROUP_K, M, N, a.shape[1], G, 0)
+        else:
+            hip_ops().gemm_mfma(out, a.t(), b, acc, offsets, GROUP_K, M, N, a.shape[0], G, 0)
         return out
     offs = offsets.tolist()
     for e in range(G):
         lo, hi = offs[e], offs[e + 1]
-        r = a[lo:hi].float().t() @ b[lo:hi].float()
+        if kmajor:
+            r = a[:, lo:hi].float() @ b[:, lo:hi].float().t()
+        else:
+            r = a[lo:hi].float().t() @ b[lo:hi].float()
         if acc:
             out[e].add_(r.to(out.dtype))
         else:

@@ -121,6 +121,31 @@ def pad_plan(offsets: torch.Tensor, rows: int, align: int = 64) -> Tuple[torch.T
     return src, poff.to(torch.int32)
 
 
+def pad_plan_multi(offsets: torch.Tensor, rows: int, align: int = 64) -> Tuple[torch.Tensor, torch.Tensor]:
+    """:func:`pad_plan` over S row sets at once (offsets int32 [S, G + 1], `rows` = the sets' total): expert e's
+    rows of set 0, set 1, ... are contiguous from padded row poff[e] (a multiple of `align`). Returns (src int32
+    [padded_rows(rows, G, align)]: (set << 24) | row, or -1; poff int32 [G + 1]). For ops.gemm.transpose_multi."""
+    S, G = offsets.shape[0], offsets.shape[1] - 1
+    P = padded_rows(rows, G, align)
+    if use_native(offsets):
+        return hip_ops().moe_pad_plan_multi(offsets.contiguous(), P, align)
+    off = offsets.long()
+    cnt = off[:, 1:] - off[:, :-1]  # [S, G]
+    tot = cnt.sum(0)
+    padc = (tot + align - 1) // align * align
+    poff = torch.zeros(G + 1, dtype=torch.long)
+    poff[1:] = padc.cumsum(0)
+    src = torch.full((P,), -1, dtype=torch.int32)
+    for e in range(G):
+        p = int(poff[e])
+        for t in range(S):
+            n = int(cnt[t, e])
+            lo = int(off[t, e])
+            src[p:p + n] = (t << 24) | torch.arange(lo, lo + n, dtype=torch.int32)
+            p += n
+    return src.to(offsets.device), poff.to(torch.int32).to(offsets.device)
+
+
 def gather_rows(src: torch.Tensor, idx: torch.Tensor, idx2: Optional[torch.Tensor] = None,
                 nrows: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out[r] = src[idx2[idx[r]] if idx2 is given else idx[r]], zero rows where idx[r] < 0 (int32 idx). On the

@@ -54,5 +54,49 @@ def main():
         print(f"narrow N {d} K {K2}: grouped {t2:.3f} ms {f2 / t2 / 1e9:.0f} TF/s")
 
 
+def seg_dw():
+    """K-major segmented grouped dW (4 micro-batches x 8 experts, Mixtral w13 dW [8, 28672, 4096]) against the dense
+    kernel on one expert-sized K-major problem (x 8)."""
+    from distributed_llm_training_gpu_manager_amd.ops.gemm import transpose
+    from distributed_llm_training_gpu_manager_amd.ops.moe import pad_plan
+    dev = "cuda"
+    counts = [1320, 870, 1105, 940, 1010, 1190, 760, 997]
+    E, M, N = 8, 28672, 4096
+    R = sum(counts)
+    offs = torch.zeros(E + 1, dtype=torch.int32)
+    offs[1:] = torch.tensor(counts).cumsum(0)
+    src, poff = pad_plan(offs.to(dev), R, 64)
+    a_t, b_t = [], []
+    for _ in range(4):
+        a_t.append(transpose(torch.randn(R, M, device=dev).to(torch.bfloat16), rows=src))
+        b_t.append(transpose(torch.randn(R, N, device=dev).to(torch.bfloat16), rows=src))
+    offs_s = torch.stack([poff] * 4)
+    out = torch.zeros(E, M, N, device=dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    gm.grouped_wgrad_segments(out, a_t, b_t, offs_s, kmajor=True)
+    K1 = 4 * 1024
+    a1 = torch.randn(M, K1, device=dev).to(torch.bfloat16)
+    b1 = torch.randn(N, K1, device=dev).to(torch.bfloat16)
+    o1 = torch.zeros(M, N, device=dev)
+    gm.mfma_mm(o1, a1, b1.t())
+    torch.cuda.synchronize()
+    ev[0].record()
+    for _ in range(3):
+        gm.grouped_wgrad_segments(out, a_t, b_t, offs_s, kmajor=True)
+    ev[1].record()
+    for _ in range(3):
+        for _e in range(E):
+            gm.mfma_mm(o1, a1, b1.t())
+    ev[2].record()
+    torch.cuda.synchronize()
+    ts, td = ev[0].elapsed_time(ev[1]) / 3, ev[1].elapsed_time(ev[2]) / 3
+    f = 2.0 * 4 * R * M * N
+    fd = 2.0 * E * K1 * M * N
+    print(f"seg dW kmajor {ts:.3f} ms {f / ts / 1e9:.0f} TF/s | dense x8 (K {K1}) {td:.3f} ms {fd / td / 1e9:.0f} TF/s")
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "seg":
+        seg_dw()
+        sys.exit(0)
     main()
