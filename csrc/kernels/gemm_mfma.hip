@@ -65,6 +65,7 @@ struct GemmArgs {
   int chunk;  // grouped-M: balanced remap over the real tiles (DLGM_GEMM_CHUNK_REMAP=0: contiguous over the grid)
   int splitk;          // grouped-M split-K: each tile's K range in this many parts, fp32 partials
   int64_t c_sstride;   // elements between the partial slices of C (split-K)
+  int nreal;           // grouped-K with the chunk remap: real blocks (the grid is rounded up to 8 * kChunk)
 };
 
 int env_flag(const char* name) {
@@ -205,6 +206,14 @@ __device__ __forceinline__ int xcd_remap(int id, int total) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + id / 8;
 }
 
+constexpr int kChunk = 32;  // consecutive ids kept on one XCD (a 4-row x 8-column patch of one group's tiles)
+
+// block b runs on XCD b % 8 as its (b / 8)-th block; chunk c of kChunk consecutive ids goes to XCD c % 8
+__device__ __forceinline__ int chunk_remap(int b) {
+  const int x = b & 7, k = b >> 3;
+  return (k / kChunk) * (8 * kChunk) + x * kChunk + (k % kChunk);
+}
+
 __device__ __forceinline__ void raw_barrier() {
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
@@ -246,6 +255,17 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
       const int q = (real + 7) / 8, x = blockIdx.x & 7, k = blockIdx.x >> 3;
       id = x * q + k;
       if (k >= q || id >= real) return;  // spare block (grid sized for the worst case)
+    } else {
+      id = xcd_remap(blockIdx.x, gridDim.x);
+    }
+  } else if constexpr (MODE == kGroupK || MODE == kGroupKSeg) {
+    // grouped-K: a group's tiles are contiguous ids and their work scales with the group's rows, so the XCD-
+    // contiguous remap gave each XCD about one expert and the launch waited for the busiest expert's XCD (+29 %
+    // at Mixtral routing); chunks of kChunk consecutive ids dealt round-robin give every XCD the same mix of
+    // experts and keep each chunk's A / B panels inside one L2. The grid is a multiple of 8 * kChunk.
+    if (p.chunk) {
+      id = chunk_remap(blockIdx.x);
+      if (id >= p.nreal) return;
     } else {
       id = xcd_remap(blockIdx.x, gridDim.x);
     }
@@ -603,6 +623,8 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
       nblk = (nblk + 7) / 8 * 8;  // whole rounds of the 8 XCDs (the balanced remap's block -> XCD mapping)
     } else {
       nblk = G * (int64_t)p.tiles_m * p.tiles_n;
+      p.nreal = (int)nblk;
+      if (p.chunk) nblk = (nblk + 8 * kChunk - 1) / (8 * kChunk) * (8 * kChunk);
     }
   }
   if (nblk == 0) return;
@@ -700,8 +722,11 @@ void dlgm_gemm_mfma_seg(at::Tensor out, const std::vector<at::Tensor>& a, const 
   p.c_gstride = out.stride(0);
   p.tiles_n = (int)(N / BN);
   p.tiles_m = (int)(M / BM);
-  const int64_t nblk = G * (int64_t)p.tiles_m * p.tiles_n;
+  int64_t nblk = G * (int64_t)p.tiles_m * p.tiles_n;
   if (nblk == 0) return;
+  p.nreal = (int)nblk;
+  p.chunk = chunk_env();
+  if (p.chunk) nblk = (nblk + 8 * kChunk - 1) / (8 * kChunk) * (8 * kChunk);
   if (kmajor)
     launch_epi<kGroupKSeg, true, true>(accumulate ? kAccF32 : kStoreF32, dim3((unsigned)nblk),
                                        c10::hip::getCurrentHIPStream(), p);
