@@ -604,7 +604,7 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
   // rounds of 256 CUs, so a third round runs ~20 % full: split the long K in two (fp32 partials + one reduce)
   at::Tensor part;
   at::Tensor out_final = out;
-  if (mode == kGroupM && !out32 && p.tiles_n <= 16 && K >= 16384 && splitk_env()) {
+  if (mode == kGroupM && !out32 && out.is_contiguous() && ldc == N && p.tiles_n <= 16 && K >= 16384 && splitk_env()) {
     p.splitk = 2;
     part = at::empty({p.splitk, M, N}, out.options().dtype(at::kFloat));
     p.c = part.data_ptr();
