@@ -1,5 +1,7 @@
-"""MoE ops: router top-k (csrc/kernels/embedding.hip) and the gather-based, deterministic,
-atomic-free combine (csrc/kernels/moe.hip)."""
+"""MoE ops: router top-k (csrc/kernels/embedding.hip), the device-side expert permute, the gather-based,
+deterministic, atomic-free combine, the capacity plan and the aligned re-layouts of the deferred expert dW
+(csrc/kernels/moe.hip). The reference has no MoE code; its anchor is BASELINE config 5 (Mixtral expert
+parallelism) on the reference's 8-GPU preset world (``/root/reference/ai_engine/deepspeed_launcher.py:383-406``)."""
 from __future__ import annotations
 
 import math

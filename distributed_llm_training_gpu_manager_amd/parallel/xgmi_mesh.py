@@ -1,5 +1,9 @@
 """Peer-write xGMI mesh all-gather (plan item 3) over HIP IPC symmetric buffers.
 
+The reference only asks DeepSpeed for bucketed, overlapped partition all-gathers
+(``/root/reference/ai_engine/deepspeed_launcher.py:133-141``: ``allgather_partitions``,
+``allgather_bucket_size``, ``overlap_comm``); this is the MI355X-native transport option for them.
+
 Every rank allocates one symmetric buffer (``cap`` bytes, its own hipMalloc), exports its IPC handle, and maps
 every peer's buffer (``hipIpcOpenMemHandle``; on one 8-GPU MI355X node every pair of GPUs has its own xGMI link).
 An all-gather is then:
