@@ -134,7 +134,21 @@ __device__ __forceinline__ float clip_coef(const float* stats, const float* inv_
   return coef;
 }
 
-template <typename GT, typename PT>
+template <bool NT, typename V>
+__device__ __forceinline__ V ld_stream(const V* a) {
+  if constexpr (NT) return __builtin_nontemporal_load(a);
+  return *a;
+}
+
+template <bool NT, typename V>
+__device__ __forceinline__ void st_stream(V* a, V v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, a);
+  else *a = v;
+}
+
+// NT: the optimizer state and the compute copy are streamed once per step -- non-temporal loads / stores keep
+// them from displacing anything in L2 / MALL (DLGM_ADAMW_NT=0: ordinary accesses)
+template <typename GT, typename PT, bool NT>
 __global__ __launch_bounds__(kThreads) void adamw_kernel(float* __restrict__ p, float* __restrict__ m,
                                                          float* __restrict__ v, const GT* __restrict__ g,
                                                          PT* __restrict__ p16, const float* __restrict__ stats,
@@ -148,9 +162,9 @@ __global__ __launch_bounds__(kThreads) void adamw_kernel(float* __restrict__ p, 
   const float inv_sqrt_bc2 = rsqrtf(h.bc2);
   const int64_t nv = n >> 2;
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kThreads) {
-    f32x4 pp = *reinterpret_cast<f32x4*>(p + i * 4);
-    f32x4 mm = *reinterpret_cast<f32x4*>(m + i * 4);
-    f32x4 vv = *reinterpret_cast<f32x4*>(v + i * 4);
+    f32x4 pp = ld_stream<NT>(reinterpret_cast<const f32x4*>(p + i * 4));
+    f32x4 mm = ld_stream<NT>(reinterpret_cast<const f32x4*>(m + i * 4));
+    f32x4 vv = ld_stream<NT>(reinterpret_cast<const f32x4*>(v + i * 4));
     float gg[4];
     load4<GT>(g + i * 4, gg);
 #pragma unroll
@@ -161,10 +175,10 @@ __global__ __launch_bounds__(kThreads) void adamw_kernel(float* __restrict__ p, 
       const float denom = sqrtf(vv[j]) * inv_sqrt_bc2 + h.eps;
       pp[j] = pp[j] * decay - step_size * mm[j] / denom;
     }
-    *reinterpret_cast<f32x4*>(p + i * 4) = pp;
-    *reinterpret_cast<f32x4*>(m + i * 4) = mm;
-    *reinterpret_cast<f32x4*>(v + i * 4) = vv;
-    if (p16) *reinterpret_cast<vec4_t<PT>*>(p16 + i * 4) = __builtin_convertvector(pp, vec4_t<PT>);
+    st_stream<NT>(reinterpret_cast<f32x4*>(p + i * 4), pp);
+    st_stream<NT>(reinterpret_cast<f32x4*>(m + i * 4), mm);
+    st_stream<NT>(reinterpret_cast<f32x4*>(v + i * 4), vv);
+    if (p16) st_stream<NT>(reinterpret_cast<vec4_t<PT>*>(p16 + i * 4), __builtin_convertvector(pp, vec4_t<PT>));
   }
   if (blockIdx.x == 0)
     for (int64_t i = nv * 4 + threadIdx.x; i < n; i += kThreads) {
@@ -302,14 +316,24 @@ void dlgm_adamw_step_(at::Tensor p, at::Tensor m, at::Tensor v, const at::Tensor
   // the compute copy's dtype selects the instantiation (bf16 unless the engine runs the fp16 path)
   DLGM_DISPATCH_16(has16 ? p16->scalar_type() : at::kBFloat16, PT, {
     PT* p16p = has16 ? reinterpret_cast<PT*>(p16->data_ptr()) : nullptr;
-    if (g.scalar_type() == at::kFloat)
-      adamw_kernel<float, PT><<<grid, kThreads, 0, stream>>>(p.data_ptr<float>(), m.data_ptr<float>(),
-                                                             v.data_ptr<float>(), g.data_ptr<float>(), p16p, sp, inv, n,
-                                                             h);
-    else
-      DLGM_DISPATCH_16(g.scalar_type(), GT, adamw_kernel<GT, PT><<<grid, kThreads, 0, stream>>>(
+    static const bool nt = [] {
+      const char* e = std::getenv("DLGM_ADAMW_NT");
+      return !(e != nullptr && e[0] == '0');
+    }();
+    if (g.scalar_type() == at::kFloat) {
+      if (nt)
+        adamw_kernel<float, PT, true><<<grid, kThreads, 0, stream>>>(p.data_ptr<float>(), m.data_ptr<float>(),
+                                                                     v.data_ptr<float>(), g.data_ptr<float>(), p16p,
+                                                                     sp, inv, n, h);
+      else
+        adamw_kernel<float, PT, false><<<grid, kThreads, 0, stream>>>(p.data_ptr<float>(), m.data_ptr<float>(),
+                                                                      v.data_ptr<float>(), g.data_ptr<float>(), p16p,
+                                                                      sp, inv, n, h);
+    } else {
+      DLGM_DISPATCH_16(g.scalar_type(), GT, adamw_kernel<GT, PT, false><<<grid, kThreads, 0, stream>>>(
                                                 p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
                                                 reinterpret_cast<const GT*>(g.data_ptr()), p16p, sp, inv, n, h));
+    }
   });
   DLGM_CHECK_HIP(hipGetLastError());
 }
