@@ -245,6 +245,7 @@ def main() -> int:
                 "model_tflops_per_gpu": round(tflops_gpu, 1),
                 "mfu_vs_2.5PF_dense_bf16": round(tflops_gpu / 2500.0, 4),
                 "final_loss": round(loss, 4),
+                "final_grad_norm": round(float(m["grad_norm"]), 4),
                 "init_s": round(init_s, 1),
                 "params": eng.num_params(),
                 "zero3_allgathers_per_step": eng.live_plan.gathers_per_step(args.ga),

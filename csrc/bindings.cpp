@@ -73,7 +73,7 @@ int64_t dlgm_gemm_lt_version();
 // gemm_mfma.hip
 void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bool accumulate,
                     const c10::optional<at::Tensor>& offsets, int64_t mode, int64_t M, int64_t N, int64_t K,
-                    int64_t G, int64_t b_gstride);
+                    int64_t G, int64_t b_gstride, const c10::optional<at::Tensor>& stats_part);
 void dlgm_gemm_mfma_seg(at::Tensor out, const std::vector<at::Tensor>& a, const std::vector<at::Tensor>& b,
                         const at::Tensor& offsets, bool accumulate, bool kmajor);
 
@@ -118,7 +118,7 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("ipc_open(Tensor handle) -> int", &dlgm_ipc_open);
   m.def("ipc_close(int ptr) -> ()", &dlgm_ipc_close);
   m.def("mesh_push(Tensor src, Tensor peers, int dst_off, int cap) -> ()");
-  m.def("gemm_mfma(Tensor(a!) out, Tensor a, Tensor b, bool accumulate, Tensor? offsets, int mode, int M, int N, int K, int G, int b_gstride) -> ()");
+  m.def("gemm_mfma(Tensor(a!) out, Tensor a, Tensor b, bool accumulate, Tensor? offsets, int mode, int M, int N, int K, int G, int b_gstride, Tensor(b!)? stats_part=None) -> ()");
   m.def("gemm_mfma_seg(Tensor(a!) out, Tensor[] a, Tensor[] b, Tensor offsets, bool accumulate, bool kmajor=False) -> ()");
 }
 

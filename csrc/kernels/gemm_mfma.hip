@@ -66,6 +66,8 @@ struct GemmArgs {
   int splitk;          // grouped-M split-K: each tile's K range in this many parts, fp32 partials
   int64_t c_sstride;   // elements between the partial slices of C (split-K)
   int nreal;           // grouped-K with the chunk remap: real blocks (the grid is rounded up to 8 * kChunk)
+  float* stats_part;   // grouped-K fp32 epilogues: per-tile (sum of squares of the finite, #non-finite) of the
+                       // FINAL C values, at [2 * tile] (deterministic: reduced later in a fixed order)
 };
 
 int env_flag(const char* name) {
@@ -362,7 +364,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
   const int nk = MODE == kGroupKSeg ? seg_cum[kMaxSeg] : (k_hi - k_lo + BK - 1) / BK;
   // an empty reduction that accumulates leaves C as it is: skip the read-modify-write of the tile (the MoE
   // capacity layout's overflow dW launches cover every expert and usually find no rows at all)
-  if (EPI == kAccF32 && nk <= 0) return;
+  if (EPI == kAccF32 && nk <= 0 && p.stats_part == nullptr) return;  // (with stats: count the old values)
   // partial tiles: K (grouped-K group ends), M rows (K-contiguous A: grouped-M group ends / M % 256 != 0)
   constexpr bool PK = MODE == kGroupK || MODE == kGroupKSeg, PM = AK;
   if (nk > 0) {
@@ -486,6 +488,16 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
 
   // ---- epilogue: lane holds C[m][n .. n+3] (m = column of D^T, n = 4 rows of D^T)
   const int i = lane & 15, g = lane >> 4;
+  float st_ss = 0.f, st_bad = 0.f;  // gradient statistics of the stored values (grouped-K, p.stats_part)
+  auto tally = [&](const f32x4& v) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool fin = __builtin_isfinite(v[j]);
+      st_bad += fin ? 0.f : 1.f;
+      st_ss += fin ? v[j] * v[j] : 0.f;
+    }
+  };
+  constexpr bool KSTATS = (MODE == kGroupK || MODE == kGroupKSeg) && EPI != kStoreBf16;
 #pragma unroll
   for (int mi = 0; mi < 8; ++mi) {
     const int mrow = wr * 128 + 16 * mi + i;  // row within the block tile
@@ -497,8 +509,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
       for (int ni = 0; ni < 4; ++ni)
         old[ni] = *reinterpret_cast<const f32x4*>(C + (m * p.ldc + n0 + wc * 64 + 16 * ni + 4 * g) * 4);
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
-        *reinterpret_cast<f32x4*>(C + (m * p.ldc + n0 + wc * 64 + 16 * ni + 4 * g) * 4) = old[ni] + acc[mi][ni];
+      for (int ni = 0; ni < 4; ++ni) {
+        const f32x4 nv = old[ni] + acc[mi][ni];
+        *reinterpret_cast<f32x4*>(C + (m * p.ldc + n0 + wc * 64 + 16 * ni + 4 * g) * 4) = nv;
+        if (KSTATS) tally(nv);
+      }
       continue;
     }
 #pragma unroll
@@ -509,6 +524,28 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
         *reinterpret_cast<bf16x4*>(C + (m * p.ldc + n) * 2) = v;
       } else {
         *reinterpret_cast<f32x4*>(C + (m * p.ldc + n) * 4) = acc[mi][ni];
+        if (KSTATS) tally(acc[mi][ni]);
+      }
+    }
+  }
+  if constexpr (KSTATS) {
+    if (p.stats_part != nullptr) {  // block reduce in LDS (the main loop is over), one float2 per tile
+      __syncthreads();
+      float* red = reinterpret_cast<float*>(smem);
+      const float a = wave_sum(st_ss), b = wave_sum(st_bad);
+      if (lane == 0) {
+        red[2 * w] = a;
+        red[2 * w + 1] = b;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        float sa = 0.f, sb = 0.f;
+        for (int q = 0; q < NTHR / 64; ++q) {
+          sa += red[2 * q];
+          sb += red[2 * q + 1];
+        }
+        p.stats_part[2 * id] = sa;
+        p.stats_part[2 * id + 1] = sb;
       }
     }
   }
@@ -552,7 +589,7 @@ void launch_epi(int epi, dim3 grid, hipStream_t st, const GemmArgs& a) {
 // b_gstride elements per group; mode 2 grouped-K: offsets split the K rows, out is [G, M, N].
 void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bool accumulate,
                     const c10::optional<at::Tensor>& offsets, int64_t mode, int64_t M, int64_t N, int64_t K,
-                    int64_t G, int64_t b_gstride) {
+                    int64_t G, int64_t b_gstride, const c10::optional<at::Tensor>& stats_part) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda() && out.is_cuda(), "gemm_mfma: GPU tensors");
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16, "gemm_mfma: bf16 operands");
   TORCH_CHECK(a.dim() == 2 && b.dim() >= 2 && out.dim() >= 2, "gemm_mfma: 2-D operand views");
@@ -611,6 +648,8 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
     p.ldc = N;
     p.c_sstride = M * N;
   }
+  TORCH_CHECK(!(stats_part.has_value() && stats_part->defined()) || mode == kGroupK,
+              "gemm_mfma: stats_part is a grouped-K epilogue");
   int64_t nblk;
   if (mode == kDense) {
     nblk = (int64_t)p.tiles_m * p.tiles_n;
@@ -624,6 +663,12 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
     } else {
       nblk = G * (int64_t)p.tiles_m * p.tiles_n;
       p.nreal = (int)nblk;
+      if (stats_part.has_value() && stats_part->defined()) {
+        TORCH_CHECK(mode == kGroupK && out32 && stats_part->is_cuda() && stats_part->scalar_type() == at::kFloat &&
+                        stats_part->is_contiguous() && stats_part->numel() == 2 * nblk,
+                    "gemm_mfma: stats_part must be fp32 [2 * G * tiles] for a grouped-K fp32 launch");
+        p.stats_part = stats_part->data_ptr<float>();
+      }
       if (p.chunk) nblk = (nblk + 8 * kChunk - 1) / (8 * kChunk) * (8 * kChunk);
     }
   }

@@ -63,6 +63,9 @@ class StepContext:
     # units may keep weight-gradient operands across the step's micro-batches and run ONE GEMM with the
     # micro-batches concatenated along K at the last one (their gradients go straight to fp32 targets)
     defer_wgrad: bool = False
+    # last micro-batch, single rank: fp32 [2] the units add [sum g^2, #non-finite] of each expert weight's FINAL
+    # gradient to (fused into its dW GEMM), counting the weights in aux["expert_stats_weights"]
+    expert_stats: Optional[torch.Tensor] = None
     # fp16 path: the dynamic loss scale as a device word (multiplied into the loss gradient on the device)
     loss_scale: Optional[torch.Tensor] = None
 

@@ -27,7 +27,7 @@ the expert-data-parallel group only).
 """
 from __future__ import annotations
 
-from typing import Any, List, Tuple
+from typing import Any, List, Optional, Tuple
 
 import torch
 
@@ -243,10 +243,12 @@ class MixtralBlock(LlamaBlock):
                 self._wstash.append(item)
                 self._wbytes += sum(t.numel() * t.element_size() for t in item[:4])
                 if ctx.last_micro or self._wbytes > getattr(ctx, "defer_budget_bytes", 48 << 30):
-                    self._flush_wgrad_grouped(g)
+                    self._flush_wgrad_grouped(g, ctx)
                 return dx
-            gm.grouped_wgrad(g["w_down"], dy, a_all, offs, acc)
-            gm.grouped_wgrad(g["w_gate_up"], dgu_all, x, offs, acc)
+            xs = self._final_stats(ctx)
+            gm.grouped_wgrad(g["w_down"], dy, a_all, offs, acc, stats=xs)
+            gm.grouped_wgrad(g["w_gate_up"], dgu_all, x, offs, acc, stats=xs)
+            self._count_stats(ctx, xs, 2)
             return dx
         counts = dctx.counts()
         if ctx is not None and ctx.defer_wgrad:
@@ -337,7 +339,17 @@ class MixtralBlock(LlamaBlock):
             del dgue, xe
         self._wstash, self._wflushed, self._wbytes = [], True, 0
 
-    def _flush_wgrad_grouped(self, g: Params) -> None:
+    @staticmethod
+    def _final_stats(ctx) -> Optional[torch.Tensor]:
+        """The engine's fused expert-statistics accumulator when this launch stores the step's final dW."""
+        return ctx.expert_stats if ctx is not None and ctx.last_micro else None
+
+    @staticmethod
+    def _count_stats(ctx, xs, n: int) -> None:
+        if xs is not None:
+            ctx.aux["expert_stats_weights"] = ctx.aux.get("expert_stats_weights", 0) + n
+
+    def _flush_wgrad_grouped(self, g: Params, ctx=None) -> None:
         """Deferred expert dW with device offsets: ONE segmented grouped GEMM per weight reduces each expert over
         its rows of every stashed micro-batch (segment = micro-batch, its offsets row = that micro-batch's
         routing; no host read, no concatenation of the rows)."""
@@ -347,12 +359,15 @@ class MixtralBlock(LlamaBlock):
             part = stash[i:i + gm.MAX_SEGMENTS]
             offs = torch.stack([t[4] for t in part])  # [segments, experts + 1] int32, on the device
             if part[0][5]:
+                # the last launch over a weight stores its final gradient: tally the statistics there
+                xs = self._final_stats(ctx) if i + gm.MAX_SEGMENTS >= len(stash) else None
                 src, poff = pad_plan_multi(offs, sum(int(t[0].shape[0]) for t in part))
                 for wname, ia, ib in (("w_down", 0, 1), ("w_gate_up", 2, 3)):
                     at_ = transpose_multi([t[ia] for t in part], src)
                     bt_ = transpose_multi([t[ib] for t in part], src)
-                    gm.grouped_wgrad(g[wname], at_, bt_, poff, acc or i > 0, kmajor=True)
+                    gm.grouped_wgrad(g[wname], at_, bt_, poff, acc or i > 0, kmajor=True, stats=xs)
                     del at_, bt_
+                self._count_stats(ctx, xs, 2)
                 continue
             gm.grouped_wgrad_segments(g["w_down"], [t[0] for t in part], [t[1] for t in part], offs, acc or i > 0)
             gm.grouped_wgrad_segments(g["w_gate_up"], [t[2] for t in part], [t[3] for t in part], offs,

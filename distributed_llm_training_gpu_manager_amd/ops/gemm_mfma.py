@@ -120,16 +120,25 @@ def grouped_mm(x: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, transpos
 
 
 def grouped_wgrad(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, offsets: torch.Tensor,
-                  acc: bool = False, kmajor: bool = False) -> torch.Tensor:
+                  acc: bool = False, kmajor: bool = False, stats: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out[e] (+)= a[rows of e]^T @ b[rows of e]: a [R, M], b [R, N] row-major (token rows), out [G, M, N].
     kmajor: a [M, P] and b [N, P] come transposed (K contiguous) with every group's column range a whole number
-    of 64-wide tiles, zero padded (ops.moe.pad_plan_multi + ops.gemm.transpose_multi)."""
+    of 64-wide tiles, zero padded (ops.moe.pad_plan_multi + ops.gemm.transpose_multi).
+    stats: fp32 [>= 2] += [sum of squares of the finite, #non-finite] over the stored out (fp32 out only): the
+    native launch tallies them in its epilogue (one partial per tile, summed here in a fixed order), so the
+    optimizer's gradient statistics need not re-read the expert gradients (ops.grad_stats semantics)."""
     G, M, N = out.shape
     if use_native(out):
+        part = None
+        if stats is not None:
+            assert out.dtype == torch.float32, "grouped_wgrad: fused statistics need an fp32 out"
+            part = torch.empty(2 * G * ((M + 255) // 256) * (N // 256), dtype=torch.float32, device=out.device)
         if kmajor:
-            hip_ops().gemm_mfma(out, a, b.t(), acc, offsets, GROUP_K, M, N, a.shape[1], G, 0)
+            hip_ops().gemm_mfma(out, a, b.t(), acc, offsets, GROUP_K, M, N, a.shape[1], G, 0, part)
         else:
-            hip_ops().gemm_mfma(out, a.t(), b, acc, offsets, GROUP_K, M, N, a.shape[0], G, 0)
+            hip_ops().gemm_mfma(out, a.t(), b, acc, offsets, GROUP_K, M, N, a.shape[0], G, 0, part)
+        if part is not None:
+            stats[:2] += part.view(-1, 2).sum(0)
         return out
     offs = offsets.tolist()
     for e in range(G):
@@ -142,6 +151,11 @@ def grouped_wgrad(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, offsets: 
             out[e].add_(r.to(out.dtype))
         else:
             out[e].copy_(r.to(out.dtype))
+    if stats is not None:
+        o = out.float()
+        fin = torch.isfinite(o)
+        stats[0] += torch.where(fin, o, torch.zeros_like(o)).square().sum()
+        stats[1] += (~fin).sum().to(stats.dtype)
     return out
 
 

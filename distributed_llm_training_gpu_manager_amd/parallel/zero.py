@@ -117,6 +117,11 @@ class EngineConfig:
     # when grad_accum > 1. Stashed operands are capped by defer_wgrad_budget_gb (flushed early above it).
     defer_expert_wgrad: Any = "auto"
     defer_wgrad_budget_gb: float = 48.0
+    # the expert groups' gradient statistics (sum of squares, #non-finite) tallied by the grouped dW GEMM's
+    # epilogue at the last micro-batch instead of a separate pass over the expert gradients (single rank:
+    # the stored gradient is then final); falls back to ops.grad_stats whenever a weight was not covered.
+    # DLGM_FUSED_XSTATS=1 turns it on (A/B; off until measured on the GPU)
+    fused_expert_grad_stats: bool = os.environ.get("DLGM_FUSED_XSTATS", "0") != "0"
     nvme_path: Optional[str] = None
     # ZeRO-2/3 gradients: True = accumulate fp32 locally and reduce-scatter once per optimizer step;
     # False = reduce-scatter every micro-batch (DeepSpeed); "hbm" = True when GA > 1 and the full fp32
@@ -317,6 +322,14 @@ class ZeroEngine:
             fg.gcomm = self.gather_comm if kind != "expert" else comm_g
             self.groups.append(fg)
         self.has_experts = any(g.kind == "expert" for g in self.groups)
+        # fused expert gradient statistics: only where the gradient the dW epilogue stores is the final one
+        # (no reduction, no EP rescale, no post-scale after it)
+        self._xstats_weights = sum(len(g.specs) for g in self.groups if g.kind == "expert")
+        self._xstats = None
+        self._xstats_ok = False
+        if (self.has_experts and cfg.fused_expert_grad_stats and self.W == 1 and self.ep_size == 1
+                and (self.ep_comm is None or self.ep_comm.world == 1) and not cfg.prescale_gradients):
+            self._xstats = torch.zeros(2, dtype=torch.float32, device=self.device)
         soff = foff = 0
         for g in self.groups:
             g.shard_off, g.full_off = soff, foff
@@ -838,6 +851,9 @@ class ZeroEngine:
         ctx.defer_wgrad = bool((dw == "auto" and self.cfg.grad_accum > 1) or dw is True) and all(
             self._direct_target(g) is not None for g in self.groups if g.kind == "expert")
         ctx.defer_budget_bytes = int(self.cfg.defer_wgrad_budget_gb * (1 << 30))
+        if last and self._xstats is not None:
+            self._xstats.zero_()
+            ctx.expert_stats = self._xstats  # units add each expert weight's final gradient statistics
         n = len(self.stages)
         saved: List[Any] = [None] * n
         x: Any = None
@@ -924,6 +940,9 @@ class ZeroEngine:
         if self.stage == 3 and last:
             self._live.clear()  # nothing outlives the step: the optimizer changes the parameters
         self.last_aux = ctx.aux
+        if last:  # every expert weight tallied by its final dW launch -> the optimizer skips their re-read
+            self._xstats_ok = (self._xstats is not None
+                               and ctx.aux.get("expert_stats_weights", 0) == self._xstats_weights)
         return loss
 
     def sync_params_from_master(self) -> None:
@@ -957,7 +976,11 @@ class ZeroEngine:
             exp = torch.zeros(2, dtype=torch.float32, device=self.device)
             ops.grad_stats([sl(g) for g in self.groups if g.kind != "expert" and g.P > 1], dense)
             ops.grad_stats([sl(g) for g in self.groups if g.kind != "expert" and g.P == 1], rep)
-            ops.grad_stats([sl(g) for g in self.groups if g.kind == "expert"], exp)
+            if self._xstats_ok:
+                exp.copy_(self._xstats)
+            else:
+                ops.grad_stats([sl(g) for g in self.groups if g.kind == "expert"], exp)
+            self._xstats_ok = False
             dense[2].fill_(self.host_flag)
             if any(g.P > 1 and g.kind != "expert" for g in self.groups):
                 self.comm.all_reduce(dense, async_op=False).wait()

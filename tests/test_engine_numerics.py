@@ -331,7 +331,7 @@ def test_mixtral_grouped_deferred_wgrad_matches_per_micro_batch_cpu(monkeypatch,
         eng = ZeroEngine(mc, ec, torch.device("cpu"))
         flushed = []
         monkeypatch.setattr(MixtralBlock, "_flush_wgrad_grouped",
-                            lambda self, gg: (flushed.append(len(self._wstash)), orig(self, gg))[1])
+                            lambda self, gg, ctx=None: (flushed.append(len(self._wstash)), orig(self, gg, ctx))[1])
         for i, t in enumerate(data):
             eng.micro_step(t[:, :-1], t[:, 1:], first=i == 0, last=i == 2)
         assert (flushed and flushed[0] == 3) if dw else not flushed
@@ -339,3 +339,34 @@ def test_mixtral_grouped_deferred_wgrad_matches_per_micro_batch_cpu(monkeypatch,
     for k, v in grads[False].items():
         err = float((grads[True][k] - v).abs().max() / v.abs().max().clamp_min(1e-8))
         assert err < 1e-2, (k, err)
+
+
+@pytest.mark.parametrize("ga,kmajor", [(1, True), (3, True), (3, False)])
+def test_mixtral_fused_expert_grad_stats_match_grad_stats_cpu(monkeypatch, ga, kmajor):
+    """The expert gradients' statistics tallied by the last grouped dW launch of the step (non-deferred at
+    GA 1, the K-major deferred flush at GA 3) equal ops.grad_stats over the expert groups; the token-major
+    segmented flush does not tally and falls back to the separate pass."""
+    from distributed_llm_training_gpu_manager_amd.models.mixtral import MixtralBlock
+    from distributed_llm_training_gpu_manager_amd.parallel.zero import EngineConfig, ZeroEngine
+    from distributed_llm_training_gpu_manager_amd.ops import gemm_mfma as gm
+    monkeypatch.setattr(gm, "CAPACITY", False)
+    monkeypatch.setattr(gm, "KMAJOR_DW", kmajor)
+    monkeypatch.setattr(MixtralBlock, "_grouped", lambda self, x, wgrad=False: True)
+    mc = get_config("mixtral-tiny")
+    g = torch.Generator().manual_seed(5)
+    data = [torch.randint(0, mc.vocab_size, (2, 33), generator=g) for _ in range(ga)]
+    ec = EngineConfig(zero_stage=3, micro_batch_size=2, seq_len=32, grad_accum=ga, lr=1e-3, scheduler="constant",
+                      init_device="cpu", fused_expert_grad_stats=True)
+    eng = ZeroEngine(mc, ec, torch.device("cpu"))
+    for i, t in enumerate(data):
+        eng.micro_step(t[:, :-1], t[:, 1:], first=i == 0, last=i == ga - 1)
+    fused = eng._xstats_ok
+    assert fused == (ga == 1 or kmajor)
+    eng._global_grad_stats()
+    st_fused = eng.stats[:2].clone()
+    eng._xstats_ok = False
+    eng._global_grad_stats()
+    st_ref = eng.stats[:2].clone()
+    assert float(st_ref[0]) > 0 and float(st_ref[1]) == 0
+    assert abs(float(st_fused[0]) - float(st_ref[0])) <= 1e-5 * float(st_ref[0])
+    assert float(st_fused[1]) == 0

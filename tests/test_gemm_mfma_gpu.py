@@ -129,6 +129,46 @@ def test_grouped_weight_gradient_uneven_and_empty_groups():
         lo += n
 
 
+def _stats_ref(t):
+    fin = torch.isfinite(t)
+    return float(torch.where(fin, t, torch.zeros_like(t)).double().square().sum()), float((~fin).sum())
+
+
+@pytest.mark.parametrize("acc", [False, True])
+@pytest.mark.parametrize("kmajor", [False, True])
+def test_grouped_weight_gradient_fused_statistics(acc, kmajor):
+    """The grouped-K epilogue's per-tile statistics of the stored gradient (sum of squares of the finite, count of
+    the non-finite) summed = the same statistics of the whole output: uneven / empty groups, a partial M tile (K-major),
+    token-major and K-major operands (spare blocks of the chunked XCD remap must not write partials), a
+    non-finite accumulated value counted once."""
+    g = torch.Generator(device=dev).manual_seed(11)
+    sizes = [192, 0, 704, 64, 64] if kmajor else [130, 0, 700, 1, 64]
+    R, M, N, G = sum(sizes), 384 if kmajor else 512, 512, len(sizes)  # partial M tile: K-contiguous rows only
+    offs = torch.tensor([0] + list(torch.tensor(sizes).cumsum(0)), dtype=torch.int32, device=dev)
+    dy = torch.randn(R, M, device=dev, generator=g).to(torch.bfloat16)
+    x = torch.randn(R, N, device=dev, generator=g).to(torch.bfloat16)
+    out = torch.randn(G, M, N, device=dev, generator=g) if acc else torch.full((G, M, N), 3.0, device=dev)
+    if acc:
+        out[1, 5, 7] = float("inf")  # empty group: the old value is still counted
+        out[2, 300, 9] = float("nan")
+    ref = out.clone() if acc else torch.zeros_like(out)
+    lo = 0
+    for e, n in enumerate(sizes):
+        ref[e] += dy[lo:lo + n].float().t() @ x[lo:lo + n].float()
+        lo += n
+    st = torch.tensor([1.0, 0.0], device=dev)  # accumulated into, not overwritten
+    if kmajor:
+        gm.grouped_wgrad(out, dy.t().contiguous(), x.t().contiguous(), offs, acc=acc, kmajor=True, stats=st)
+    else:
+        gm.grouped_wgrad(out, dy, x, offs, acc=acc, stats=st)
+    fin = torch.isfinite(ref)
+    assert torch.equal(fin, torch.isfinite(out))
+    assert _rel(torch.where(fin, out, 0.0), torch.where(fin, ref, 0.0)) < 1e-5
+    ss, bad = _stats_ref(out)
+    assert float(st[1]) == bad == (2.0 if acc else 0.0)
+    assert abs(float(st[0]) - 1.0 - ss) <= 1e-5 * ss
+
+
 @pytest.mark.parametrize("nseg", [1, 3, 8])
 def test_grouped_weight_gradient_over_segments(nseg):
     """Segmented grouped-K (the deferred expert dW over a step's micro-batches): every group reduces over its
