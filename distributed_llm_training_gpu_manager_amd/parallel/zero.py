@@ -120,8 +120,9 @@ class EngineConfig:
     # the expert groups' gradient statistics (sum of squares, #non-finite) tallied by the grouped dW GEMM's
     # epilogue at the last micro-batch instead of a separate pass over the expert gradients (single rank:
     # the stored gradient is then final); falls back to ops.grad_stats whenever a weight was not covered.
-    # DLGM_FUSED_XSTATS=1 turns it on (A/B; off until measured on the GPU)
-    fused_expert_grad_stats: bool = os.environ.get("DLGM_FUSED_XSTATS", "0") != "0"
+    # DLGM_FUSED_XSTATS=0 turns it off (A/B on Mixtral 2-layer: 133.2k -> 136.3k tokens/s, identical grad norm;
+    # profiles/fused_expert_stats_ab_r03.json)
+    fused_expert_grad_stats: bool = os.environ.get("DLGM_FUSED_XSTATS", "1") != "0"
     nvme_path: Optional[str] = None
     # ZeRO-2/3 gradients: True = accumulate fp32 locally and reduce-scatter once per optimizer step;
     # False = reduce-scatter every micro-batch (DeepSpeed); "hbm" = True when GA > 1 and the full fp32
