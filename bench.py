@@ -113,6 +113,11 @@ def main() -> int:
     ap.add_argument("--comm-sweep", default="auto", choices=["auto", "on", "off"],
                     help="after the timed steps, measure RCCL busbw over xGMI (auto: when WORLD_SIZE > 1)")
     ap.add_argument("--comm-sweep-timeout", type=float, default=120.0)
+    ap.add_argument("--mesh-sweep", default="auto", choices=["auto", "on", "off"],
+                    help="after the result line, measure the device-driven xGMI mesh all-gather / reduce-scatter in a "
+                         "child process per rank (auto: on the GPU when WORLD_SIZE > 1)")
+    ap.add_argument("--xgmi-mesh", default="off", choices=["on", "off"],
+                    help="run the ZeRO collectives over the device-driven xGMI mesh instead of RCCL rings")
     ap.add_argument("--defer-expert-wgrad", default="auto", choices=["auto", "on", "off"],
                     help="MoE: expert dW once per step over the concatenated micro-batches")
     ap.add_argument("--telemetry-interval", type=float, default=2.0)
@@ -148,7 +153,7 @@ def main() -> int:
                         activation_checkpointing=args.ckpt, max_live_parameters=_knob(args.live_params),
                         max_reuse_distance=_knob(args.reuse_distance),
                         local_grad_accum={"on": True, "off": False}.get(args.local_grads, args.local_grads),
-                        hip_graphs=args.hip_graphs, fp16=args.dtype == "fp16",
+                        hip_graphs=args.hip_graphs, fp16=args.dtype == "fp16", xgmi_mesh=args.xgmi_mesh,
                         defer_expert_wgrad={"on": True, "off": False}.get(args.defer_expert_wgrad, "auto"))
     t0 = time.time()
     eng = ZeroEngine(mcfg, ecfg, env.device, comm)
@@ -239,6 +244,7 @@ def main() -> int:
                 "grad_reduce_scatter": ("none (single rank)" if eng.W == 1 else
                                         "per_step" if eng.local_grads else "per_micro_batch"),
                 "hip_graphs": eng._graph is not None,
+                "transport": ("xgmi_mesh" if eng.mesh is not None else "rccl") if eng.W > 1 else "none",
             },
             "extra": {
                 "tokens_per_sec_per_gpu": round(tps / env.world, 2),
@@ -279,11 +285,46 @@ def main() -> int:
         dog.cancel()
         if out is not None:
             out["extra"]["comm_busbw"] = rows
+    mesh_sweep = args.mesh_sweep == "on" or (args.mesh_sweep == "auto" and env.world > 1
+                                               and env.device.type == "cuda")
+    port = None
+    if mesh_sweep and env.world > 1:  # agree on the child job's rendezvous port while the group still exists
+        pt = torch.tensor([_free_port() if env.rank == 0 else 0], dtype=torch.int64, device=env.device)
+        torch.distributed.broadcast(pt, src=0)
+        port = int(pt.item())
     if out is not None:
         print(json.dumps(out), flush=True)
+    for m_ in (eng.mesh, eng.ep_mesh):
+        if m_ is not None:
+            m_.close()  # collective: every rank unmaps its peers' heaps before any heap is freed
     if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
+    if mesh_sweep:
+        _mesh_sweep_child(port, eng, args.comm_sweep_timeout + 60)
     return 0
+
+
+def _mesh_sweep_child(port, eng, timeout_s: float) -> None:
+    """The ipc_mesh_* bus-bandwidth rows in a child process per rank, after the result line is out (VERDICT r3:
+    a new transport must never share the measuring process). Its output goes to stderr; stdout keeps one line."""
+    import gc
+    import subprocess
+    eng.__dict__.clear()  # hand this rank's HBM back before the child maps its heaps
+    gc.collect()
+    if torch.cuda.is_available():
+        torch.cuda.empty_cache()
+    env = dict(os.environ)
+    # the child job hosts its own rendezvous store (rank 0 serves it on the agreed port): not torchrun's agent store
+    env.pop("TORCHELASTIC_USE_AGENT_STORE", None)
+    if port is not None:
+        env["MASTER_PORT"] = str(port)
+    if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
+        env.setdefault("DLGM_SWEEP_DIR", os.path.join(ROOT, "gpurun_out"))
+    try:
+        subprocess.run([sys.executable, os.path.join(ROOT, "tools", "mesh_sweep.py")], env=env, cwd=ROOT,
+                       stdout=sys.stderr, stderr=sys.stderr, timeout=timeout_s)
+    except Exception as e:  # noqa: BLE001 -- the result line is already out
+        print(f"[bench] mesh sweep: {type(e).__name__}: {e}", file=sys.stderr, flush=True)
 
 
 if __name__ == "__main__":

@@ -50,13 +50,9 @@ at::Tensor dlgm_moe_combine_fwd(const at::Tensor& y, const at::Tensor& pos, cons
 std::tuple<at::Tensor, at::Tensor> dlgm_moe_combine_bwd(const at::Tensor& dout, const at::Tensor& y,
                                                         const at::Tensor& pos, const at::Tensor& gates);
 std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_moe_permute(const at::Tensor& topi, int64_t n_experts);
-std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dlgm_moe_capacity_plan(const at::Tensor& offsets,
-                                                                                   int64_t rows, int64_t capacity);
 std::tuple<at::Tensor, at::Tensor> dlgm_moe_pad_plan(const at::Tensor& offsets, int64_t padded_rows, int64_t align);
 std::tuple<at::Tensor, at::Tensor> dlgm_moe_pad_plan_multi(const at::Tensor& offsets, int64_t padded_rows,
                                                             int64_t align);
-at::Tensor dlgm_gather_rows(const at::Tensor& src, const at::Tensor& idx, const c10::optional<at::Tensor>& idx2,
-                            const c10::optional<at::Tensor>& nrows);
 // transpose.hip
 at::Tensor dlgm_transpose(const at::Tensor& x, const c10::optional<at::Tensor>& out,
                           const c10::optional<at::Tensor>& rows);
@@ -78,11 +74,31 @@ void dlgm_gemm_mfma_seg(at::Tensor out, const std::vector<at::Tensor>& a, const 
                         const at::Tensor& offsets, bool accumulate, bool kmajor);
 
 // xgmi_mesh.hip
-at::Tensor dlgm_ipc_alloc(int64_t nbytes);
+at::Tensor dlgm_ipc_alloc(int64_t nbytes, int64_t mode);
 at::Tensor dlgm_ipc_handle(const at::Tensor& buf);
 int64_t dlgm_ipc_open(const at::Tensor& handle);
 void dlgm_ipc_close(int64_t ptr);
-void dlgm_mesh_push(const at::Tensor& src, const at::Tensor& peers, int64_t dst_off, int64_t cap);
+int64_t dlgm_mesh_flag_bytes();
+int64_t dlgm_mesh_state_words();
+void dlgm_mesh_sync(at::Tensor state, const at::Tensor& peers, int64_t me, int64_t ch, int64_t inc, int64_t val,
+                    int64_t store_kind, int64_t wait_kind, int64_t lag, int64_t timeout);
+void dlgm_mesh_pull(at::Tensor out, const at::Tensor& peers, int64_t src_off, int64_t heap_bytes);
+void dlgm_mesh_rs_push(const at::Tensor& x, const at::Tensor& peers, at::Tensor state, int64_t me, int64_t ch,
+                       int64_t region_off, int64_t slot_bytes, int64_t rank_stride, int64_t slots,
+                       int64_t heap_bytes);
+void dlgm_mesh_rs_reduce(at::Tensor out, double scale, bool accumulate, const at::Tensor& peers, at::Tensor state,
+                         int64_t me, int64_t ch, int64_t region_off, int64_t slot_bytes, int64_t rank_stride,
+                         int64_t slots, int64_t heap_bytes);
+std::vector<int64_t> dlgm_mesh_plan_layout(int64_t W, int64_t E);
+void dlgm_mesh_ep_plan(const at::Tensor& offsets, at::Tensor plan, int64_t capacity, const at::Tensor& peers,
+                       at::Tensor state, int64_t me, int64_t ch, int64_t region_off, int64_t slot_bytes,
+                       int64_t slots, int64_t heap_bytes, int64_t timeout);
+void dlgm_mesh_push_rows(const at::Tensor& x, const at::Tensor& plan, bool combine, const at::Tensor& peers,
+                         at::Tensor state, int64_t me, int64_t ch, int64_t region_off, int64_t slot_bytes,
+                         int64_t hdr_bytes, int64_t slots, int64_t slot_rows, int64_t heap_bytes, int64_t n_experts);
+void dlgm_mesh_copy_rows(at::Tensor out, const c10::optional<at::Tensor>& nrows, const at::Tensor& peers,
+                         at::Tensor state, int64_t me, int64_t ch, int64_t region_off, int64_t slot_bytes,
+                         int64_t hdr_bytes, int64_t slots, int64_t heap_bytes);
 
 TORCH_LIBRARY(dlgm, m) {
   m.def("rmsnorm_fwd(Tensor x, Tensor? residual, Tensor w, float eps) -> (Tensor, Tensor, Tensor)");
@@ -100,11 +116,9 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("moe_combine_fwd(Tensor y, Tensor pos, Tensor? gates) -> Tensor");
   m.def("moe_combine_bwd(Tensor dout, Tensor y, Tensor pos, Tensor gates) -> (Tensor, Tensor)");
   m.def("moe_permute(Tensor topi, int n_experts) -> (Tensor, Tensor, Tensor)");
-  m.def("moe_capacity_plan(Tensor offsets, int rows, int capacity) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("moe_pad_plan(Tensor offsets, int padded_rows, int align) -> (Tensor, Tensor)");
   m.def("moe_pad_plan_multi(Tensor offsets, int padded_rows, int align) -> (Tensor, Tensor)");
   m.def("transpose_multi(Tensor[] xs, Tensor rows) -> Tensor");
-  m.def("gather_rows(Tensor src, Tensor idx, Tensor? idx2=None, Tensor? nrows=None) -> Tensor");
   m.def("transpose(Tensor x, Tensor(a!)? out=None, Tensor? rows=None) -> Tensor");
   m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, float softmax_scale, bool causal, Tensor? dqkv=None) -> (Tensor, Tensor, Tensor)");
   m.def("embedding_fwd(Tensor table, Tensor ids) -> Tensor");
@@ -113,11 +127,20 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("gemm_lt(Tensor(a!) out, Tensor a, Tensor b, float beta, int algo) -> int");
   m.def("gemm_lt_tune(Tensor out, Tensor a, Tensor b, float beta, int n_heuristic, bool all_algos, int reps) -> Tensor");
   m.def("gemm_lt_version() -> int", &dlgm_gemm_lt_version);
-  m.def("ipc_alloc(int nbytes) -> Tensor", &dlgm_ipc_alloc);
+  m.def("ipc_alloc(int nbytes, int mode=0) -> Tensor", &dlgm_ipc_alloc);
   m.def("ipc_handle(Tensor buf) -> Tensor", &dlgm_ipc_handle);
   m.def("ipc_open(Tensor handle) -> int", &dlgm_ipc_open);
   m.def("ipc_close(int ptr) -> ()", &dlgm_ipc_close);
-  m.def("mesh_push(Tensor src, Tensor peers, int dst_off, int cap) -> ()");
+  m.def("mesh_flag_bytes() -> int", &dlgm_mesh_flag_bytes);
+  m.def("mesh_state_words() -> int", &dlgm_mesh_state_words);
+  m.def("mesh_plan_layout(int W, int E) -> int[]", &dlgm_mesh_plan_layout);
+  m.def("mesh_sync(Tensor(a!) state, Tensor peers, int me, int ch, int inc, int val, int store_kind, int wait_kind, int lag, int timeout) -> ()");
+  m.def("mesh_pull(Tensor(a!) out, Tensor peers, int src_off, int heap_bytes) -> ()");
+  m.def("mesh_rs_push(Tensor x, Tensor peers, Tensor(a!) state, int me, int ch, int region_off, int slot_bytes, int rank_stride, int slots, int heap_bytes) -> ()");
+  m.def("mesh_rs_reduce(Tensor(a!) out, float scale, bool accumulate, Tensor peers, Tensor(b!) state, int me, int ch, int region_off, int slot_bytes, int rank_stride, int slots, int heap_bytes) -> ()");
+  m.def("mesh_ep_plan(Tensor offsets, Tensor(a!) plan, int capacity, Tensor peers, Tensor(b!) state, int me, int ch, int region_off, int slot_bytes, int slots, int heap_bytes, int timeout) -> ()");
+  m.def("mesh_push_rows(Tensor x, Tensor plan, bool combine, Tensor peers, Tensor(a!) state, int me, int ch, int region_off, int slot_bytes, int hdr_bytes, int slots, int slot_rows, int heap_bytes, int n_experts) -> ()");
+  m.def("mesh_copy_rows(Tensor(a!) out, Tensor? nrows, Tensor peers, Tensor(b!) state, int me, int ch, int region_off, int slot_bytes, int hdr_bytes, int slots, int heap_bytes) -> ()");
   m.def("gemm_mfma(Tensor(a!) out, Tensor a, Tensor b, bool accumulate, Tensor? offsets, int mode, int M, int N, int K, int G, int b_gstride, Tensor(b!)? stats_part=None) -> ()");
   m.def("gemm_mfma_seg(Tensor(a!) out, Tensor[] a, Tensor[] b, Tensor offsets, bool accumulate, bool kmajor=False) -> ()");
 }
@@ -139,8 +162,6 @@ TORCH_LIBRARY_IMPL(dlgm, CUDA, m) {
   m.impl("moe_combine_fwd", &dlgm_moe_combine_fwd);
   m.impl("moe_combine_bwd", &dlgm_moe_combine_bwd);
   m.impl("moe_permute", &dlgm_moe_permute);
-  m.impl("moe_capacity_plan", &dlgm_moe_capacity_plan);
-  m.impl("gather_rows", &dlgm_gather_rows);
   m.impl("moe_pad_plan", &dlgm_moe_pad_plan);
   m.impl("moe_pad_plan_multi", &dlgm_moe_pad_plan_multi);
   m.impl("transpose_multi", &dlgm_transpose_multi);
@@ -152,5 +173,11 @@ TORCH_LIBRARY_IMPL(dlgm, CUDA, m) {
   m.impl("gemm_lt_tune", &dlgm_gemm_lt_tune);
   m.impl("gemm_mfma", &dlgm_gemm_mfma);
   m.impl("gemm_mfma_seg", &dlgm_gemm_mfma_seg);
-  m.impl("mesh_push", &dlgm_mesh_push);
+  m.impl("mesh_sync", &dlgm_mesh_sync);
+  m.impl("mesh_pull", &dlgm_mesh_pull);
+  m.impl("mesh_rs_push", &dlgm_mesh_rs_push);
+  m.impl("mesh_rs_reduce", &dlgm_mesh_rs_reduce);
+  m.impl("mesh_ep_plan", &dlgm_mesh_ep_plan);
+  m.impl("mesh_push_rows", &dlgm_mesh_push_rows);
+  m.impl("mesh_copy_rows", &dlgm_mesh_copy_rows);
 }

@@ -61,8 +61,8 @@ struct GemmArgs {
   int M, N, K;                     // K: dense / grouped-M reduction length; M: rows for dense/grouped-K
   int G, mode;
   int tiles_n, tiles_m;
-  int qskip;  // skip the MFMAs of row quadrants wholly past the valid rows (DLGM_GEMM_QSKIP=0: A/B off)
-  int chunk;  // grouped-M: balanced remap over the real tiles (DLGM_GEMM_CHUNK_REMAP=0: contiguous over the grid)
+  int qskip;  // skip the MFMAs of row quadrants wholly past the valid rows (+0.5 % Mixtral, round 3)
+  int chunk;  // grouped-M: balanced remap over the real tiles (+0.7 % vs contiguous over the grid, round 3)
   int splitk;          // grouped-M split-K: each tile's K range in this many parts, fp32 partials
   int64_t c_sstride;   // elements between the partial slices of C (split-K)
   int nreal;           // grouped-K with the chunk remap: real blocks (the grid is rounded up to 8 * kChunk)
@@ -70,20 +70,6 @@ struct GemmArgs {
                        // FINAL C values, at [2 * tile] (deterministic: reduced later in a fixed order)
 };
 
-int env_flag(const char* name) {
-  const char* e = std::getenv(name);
-  return (e != nullptr && e[0] == '0') ? 0 : 1;
-}
-
-int qskip_env() {
-  static const int v = env_flag("DLGM_GEMM_QSKIP");
-  return v;
-}
-
-int chunk_env() {
-  static const int v = env_flag("DLGM_GEMM_CHUNK_REMAP");
-  return v;
-}
 
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -566,10 +552,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
-int splitk_env() {
-  static const int v = env_flag("DLGM_GEMM_SPLITK");
-  return v;
-}
 
 template <int MODE, bool AK, bool BKM>
 void launch_epi(int epi, dim3 grid, hipStream_t st, const GemmArgs& a) {
@@ -634,14 +616,14 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
   p.c_gstride = mode == kGroupK ? out.stride(0) : 0;
   p.tiles_n = (int)(N / BN);
   p.tiles_m = (int)((M + BM - 1) / BM);
-  p.qskip = qskip_env();
-  p.chunk = chunk_env();
+  p.qskip = 1;
+  p.chunk = 1;
   p.splitk = 1;
   // narrow grouped-M problems (<= 16 column tiles: the expert down projection and input gradients) fill only ~2.2
   // rounds of 256 CUs, so a third round runs ~20 % full: split the long K in two (fp32 partials + one reduce)
   at::Tensor part;
   at::Tensor out_final = out;
-  if (mode == kGroupM && !out32 && out.is_contiguous() && ldc == N && p.tiles_n <= 16 && K >= 16384 && splitk_env()) {
+  if (mode == kGroupM && !out32 && out.is_contiguous() && ldc == N && p.tiles_n <= 16 && K >= 16384) {
     p.splitk = 2;
     part = at::empty({p.splitk, M, N}, out.options().dtype(at::kFloat));
     p.c = part.data_ptr();
@@ -770,7 +752,7 @@ void dlgm_gemm_mfma_seg(at::Tensor out, const std::vector<at::Tensor>& a, const 
   int64_t nblk = G * (int64_t)p.tiles_m * p.tiles_n;
   if (nblk == 0) return;
   p.nreal = (int)nblk;
-  p.chunk = chunk_env();
+  p.chunk = 1;
   if (p.chunk) nblk = (nblk + 8 * kChunk - 1) / (8 * kChunk) * (8 * kChunk);
   if (kmajor)
     launch_epi<kGroupKSeg, true, true>(accumulate ? kAccF32 : kStoreF32, dim3((unsigned)nblk),

@@ -125,59 +125,14 @@ __global__ __launch_bounds__(kPermThreads) void moe_permute_kernel(const int64_t
   }
 }
 
-// Capacity plan over the expert-sorted rows (offsets [G + 1] splits R rows by expert). The "expanded" row space
-// is [G * C capacity rows: expert e's first C rows at e*C ..][R overflow rows: the rows past an expert's C-th, packed
-// expert by expert from G*C on]. Capacity rows past an expert's count are padding (exp_src = -1, gathered as zeros),
-// so the capacity region is a static [G, C, .] batch for the library GEMMs; the overflow region is a grouped
-// problem (ovf_offsets) whose used length (nrows - G*C) is known only on the device.
-// Every block rebuilds the (G <= 64) prefix tables in LDS; the rows are grid-strided.
-constexpr int kMaxCapGroups = 64;
-
-__global__ __launch_bounds__(256) void moe_capacity_plan_kernel(const int* __restrict__ offsets, int G, int64_t R,
-                                                                int C, int* __restrict__ exp_src,
-                                                                int64_t* __restrict__ row_map,
-                                                                int* __restrict__ ovf_offsets, int* __restrict__ nrows) {
-  __shared__ int s_off[kMaxCapGroups + 1], s_ovf[kMaxCapGroups + 1];
-  if (threadIdx.x == 0) {
-    int acc = 0;
-    for (int e = 0; e < G; ++e) {
-      s_off[e] = offsets[e];
-      s_ovf[e] = acc;
-      acc += max(0, offsets[e + 1] - offsets[e] - C);
-    }
-    s_off[G] = offsets[G];
-    s_ovf[G] = acc;
-  }
-  __syncthreads();
-  if (blockIdx.x == 0) {
-    if ((int)threadIdx.x <= G) ovf_offsets[threadIdx.x] = s_ovf[threadIdx.x];
-    if (threadIdx.x == 0) nrows[0] = G * C + s_ovf[G];
-  }
-  const int64_t gc = (int64_t)G * C, total = gc + R;
-  for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += (int64_t)gridDim.x * blockDim.x) {
-    int src = -1;
-    if (x < gc) {
-      const int e = (int)(x / C), r = (int)(x - (int64_t)e * C);
-      if (r < s_off[e + 1] - s_off[e]) src = s_off[e] + r;
-    } else {
-      const int o = (int)(x - gc);
-      if (o < s_ovf[G]) {
-        int e = 0;
-        while (s_ovf[e + 1] <= o) ++e;
-        src = s_off[e] + C + (o - s_ovf[e]);
-      }
-    }
-    exp_src[x] = src;
-    if (src >= 0) row_map[src] = x;
-  }
-}
+constexpr int kMaxGroups = 64;
 
 // Aligned re-layout of expert-sorted rows: expert e's rows start at padded row poff[e] (a multiple of `align`,
 // poff[e+1] - poff[e] = count rounded up to align). rows[p] = the sorted row at padded row p, or -1 (padding; also
 // every p past poff[G]). With it a transposed [D, P] image has every expert's reduction range on whole K tiles.
 __global__ __launch_bounds__(256) void moe_pad_plan_kernel(const int* __restrict__ offsets, int G, int64_t P,
                                                            int align, int* __restrict__ rows, int* __restrict__ poff) {
-  __shared__ int s_off[kMaxCapGroups + 1], s_pad[kMaxCapGroups + 1];
+  __shared__ int s_off[kMaxGroups + 1], s_pad[kMaxGroups + 1];
   if (threadIdx.x == 0) {
     int acc = 0;
     for (int e = 0; e < G; ++e) {
@@ -211,7 +166,7 @@ constexpr int kMaxSets = 8;
 __global__ __launch_bounds__(256) void moe_pad_plan_multi_kernel(const int* __restrict__ offsets, int S, int G,
                                                                  int64_t P, int align, int* __restrict__ rows,
                                                                  int* __restrict__ poff) {
-  __shared__ int s_off[kMaxSets][kMaxCapGroups + 1], s_cum[kMaxSets + 1][kMaxCapGroups], s_pad[kMaxCapGroups + 1];
+  __shared__ int s_off[kMaxSets][kMaxGroups + 1], s_cum[kMaxSets + 1][kMaxGroups], s_pad[kMaxGroups + 1];
   for (int i = threadIdx.x; i < S * (G + 1); i += blockDim.x) s_off[i / (G + 1)][i % (G + 1)] = offsets[i];
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -243,24 +198,6 @@ __global__ __launch_bounds__(256) void moe_pad_plan_multi_kernel(const int* __re
       }
     }
     rows[p] = src;
-  }
-}
-
-// out[r] = src[idx2 ? idx2[idx[r]] : idx[r]] for idx[r] >= 0, zeros for idx[r] < 0; rows at or past *nrows (when
-// given) are left untouched. One wave per row, 16 B per lane.
-template <typename E>
-__global__ __launch_bounds__(256) void gather_rows_kernel(const E* __restrict__ src, const int* __restrict__ idx,
-                                                          const int64_t* __restrict__ idx2, const int* __restrict__ nrows,
-                                                          E* __restrict__ out, int64_t M, int64_t D) {
-  const int lane = threadIdx.x & 63;
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= M || (nrows != nullptr && r >= (int64_t)nrows[0])) return;
-  int64_t s = idx[r];
-  if (s >= 0 && idx2 != nullptr) s = idx2[s];
-  for (int64_t c = lane * 8; c < D; c += 512) {
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (s >= 0) v = *reinterpret_cast<const uint4*>(src + s * D + c);
-    *reinterpret_cast<uint4*>(out + r * D + c) = v;
   }
 }
 
@@ -321,32 +258,11 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_moe_permute(const at::Tensor
   return {offsets, pos, src};
 }
 
-std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dlgm_moe_capacity_plan(const at::Tensor& offsets,
-                                                                                   int64_t rows, int64_t capacity) {
-  TORCH_CHECK(offsets.is_cuda() && offsets.scalar_type() == at::kInt && offsets.is_contiguous() && offsets.dim() == 1,
-              "moe_capacity_plan: offsets must be a contiguous int32 [G + 1] GPU tensor");
-  const int64_t G = offsets.numel() - 1;
-  TORCH_CHECK(G >= 1 && G <= kMaxCapGroups, "moe_capacity_plan: 1..64 groups");
-  TORCH_CHECK(capacity >= 1 && rows >= 0 && G * capacity + rows < (1ll << 31), "moe_capacity_plan: bad sizes");
-  const int64_t total = G * capacity + rows;
-  auto iopt = offsets.options();
-  auto exp_src = at::empty({total}, iopt);
-  auto row_map = at::empty({rows}, iopt.dtype(at::kLong));
-  auto ovf = at::empty({G + 1}, iopt);
-  auto nrows = at::empty({1}, iopt);
-  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 2048));
-  moe_capacity_plan_kernel<<<(unsigned)blocks, 256, 0, c10::hip::getCurrentHIPStream()>>>(
-      offsets.data_ptr<int>(), (int)G, rows, (int)capacity, exp_src.data_ptr<int>(), row_map.data_ptr<int64_t>(),
-      ovf.data_ptr<int>(), nrows.data_ptr<int>());
-  DLGM_CHECK_HIP(hipGetLastError());
-  return {exp_src, row_map, ovf, nrows};
-}
-
 std::tuple<at::Tensor, at::Tensor> dlgm_moe_pad_plan(const at::Tensor& offsets, int64_t padded_rows, int64_t align) {
   TORCH_CHECK(offsets.is_cuda() && offsets.scalar_type() == at::kInt && offsets.is_contiguous() && offsets.dim() == 1,
               "moe_pad_plan: offsets must be a contiguous int32 [G + 1] GPU tensor");
   const int64_t G = offsets.numel() - 1;
-  TORCH_CHECK(G >= 1 && G <= kMaxCapGroups && align >= 1 && padded_rows >= 0 && padded_rows < (1ll << 31),
+  TORCH_CHECK(G >= 1 && G <= kMaxGroups && align >= 1 && padded_rows >= 0 && padded_rows < (1ll << 31),
               "moe_pad_plan: 1..64 groups, align >= 1");
   auto rows = at::empty({padded_rows}, offsets.options());
   auto poff = at::empty({G + 1}, offsets.options());
@@ -362,7 +278,7 @@ std::tuple<at::Tensor, at::Tensor> dlgm_moe_pad_plan_multi(const at::Tensor& off
   TORCH_CHECK(offsets.is_cuda() && offsets.scalar_type() == at::kInt && offsets.is_contiguous() && offsets.dim() == 2,
               "moe_pad_plan_multi: offsets must be a contiguous int32 [S, G + 1] GPU tensor");
   const int64_t S = offsets.size(0), G = offsets.size(1) - 1;
-  TORCH_CHECK(S >= 1 && S <= kMaxSets && G >= 1 && G <= kMaxCapGroups && align >= 1 && padded_rows >= 0 &&
+  TORCH_CHECK(S >= 1 && S <= kMaxSets && G >= 1 && G <= kMaxGroups && align >= 1 && padded_rows >= 0 &&
                   padded_rows < (1ll << 31), "moe_pad_plan_multi: 1..8 sets, 1..64 groups, align >= 1");
   auto rows = at::empty({padded_rows}, offsets.options());
   auto poff = at::empty({G + 1}, offsets.options());
@@ -371,28 +287,6 @@ std::tuple<at::Tensor, at::Tensor> dlgm_moe_pad_plan_multi(const at::Tensor& off
       offsets.data_ptr<int>(), (int)S, (int)G, padded_rows, (int)align, rows.data_ptr<int>(), poff.data_ptr<int>());
   DLGM_CHECK_HIP(hipGetLastError());
   return {rows, poff};
-}
-
-at::Tensor dlgm_gather_rows(const at::Tensor& src, const at::Tensor& idx, const c10::optional<at::Tensor>& idx2,
-                            const c10::optional<at::Tensor>& nrows) {
-  TORCH_CHECK(src.is_cuda() && DLGM_IS16(src) && src.is_contiguous() && src.dim() == 2,
-              "gather_rows: src must be a contiguous [N, D] bf16/fp16 GPU tensor");
-  const int64_t D = src.size(1);
-  TORCH_CHECK(D % 8 == 0 && reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0, "gather_rows: 16-byte rows");
-  TORCH_CHECK(idx.scalar_type() == at::kInt && idx.is_contiguous() && idx.dim() == 1, "gather_rows: idx int32 [M]");
-  const bool has2 = idx2.has_value() && idx2->defined(), hasn = nrows.has_value() && nrows->defined();
-  if (has2) TORCH_CHECK(idx2->scalar_type() == at::kLong && idx2->is_contiguous(), "gather_rows: idx2 int64");
-  if (hasn) TORCH_CHECK(nrows->scalar_type() == at::kInt && nrows->numel() == 1, "gather_rows: nrows int32 [1]");
-  const int64_t M = idx.numel();
-  auto out = at::empty({M, D}, src.options());
-  if (M == 0) return out;
-  DLGM_DISPATCH_16(src.scalar_type(), E, {
-    gather_rows_kernel<E><<<(unsigned)((M + 3) / 4), 256, 0, c10::hip::getCurrentHIPStream()>>>(
-        reinterpret_cast<const E*>(src.data_ptr()), idx.data_ptr<int>(), has2 ? idx2->data_ptr<int64_t>() : nullptr,
-        hasn ? nrows->data_ptr<int>() : nullptr, reinterpret_cast<E*>(out.data_ptr()), M, D);
-  });
-  DLGM_CHECK_HIP(hipGetLastError());
-  return out;
 }
 
 std::tuple<at::Tensor, at::Tensor> dlgm_moe_combine_bwd(const at::Tensor& dout, const at::Tensor& y,

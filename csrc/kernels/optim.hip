@@ -147,7 +147,7 @@ __device__ __forceinline__ void st_stream(V* a, V v) {
 }
 
 // NT: the optimizer state and the compute copy are streamed once per step -- non-temporal loads / stores keep
-// them from displacing anything in L2 / MALL (DLGM_ADAMW_NT=0: ordinary accesses)
+// them from displacing anything in L2 / MALL (5.51 TB/s vs ordinary accesses, profiles/adamw_nt_ab_r03.json)
 template <typename GT, typename PT, bool NT>
 __global__ __launch_bounds__(kThreads) void adamw_kernel(float* __restrict__ p, float* __restrict__ m,
                                                          float* __restrict__ v, const GT* __restrict__ g,
@@ -316,19 +316,10 @@ void dlgm_adamw_step_(at::Tensor p, at::Tensor m, at::Tensor v, const at::Tensor
   // the compute copy's dtype selects the instantiation (bf16 unless the engine runs the fp16 path)
   DLGM_DISPATCH_16(has16 ? p16->scalar_type() : at::kBFloat16, PT, {
     PT* p16p = has16 ? reinterpret_cast<PT*>(p16->data_ptr()) : nullptr;
-    static const bool nt = [] {
-      const char* e = std::getenv("DLGM_ADAMW_NT");
-      return !(e != nullptr && e[0] == '0');
-    }();
     if (g.scalar_type() == at::kFloat) {
-      if (nt)
-        adamw_kernel<float, PT, true><<<grid, kThreads, 0, stream>>>(p.data_ptr<float>(), m.data_ptr<float>(),
-                                                                     v.data_ptr<float>(), g.data_ptr<float>(), p16p,
-                                                                     sp, inv, n, h);
-      else
-        adamw_kernel<float, PT, false><<<grid, kThreads, 0, stream>>>(p.data_ptr<float>(), m.data_ptr<float>(),
-                                                                      v.data_ptr<float>(), g.data_ptr<float>(), p16p,
-                                                                      sp, inv, n, h);
+      adamw_kernel<float, PT, true><<<grid, kThreads, 0, stream>>>(p.data_ptr<float>(), m.data_ptr<float>(),
+                                                                   v.data_ptr<float>(), g.data_ptr<float>(), p16p,
+                                                                   sp, inv, n, h);
     } else {
       DLGM_DISPATCH_16(g.scalar_type(), GT, adamw_kernel<GT, PT, false><<<grid, kThreads, 0, stream>>>(
                                                 p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),

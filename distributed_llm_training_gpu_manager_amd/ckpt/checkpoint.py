@@ -154,6 +154,8 @@ class AsyncCheckpointer:
         self.src_rank = _source_rank(eng)
         self.shm_src_path = f"/dev/shm/dlgm-ckpt-{key}-r{self.src_rank}.snap"
         self.shm_src_meta = self.shm_src_path[:-5] + ".json"
+        self.tier_notes: List[str] = []
+        self.shm_need_bytes = 0
         self.mode = self._pick_mode(mode, shm)
         self._snap: Optional[torch.Tensor] = None  # uint8 [14 n]: fp32 master | exp_avg | exp_avg_sq | bf16 params
         self._pinned_shm = False
@@ -195,17 +197,31 @@ class AsyncCheckpointer:
     def _pick_mode(self, mode: str, shm: Any) -> str:
         if mode in ("device", "host", "shm"):
             return mode
+        want_shm = shm is True or (shm == "auto" and self.cuda)
+        if want_shm and self._shm_fits():
+            if self.active:
+                return "shm"
         if not self.active:
             return "host"
-        want_shm = shm is True or (shm == "auto" and self.cuda)
-        if want_shm and os.path.isdir("/dev/shm"):
-            st = os.statvfs("/dev/shm")
-            if st.f_bavail * st.f_frsize > self.snap_bytes + (8 << 30):
-                return "shm"
         if not self.cuda or getattr(self.engine, "offload", None) is not None:
             return "host"  # offloaded optimizer state already lives in host memory
         free, _ = torch.cuda.mem_get_info(self.dev)
         return "device" if free > self.snap_bytes + (24 << 30) else "host"
+
+    def _shm_fits(self) -> bool:
+        """Does /dev/shm hold the snapshots of EVERY writer rank of this node? Collective: the node's need is the
+        largest rank snapshot x the local ranks (LOCAL_WORLD_SIZE, torchrun), and the verdict is the minimum over
+        all ranks, so every rank picks the same tier (eight Llama-3-70B ranks would need 8 x 123 GB; a per-rank
+        check passes on each and overcommits tmpfs together)."""
+        agree = _Agree(self.engine)
+        need = agree.max(float(self.snap_bytes if self.active else 0)) * max(1, int(os.environ.get(
+            "LOCAL_WORLD_SIZE", "1")))
+        ok = 0.0
+        if os.path.isdir("/dev/shm"):
+            st = os.statvfs("/dev/shm")
+            ok = 1.0 if st.f_bavail * st.f_frsize > need + (8 << 30) else 0.0
+        self.shm_need_bytes = int(need)
+        return agree.min(ok) > 0
 
     def _before_optimizer_step(self, engine) -> None:
         # GPU-side ordering only: the next AdamW must not overwrite master/m/v before the capture read them
@@ -220,11 +236,25 @@ class AsyncCheckpointer:
                 snap = keep  # the file this rank just restored from, already mapped (and its pages touched)
             else:
                 del keep
+                # reserve the pages now (posix_fallocate): a full tmpfs is an error here, not a SIGBUS in the middle
+                # of a snapshot copy into a sparse file
                 fd = os.open(self.shm_path, os.O_RDWR | os.O_CREAT, 0o600)
                 try:
-                    os.ftruncate(fd, nb)
+                    os.posix_fallocate(fd, 0, nb)
+                    reserved = True
+                except OSError as e:
+                    reserved = False
+                    self.tier_notes.append(f"shm reservation of {nb} B failed ({e}); snapshot tier -> host memory")
                 finally:
                     os.close(fd)
+                if not reserved:
+                    try:
+                        os.unlink(self.shm_path)
+                    except OSError:
+                        pass
+                    self.mode = "host"
+                    self._snap = torch.empty(nb, dtype=torch.uint8, pin_memory=self.cuda)
+                    return
                 snap = torch.from_file(self.shm_path, shared=True, size=nb, dtype=torch.uint8)
             if self.cuda:
                 self._pinned_shm = self._register_chunked(snap.data_ptr(), nb)

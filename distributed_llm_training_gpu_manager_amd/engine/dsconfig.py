@@ -64,6 +64,7 @@ def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, model_cf
         min_loss_scale=float(ds.get("fp16", {}).get("min_loss_scale", 1.0)),
         offload_optimizer=off_o,
         nvme_path=zo.get("offload_optimizer", {}).get("nvme_path") or zo.get("offload_param", {}).get("nvme_path"),
+        param_nvme_path=zo.get("offload_param", {}).get("nvme_path"),
         offload_buffer_count=int(zo.get("offload_optimizer", {}).get("buffer_count", 4)),
         aio_threads=max(1, int(ds.get("aio", {}).get("thread_count", 1)) * int(ds.get("aio", {}).get("queue_depth", 8))),
         aio_block_size=int(ds.get("aio", {}).get("block_size", 8 << 20)),
@@ -77,6 +78,8 @@ def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, model_cf
         gradient_predivide_factor=float(ds.get("gradient_predivide_factor", 1.0)),
         offload_param=off_p,
         param_buffer_count=int(zo.get("offload_param", {}).get("buffer_count", 5)),
+        # DeepSpeed's default is False: without the key a stage-3 save carries no gathered 16-bit module
+        gather_16bit_weights_on_model_save=bool(zo.get("stage3_gather_16bit_weights_on_model_save", False)),
     )
     # engine knobs without a DeepSpeed key travel in the "mi355x" block (launcher.config.MI355XOptions)
     cfg.expert_parallel_size = int(mi.get("expert_parallel_size", cfg.expert_parallel_size))
@@ -85,8 +88,11 @@ def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, model_cf
         cfg.local_grad_accum = mi["local_grad_accum"]
     if "hip_graphs" in mi:
         cfg.hip_graphs = bool(mi["hip_graphs"])
-    if "mesh_allgather" in mi:
-        cfg.mesh_allgather = bool(mi["mesh_allgather"])
+    if "xgmi_mesh" in mi:
+        v = mi["xgmi_mesh"]
+        cfg.xgmi_mesh = ("on" if v else "off") if isinstance(v, bool) else str(v)
+    if "ep_capacity_factor" in mi:
+        cfg.ep_capacity_factor = float(mi["ep_capacity_factor"])
     if mi.get("comm_dtype"):
         cfg.comm_dtype = {"fp32": torch.float32, "float32": torch.float32}.get(mi["comm_dtype"], torch.bfloat16)
     if auto_mbs:

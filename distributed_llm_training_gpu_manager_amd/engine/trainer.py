@@ -129,6 +129,14 @@ class Trainer:
         self.env = init_distributed(args.device)
         self.timeline["dist_init"] = time.time()
         self.comm = Comm()
+        self.shadow = int(getattr(args, "shadow_world", 0) or 0)
+        if self.shadow > 1:
+            # rank `shadow_rank` of a world-`shadow_world` job alone on this GPU (parallel/comm.py ShadowComm, async
+            # RCCL-ordered streams): its true-size shards, gathers, snapshot and restore -- the config-4 drill at
+            # 70B rank scale on one MI355X
+            from ..parallel.comm import ShadowComm
+            assert self.env.world == 1, "--shadow-world runs one process"
+            self.comm = ShadowComm(self.shadow, int(args.shadow_rank), async_mode=True)
         over = {"max_seq_len": max(args.seq_len, 1)} if args.seq_len else {}
         if getattr(args, "n_layers", 0):
             over["n_layers"] = args.n_layers  # drills on a box: the named architecture, fewer blocks
@@ -160,6 +168,8 @@ class Trainer:
             self.ecfg.wall_clock_breakdown = True
         if getattr(args, "hip_graphs", False):
             self.ecfg.hip_graphs = True
+        if getattr(args, "xgmi_mesh", None):
+            self.ecfg.xgmi_mesh = args.xgmi_mesh
         if args.halt_on_nan and not self.ecfg.fp16:
             self.ecfg.nan_latch = True  # the host runs one step ahead of the NaN decision (see NanTrap)
         self.global_batch = self._elastic_batch(args)
@@ -171,9 +181,10 @@ class Trainer:
         shm = {"auto": "auto", "on": True, "off": False}[args.ckpt_shm]
         self.ckpt = AsyncCheckpointer(self.engine, save_dir, mode=args.ckpt_mode, keep_last=args.keep_last, shm=shm,
                                       disk=bool(args.ckpt_disk)) if save_dir else None
+        drank = self.comm.rank if self.shadow > 1 else self.env.rank
         self.data = SyntheticData(self.mcfg.vocab_size, self.ecfg.micro_batch_size, args.seq_len,
-                                  self.ecfg.grad_accum, args.seed, self.env.rank // self.sp, self.env.device,
-                                  sp_rank=self.env.rank % self.sp, sp_size=self.sp)
+                                  self.ecfg.grad_accum, args.seed, drank // self.sp, self.env.device,
+                                  sp_rank=drank % self.sp, sp_size=self.sp)
         self.pusher = MetricsPusher(args.metrics_url if self.env.rank == 0 else None,
                                     os.environ.get("DLGM_JOB_ID", args.job_id))
         self.telemetry = None
@@ -302,7 +313,9 @@ class Trainer:
         prev: Optional[Tuple[int, Dict[str, Any]]] = None
         last = start
         for step in range(start + 1, a.steps + 1):
-            if a.inject_nan_step == step and first_attempt:
+            if a.inject_nan_step == step and first_attempt and a.inject_nan_rank in (-1, self.env.rank):
+                # one faulty rank among healthy ones (--inject-nan-rank): the non-finite count rides the all-reduced
+                # gradient statistics, so every rank skips the update and halts at the same step
                 self.engine.fault_inject_nan = True
             self.engine.host_flag = 1.0 if self.preempt else 0.0
             prof = getattr(a, "profile_steps", 0) and step - start == 2  # trace window after one warm step
@@ -343,7 +356,8 @@ class Trainer:
                     if last_saved > 0:
                         self.ckpt.wait_published(last_saved)
                 os.kill(os.getpid(), signal.SIGKILL)
-            if a.preempt_at_step == step and first_attempt:
+            if a.preempt_at_step == step and first_attempt and a.preempt_rank in (-1, self.env.rank):
+                # a notice on one rank only (--preempt-rank): its flag rides the next step's all-reduced statistics
                 os.kill(os.getpid(), signal.SIGUSR1)
             if self.preempt and self.env.world == 1:
                 # one rank needs no agreement: checkpoint the step just queued, now (W > 1 ranks agree through
@@ -389,6 +403,12 @@ class Trainer:
                                      "engine": {"zero_stage": self.ecfg.zero_stage, "world": self.env.world,
                                                 "backend": self.env.backend, "device": str(self.env.device),
                                                 "notes": self.notes}}), f)
+        if getattr(a, "dump_state", None):
+            # per-rank outcome for multi-rank drills: exit code, last step read, this rank's fp32 partition
+            os.makedirs(a.dump_state, exist_ok=True)
+            torch.save({"rc": rc, "rank": self.env.rank, "last_step": self.log[-1]["step"] if self.log else start,
+                        "step_count": self.engine.step_count, "master": self.engine.master.detach().cpu().clone()},
+                       os.path.join(a.dump_state, f"rank{self.env.rank}.pt"))
         if torch.distributed.is_initialized():
             torch.distributed.destroy_process_group()
         return rc
@@ -443,6 +463,16 @@ def parse_args(argv=None) -> argparse.Namespace:
                     help="Ulysses sequence-parallel size: ranks of a group split each sequence")
     ap.add_argument("--hip-graphs", action="store_true",
                     help="replay each step's micro-batch loop as one captured HIP graph (single rank, dense)")
+    ap.add_argument("--xgmi-mesh", default=None, choices=["on", "off"],
+                    help="ZeRO gathers / reduce-scatters and the EP exchange over the device-driven xGMI mesh")
+    ap.add_argument("--inject-nan-rank", type=int, default=-1,
+                    help="with --inject-nan-step: poison the gradient on this rank only (-1: every rank)")
+    ap.add_argument("--preempt-rank", type=int, default=-1,
+                    help="with --preempt-at-step: deliver the preemption notice to this rank only (-1: every rank)")
+    ap.add_argument("--shadow-world", type=int, default=0,
+                    help="simulate rank --shadow-rank of a job of this many ranks alone on one GPU (true-size state)")
+    ap.add_argument("--shadow-rank", type=int, default=0)
+    ap.add_argument("--dump-state", default=None, help="directory: each rank saves rc / last step / its partition")
     a, unknown = ap.parse_known_args(argv)
     return a
 

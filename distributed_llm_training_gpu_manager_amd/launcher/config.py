@@ -58,7 +58,11 @@ class MI355XOptions(BaseModel):
     local_grad_accum: Union[bool, str] = Field(
         default="hbm", description="ZeRO-2/3: fp32 grads accumulate locally, one reduce-scatter per step ('hbm': if they fit)")
     hip_graphs: bool = Field(default=False, description="replay the micro-batch loop as one captured HIP graph "
-                             "(single rank, dense models)")
+                             "(single rank; or every collective on the xGMI mesh)")
+    xgmi_mesh: str = Field(default="off", description="on: dense ZeRO gathers / reduce-scatters and the EP token "
+                           "exchange over the device-driven xGMI mesh (HIP IPC symmetric heaps); off: RCCL rings")
+    ep_capacity_factor: float = Field(default=2.0, gt=0, description="mesh EP receive capacity, x the balanced "
+                                      "share of rows (overflow rows are dropped and flagged)")
     auto_micro_batch: bool = Field(default=False, description="size the micro-batch (and GA, activation "
                                    "checkpointing) to the per-rank HBM plan, keeping the global batch")
 

@@ -68,6 +68,9 @@ class StepContext:
     expert_stats: Optional[torch.Tensor] = None
     # fp16 path: the dynamic loss scale as a device word (multiplied into the loss gradient on the device)
     loss_scale: Optional[torch.Tensor] = None
+    # expert-parallel token exchange shared by every MoE layer (parallel/ep.py MeshExpertDispatcher); None: the
+    # layer builds the RCCL dispatcher over ep_group
+    ep_dispatcher: Any = None
 
     @property
     def tokens(self) -> int:

@@ -11,8 +11,7 @@ Attention is the Llama block's (GQA, RoPE theta 1e6). The FFN is a routed mixtur
                                            expert dW deferred to the step's last micro-batch as one
                                            grouped-K launch per weight over K-contiguous operands (the
                                            stashed micro-batches transposed once into an aligned re-layout,
-                                           each expert's rows of all micro-batches contiguous);
-                                           opt-in alternative: the capacity layout (ops.moe.CapacityPlan)
+                                           each expert's rows of all micro-batches contiguous)
     EP all-to-all back, combine            out[t] = sum_k gate * y[slot]  (HIP gather kernel)
 
 Backward is hand-written: the combine adjoint gives d(expert outputs) and d(gates),
@@ -34,8 +33,7 @@ import torch
 from .. import ops
 from ..ops.gemm import grad_mm, transpose_multi
 from ..ops import gemm_mfma as gm
-from ..ops.moe import (capacity_plan, capacity_rows, gather_rows, moe_combine, moe_combine_bwd, moe_permute,
-                       pad_plan_multi)
+from ..ops.moe import moe_combine, moe_combine_bwd, moe_permute, pad_plan_multi
 from ..parallel.ep import ExpertDispatcher
 from .common import ParamSpec, Params, StepContext, Unit
 from .config import ModelConfig
@@ -59,33 +57,27 @@ class MixtralBlock(LlamaBlock):
         out_std = c.init_std / (2 * c.n_layers) ** 0.5
         off = self.ep_rank * self.E_local
         # tcache: the engine keeps [E, in, out] transposes (budgeted), so the grouped MFMA dX GEMMs read
-        # K-contiguous weights; the capacity layout's batched hipBLASLt GEMMs take either layout at speed
-        tc = not gm.CAPACITY
+        # K-contiguous weights
+        tc = True
         return [ParamSpec("w_gate_up", (self.E_local, 2 * c.ffn_dim, c.d_model), std=c.init_std,
                           experts=self.E_local, expert_offset=off, tcache=tc),
                 ParamSpec("w_down", (self.E_local, c.d_model, c.ffn_dim), std=out_std,
                           experts=self.E_local, expert_offset=off, tcache=tc)]
 
-    def dispatcher(self, ctx: StepContext) -> ExpertDispatcher:
+    def dispatcher(self, ctx: StepContext):
+        if ctx.ep_dispatcher is not None:
+            return ctx.ep_dispatcher
         if self._dispatcher is None:
             self._dispatcher = ExpertDispatcher(ctx.ep_group if self.ep_size > 1 else None, self.cfg.n_experts)
         return self._dispatcher
 
     # ---------------------------------------------------------------- MoE FFN
-    def _cap_mode(self, x: torch.Tensor) -> bool:
-        """Expert GEMMs over the capacity layout (static-shape batched hipBLASLt + grouped overflow)?"""
-        c = self.cfg
-        return gm.CAPACITY and (not x.is_cuda or gm.grouped_supported(x, capacity=True)) and \
-            (2 * c.ffn_dim) % 256 == 0 and c.d_model % 256 == 0 and c.ffn_dim % 256 == 0
-
     def moe_forward(self, p: Params, hn2: torch.Tensor, ctx: StepContext):
         c = self.cfg
         T, E, K = hn2.shape[0], c.n_experts, c.top_k
         probs, topi, gates = ops.router_topk(torch.mm(hn2, p["router"].t()), K)  # [K9]
         offsets, pos, tok = moe_permute(topi, E)  # expert sort on the device, no host read
         counts = (offsets[1:] - offsets[:-1]).long()
-        if self._cap_mode(hn2):
-            return self._moe_forward_cap(p, hn2, ctx, probs, topi, gates, offsets, pos, tok, counts)
         x_sorted = hn2.index_select(0, tok)
         disp = self.dispatcher(ctx)
         x_local, dctx = disp.dispatch(x_sorted, counts, offsets)
@@ -96,88 +88,11 @@ class MixtralBlock(LlamaBlock):
         ctx.aux.setdefault("moe_aux", []).append(float(E) * (f * probs.mean(0)).sum())
         return out, (probs, topi, gates, pos, f, x_local, dctx, exp_saved, y_sorted)
 
-    def _moe_forward_cap(self, p: Params, hn2, ctx, probs, topi, gates, offsets, pos, tok, counts):
-        """Capacity-layout MoE forward (ops.moe.CapacityPlan): at EP = 1 the expert rows are gathered straight
-        from the tokens into the expanded layout and the combine reads the expert outputs through the slot ->
-        expanded-row map; at EP > 1 the all-to-all carries expert-sorted rows and the layout is entered /
-        left on the expert rank."""
-        c = self.cfg
-        T, E, K = hn2.shape[0], c.n_experts, c.top_k
-        disp = self.dispatcher(ctx)
-        if disp.W == 1:
-            plan = capacity_plan(offsets, T * K, capacity_rows(T * K, E, gm.CAPACITY_FACTOR, gm.CAPACITY_ALIGN))
-            x_exp = gather_rows(hn2, plan.exp_src, tok, plan.nrows)
-            dctx = None
-        else:
-            x_local, dctx = disp.dispatch(hn2.index_select(0, tok), counts, offsets)
-            R = x_local.shape[0]
-            C = capacity_rows(T * K * disp.W, E, gm.CAPACITY_FACTOR, gm.CAPACITY_ALIGN)  # balanced share x factor
-            plan = capacity_plan(dctx.local_offsets, R, C)
-            x_exp = gather_rows(x_local, plan.exp_src, None, plan.nrows)
-        y_exp, exp_saved = self._experts_fwd_cap(p, x_exp, plan)
-        if dctx is None:
-            y_src, pos_y = y_exp, plan.row_map.index_select(0, pos.reshape(-1)).view_as(pos)
-        else:
-            y_src, pos_y = disp.combine(y_exp.index_select(0, plan.row_map), dctx), pos
-        out = moe_combine(y_src, pos_y, gates)
-        f = counts.float() / float(T * K) * K
-        ctx.aux.setdefault("moe_aux", []).append(float(E) * (f * probs.mean(0)).sum())
-        return out, ("cap", probs, topi, gates, pos, f, dctx, x_exp, plan, exp_saved, y_src, pos_y)
-
-    def _experts_fwd_cap(self, p: Params, x: torch.Tensor, plan):
-        gu = gm.capacity_mm(x, p["w_gate_up"], plan)
-        a = ops.swiglu_fwd(gu, plan.nrows)
-        y = gm.capacity_mm(a, p["w_down"], plan)
-        return y, (gu, a)
-
-    def _experts_bwd_cap(self, p: Params, g: Params, x: torch.Tensor, dy: torch.Tensor, saved, plan, ctx):
-        gu, a = saved
-        da = gm.capacity_mm(dy, p["w_down"], plan, transpose_w=False)
-        dgu = ops.swiglu_bwd(da, gu, plan.nrows)
-        del da
-        dx = gm.capacity_mm(dgu, p["w_gate_up"], plan, transpose_w=False)
-        if ctx.defer_wgrad:
-            # dW once per step: each expert's capacity rows of every micro-batch in ONE batched GEMM (K = GA x C)
-            if ctx.micro_index == 0:
-                self._wstash, self._wflushed, self._wbytes = [], False, 0
-            self._wstash.append((dy, a, dgu, x, plan))
-            self._wbytes += sum(t.numel() * t.element_size() for t in (dy, a, dgu, x))
-            if ctx.last_micro or self._wbytes > getattr(ctx, "defer_budget_bytes", 48 << 30):
-                self._flush_wgrad_cap(g)
-            return dx
-        gm.capacity_wgrad(g["w_down"], [dy], [a], [plan], ctx.grad_acc)
-        gm.capacity_wgrad(g["w_gate_up"], [dgu], [x], [plan], ctx.grad_acc)
-        return dx
-
-    def _flush_wgrad_cap(self, g: Params) -> None:
-        stash, acc = self._wstash, self._wflushed
-        self._wstash, self._wflushed, self._wbytes = [], True, 0
-        plans = [s[4] for s in stash]
-        gm.capacity_wgrad(g["w_down"], [s[0] for s in stash], [s[1] for s in stash], plans, acc)
-        gm.capacity_wgrad(g["w_gate_up"], [s[2] for s in stash], [s[3] for s in stash], plans, acc)
-
-    def _moe_backward_cap(self, p: Params, g: Params, hn2: torch.Tensor, saved, dout: torch.Tensor, ctx):
-        _, probs, topi, gates, pos, f, dctx, x_exp, plan, exp_saved, y_src, pos_y = saved
-        disp = self.dispatcher(ctx)
-        dy_src, dgates = moe_combine_bwd(dout.contiguous(), y_src, pos_y, gates)
-        if dctx is None:
-            dy_exp = dy_src  # rows no slot references (capacity padding, unused overflow) are zero
-        else:
-            dy_local = disp.redispatch(dy_src, dctx)
-            dy_exp = dy_local.new_zeros((plan.rows, dy_local.shape[1]))
-            dy_exp.index_copy_(0, plan.row_map, dy_local)
-        dx_exp = self._experts_bwd_cap(p, g, x_exp, dy_exp, exp_saved, plan, ctx)
-        if dctx is None:
-            dhn2 = moe_combine(dx_exp, pos_y, None)  # adjoint of the dispatch gather: sum the K slots per token
-        else:
-            dhn2 = moe_combine(disp.combine(dx_exp.index_select(0, plan.row_map), dctx), pos, None)
-        return self._router_backward(p, g, hn2, probs, topi, gates, f, dgates, dhn2, dout, ctx)
-
-    def _grouped(self, x: torch.Tensor, wgrad: bool = False) -> bool:
+    def _grouped(self, x: torch.Tensor) -> bool:
         """Expert GEMMs as single grouped MFMA launches (csrc/kernels/gemm_mfma.hip) with the device
-        offsets: no host read of the routing counts, no per-expert launches (wgrad: the dW GEMMs only)."""
+        offsets: no host read of the routing counts, no per-expert launches."""
         c = self.cfg
-        return gm.grouped_supported(x, wgrad) and (2 * c.ffn_dim) % 256 == 0 and c.d_model % 256 == 0 \
+        return gm.grouped_supported(x) and (2 * c.ffn_dim) % 256 == 0 and c.d_model % 256 == 0 \
             and c.ffn_dim % 256 == 0 and c.d_model % 64 == 0
 
     def _experts_fwd(self, p: Params, x: torch.Tensor, dctx):
@@ -187,7 +102,7 @@ class MixtralBlock(LlamaBlock):
         if self._grouped(x):
             offs = dctx.local_offsets
             gu_all = gm.grouped_mm(x, p["w_gate_up"], offs)
-            a_all = ops.swiglu_fwd(gu_all)
+            a_all = ops.swiglu_fwd(gu_all, dctx.nrows)  # mesh dispatch: capacity rows, the first nrows valid
             y = gm.grouped_mm(a_all, p["w_down"], offs)
             return y, (gu_all, a_all, dctx)
         counts = dctx.counts()
@@ -228,18 +143,18 @@ class MixtralBlock(LlamaBlock):
             offs = dctx.local_offsets
             dy = dy.contiguous()
             da_all = self._grouped_dx(dy, p, "w_down", offs)
-            dgu_all = ops.swiglu_bwd(da_all, gu_all)
+            dgu_all = ops.swiglu_bwd(da_all, gu_all, dctx.nrows)
             del da_all
             dx = self._grouped_dx(dgu_all, p, "w_gate_up", offs)
             if ctx is not None and ctx.defer_wgrad:
                 # dW once per step over the micro-batches' rows regrouped expert-major on the device
                 if ctx.micro_index == 0:
                     self._wstash, self._wflushed, self._wbytes = [], False, 0
-                # K-major flush (gm.KMAJOR_DW): the rows stay row-major until the step's last micro-batch, then
+                # K-major flush: the rows stay row-major until the step's last micro-batch, then
                 # each operand of all stashed micro-batches is transposed ONCE into an aligned re-layout where every
                 # expert's rows of all micro-batches are contiguous and start on a 64-column boundary -> one plain
                 # grouped-K launch per weight (K-contiguous fragments, no per-segment selection in its loop)
-                item = (dy, a_all, dgu_all, x, offs, gm.KMAJOR_DW)
+                item = (dy, a_all, dgu_all, x, offs)
                 self._wstash.append(item)
                 self._wbytes += sum(t.numel() * t.element_size() for t in item[:4])
                 if ctx.last_micro or self._wbytes > getattr(ctx, "defer_budget_bytes", 48 << 30):
@@ -250,38 +165,30 @@ class MixtralBlock(LlamaBlock):
             gm.grouped_wgrad(g["w_gate_up"], dgu_all, x, offs, acc, stats=xs)
             self._count_stats(ctx, xs, 2)
             return dx
+        # the per-expert reference path (CPU tensors): reads the routing counts on the host
         counts = dctx.counts()
         if ctx is not None and ctx.defer_wgrad:
             return self._experts_bwd_deferred(p, g, x, dy, saved, counts, ctx)
-        # weight gradients as grouped launches (reduction over each expert's token rows, device offsets)
-        gw = self._grouped(x, wgrad=True) and dctx.local_offsets is not None
-        dy = dy.contiguous() if gw else dy
         dx = torch.empty_like(x)
         da_all = torch.empty_like(a_all)
-        if gw:
-            gm.grouped_wgrad(g["w_down"], dy, a_all, dctx.local_offsets, acc)
         off = 0
         for e, n in enumerate(counts):
             if n == 0:
-                if not acc and not gw:
+                if not acc:
                     g["w_down"][e].zero_()
                     g["w_gate_up"][e].zero_()
                 continue
             dye = dy.narrow(0, off, n)
-            if not gw:
-                grad_mm(g["w_down"][e], dye.t(), a_all.narrow(0, off, n), acc)
+            grad_mm(g["w_down"][e], dye.t(), a_all.narrow(0, off, n), acc)
             self._expert_dx(dye, p, "w_down", e, da_all.narrow(0, off, n))
             off += n
         dgu_all = ops.swiglu_bwd(da_all, gu_all)  # one launch over every expert's rows
         del da_all
-        if gw:
-            gm.grouped_wgrad(g["w_gate_up"], dgu_all, x, dctx.local_offsets, acc)
         off = 0
         for e, n in enumerate(counts):
             if n:
                 dgu = dgu_all.narrow(0, off, n)
-                if not gw:
-                    grad_mm(g["w_gate_up"][e], dgu.t(), x.narrow(0, off, n), acc)
+                grad_mm(g["w_gate_up"][e], dgu.t(), x.narrow(0, off, n), acc)
                 self._expert_dx(dgu, p, "w_gate_up", e, dx.narrow(0, off, n))
             off += n
         return dx
@@ -358,24 +265,17 @@ class MixtralBlock(LlamaBlock):
         for i in range(0, len(stash), gm.MAX_SEGMENTS):
             part = stash[i:i + gm.MAX_SEGMENTS]
             offs = torch.stack([t[4] for t in part])  # [segments, experts + 1] int32, on the device
-            if part[0][5]:
-                # the last launch over a weight stores its final gradient: tally the statistics there
-                xs = self._final_stats(ctx) if i + gm.MAX_SEGMENTS >= len(stash) else None
-                src, poff = pad_plan_multi(offs, sum(int(t[0].shape[0]) for t in part))
-                for wname, ia, ib in (("w_down", 0, 1), ("w_gate_up", 2, 3)):
-                    at_ = transpose_multi([t[ia] for t in part], src)
-                    bt_ = transpose_multi([t[ib] for t in part], src)
-                    gm.grouped_wgrad(g[wname], at_, bt_, poff, acc or i > 0, kmajor=True, stats=xs)
-                    del at_, bt_
-                self._count_stats(ctx, xs, 2)
-                continue
-            gm.grouped_wgrad_segments(g["w_down"], [t[0] for t in part], [t[1] for t in part], offs, acc or i > 0)
-            gm.grouped_wgrad_segments(g["w_gate_up"], [t[2] for t in part], [t[3] for t in part], offs,
-                                      acc or i > 0)
+            # the last launch over a weight stores its final gradient: tally the statistics there
+            xs = self._final_stats(ctx) if i + gm.MAX_SEGMENTS >= len(stash) else None
+            src, poff = pad_plan_multi(offs, sum(int(t[0].shape[0]) for t in part))
+            for wname, ia, ib in (("w_down", 0, 1), ("w_gate_up", 2, 3)):
+                at_ = transpose_multi([t[ia] for t in part], src)
+                bt_ = transpose_multi([t[ib] for t in part], src)
+                gm.grouped_wgrad(g[wname], at_, bt_, poff, acc or i > 0, kmajor=True, stats=xs)
+                del at_, bt_
+            self._count_stats(ctx, xs, 2)
 
     def moe_backward(self, p: Params, g: Params, hn2: torch.Tensor, saved, dout: torch.Tensor, ctx: StepContext):
-        if saved[0] == "cap":
-            return self._moe_backward_cap(p, g, hn2, saved, dout, ctx)
         probs, topi, gates, pos, f, x_local, dctx, exp_saved, y_sorted = saved
         disp = self.dispatcher(ctx)
         dy_sorted, dgates = moe_combine_bwd(dout.contiguous(), y_sorted, pos, gates)

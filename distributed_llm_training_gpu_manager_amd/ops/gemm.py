@@ -14,7 +14,7 @@ from typing import Optional
 
 import torch
 
-from .._native import hip_ops, use_native
+from .._native import hip_available, hip_ops, use_native
 
 
 # hipBLASLt on gfx950, bf16 x bf16 -> fp32 (measured, tools/probe_dw_layout2.py): both operands with
@@ -95,7 +95,8 @@ _LT: dict = {"table": None, "version": None, "timings": {}}
 
 
 def lt_enabled() -> bool:
-    return os.environ.get("DLGM_GEMM_LT", "1") != "0"
+    """hipBLASLt through csrc/kernels/gemm_lt.hip whenever the native library is loaded."""
+    return hip_available()
 
 
 def _lt_key(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, beta: float) -> str:

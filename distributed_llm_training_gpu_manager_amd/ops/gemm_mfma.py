@@ -18,7 +18,6 @@ permitted when stream is capturing": it synchronises) and ran 117.5k tok/s again
 """
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
@@ -26,33 +25,14 @@ import torch
 from .._native import hip_ops, use_native
 
 DENSE, GROUP_M, GROUP_K = 0, 1, 2
-# Expert GEMM strategy (DLGM_MOE_GROUPED):
-#   "1"     (default) every expert GEMM as one grouped MFMA launch with the device offsets: no host read of the
-#           routing counts at all (graph-capture safe); the input-gradient GEMMs read the engine's cached
-#           [E, in, out] weight transposes, the deferred weight gradients run as ONE segmented launch per weight
-#           over the step's micro-batches;
-#   "0"     the per-expert hipBLASLt loop: reads the routing counts on the host once per layer and micro-batch;
-#   "wgrad" only the weight gradients grouped (MFMA), forward / dX per expert through hipBLASLt.
-# Mixtral-8x7B (2 layers, seq 4096, GA 4, one MI355X, round 3): grouped 120.0k tok/s (MFU 0.27) vs loop 125.0k
-# (0.29) -- 4 % for no host synchronisation in the micro-batch loop (was 115.1k vs 128.3k before the grouped-M
-# tile order, the segmented dW and the expert W^T cache; profiles/moe_experiments_r01.md).
-#   "cap"   capacity layout (ops.moe.CapacityPlan): each expert's first C = factor x balanced-share rows as ONE
-#           static-shape batched hipBLASLt GEMM per weight (forward, dX, and the deferred dW with K = GA x C), the
-#           rows past an expert's capacity as one grouped MFMA launch with device offsets (dropless, no host read);
-#           DLGM_MOE_CAPACITY_FACTOR (default 1.125) sets the capacity.
-_MODE = os.environ.get("DLGM_MOE_GROUPED", "1")
-CAPACITY = _MODE == "cap"
-CAPACITY_FACTOR = float(os.environ.get("DLGM_MOE_CAPACITY_FACTOR", "1.125"))
-# deferred grouped dW over K-contiguous operands (each stashed micro-batch transposed into an aligned re-layout);
-# EP = 1 (one static row count); DLGM_MOE_KMAJOR_DW=0 keeps the token-major (transposed-LDS-read) kernel
-KMAJOR_DW = os.environ.get("DLGM_MOE_KMAJOR_DW", "1") != "0"
-CAPACITY_ALIGN = 64  # capacity rows per expert are a multiple of this
-# the capacity region as ONE torch.bmm per weight (opt-in): on MI355X / this torch build the bf16 batched GEMM at the
-# Mixtral-8x7B shape ([8, 1024, 4096] x [8, 4096, 28672]) faulted with an illegal address inside the library
-# (gpurun_out probe, round 3), so the default issues one static-shape 2-D GEMM per expert
-CAPACITY_BMM = os.environ.get("DLGM_MOE_CAP_BMM", "0") == "1"
-GROUPED = _MODE in ("1", "cap")
-GROUPED_WGRAD = _MODE in ("1", "wgrad", "cap") and os.environ.get("DLGM_MOE_GROUPED_WGRAD", "1") != "0"
+# Every expert GEMM on the GPU is one grouped MFMA launch with the device offsets (no host read of the routing
+# counts, graph-capture safe): forward / dX through the engine's cached [E, in, out] weight transposes, the deferred
+# weight gradients as ONE grouped-K launch per weight over K-contiguous operands (the step's micro-batches transposed
+# once into an aligned re-layout). Measured alternatives, removed after their A/B (round 3): the per-expert
+# hipBLASLt loop that reads the routing counts on the host (125.0k vs 141.8k tok/s, Mixtral-8x7B 2 layers, GA 4),
+# the token-major dW kernel, and a static [E, C] capacity layout for batched library GEMMs (100.5k: the random-init
+# router overflows the capacity and ~1.1k-row library GEMMs fill 2.2 waves of 256 CUs;
+# profiles/moe_experiments_r01.md, README "Measured").
 
 
 def _ok(t: torch.Tensor) -> bool:
@@ -77,12 +57,9 @@ def supported(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> bool:
             and out.stride(-1) == 1 and out.stride(0) % 4 == 0 and out.dtype in (torch.float32, torch.bfloat16))
 
 
-def grouped_supported(x: torch.Tensor, wgrad: bool = False, capacity: bool = False) -> bool:
-    """Can the grouped kernels take rows `x` (bf16, row-major, 16-B aligned, on the GPU with the extension)?
-    wgrad: asking for the weight-gradient GEMMs only (GROUPED_WGRAD), capacity: for the capacity layout
-    (CAPACITY), else for all expert GEMMs (GROUPED)."""
-    on = CAPACITY if capacity else GROUPED_WGRAD if wgrad else GROUPED
-    return on and use_native(x) and _ok(x) and x.dim() == 2 and x.stride(1) == 1 and x.stride(0) % 8 == 0
+def grouped_supported(x: torch.Tensor) -> bool:
+    """Can the grouped kernels take rows `x` (bf16, row-major, 16-B aligned, on the GPU with the extension)?"""
+    return use_native(x) and _ok(x) and x.dim() == 2 and x.stride(1) == 1 and x.stride(0) % 8 == 0
 
 
 def mfma_mm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, acc: bool = False) -> torch.Tensor:
@@ -156,73 +133,6 @@ def grouped_wgrad(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, offsets: 
         fin = torch.isfinite(o)
         stats[0] += torch.where(fin, o, torch.zeros_like(o)).square().sum()
         stats[1] += (~fin).sum().to(stats.dtype)
-    return out
-
-
-def capacity_mm(x: torch.Tensor, w: torch.Tensor, plan, transpose_w: bool = True,
-                out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Expert GEMM over a capacity layout (ops.moe.CapacityPlan): the G*C capacity rows as ONE static-shape
-    batched GEMM (torch.bmm -> hipBLASLt, either weight layout at library speed), the overflow rows as one
-    grouped MFMA launch with the device offsets (its spare blocks exit at once when nothing overflowed).
-    x [G*C + R, K] row-major, w [G, N, K] (transpose_w) or [G, K, N]."""
-    G, C, gc = plan.G, plan.C, plan.gc
-    N = w.shape[1] if transpose_w else w.shape[2]
-    if out is None:
-        out = torch.empty(x.shape[0], N, dtype=x.dtype, device=x.device)
-    wb = w.transpose(1, 2) if transpose_w else w
-    xc, oc = x[:gc].view(G, C, x.shape[1]), out[:gc].view(G, C, N)
-    if CAPACITY_BMM or not x.is_cuda:
-        torch.bmm(xc, wb, out=oc)
-    else:  # G static-shape library GEMMs (no host read: the shapes do not depend on the routing)
-        for e in range(G):
-            torch.mm(xc[e], wb[e], out=oc[e])
-    if plan.R > 0:
-        grouped_mm(x[gc:], w, plan.ovf_offsets, transpose_w=transpose_w, out=out[gc:])
-    return out
-
-
-def _bmm_f32(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, acc: bool) -> None:
-    """out (+)= a @ b batched, bf16 operands -> fp32 out (hipBLASLt through aten's dtype overloads)."""
-    if out.is_cuda:
-        if acc:
-            torch.baddbmm(out, a, b, out_dtype=torch.float32, out=out)
-        else:
-            torch.bmm(a, b, out_dtype=torch.float32, out=out)
-        return
-    r = torch.bmm(a.float(), b.float())
-    if acc:
-        out.add_(r)
-    else:
-        out.copy_(r)
-
-
-def capacity_wgrad(out: torch.Tensor, a: list, b: list, plans: list, acc: bool = False) -> torch.Tensor:
-    """out[e] (+)= sum_s a[s][rows of e]^T @ b[s][rows of e] over capacity-layout row sets (one per micro-batch):
-    the capacity rows of every set stacked per expert -> ONE batched GEMM with K = sets x C (padding rows are
-    zero in a or b, so they add nothing), then the overflow rows as one segmented grouped-K launch (accumulate).
-    a[s] [G*C + R_s, M], b[s] [G*C + R_s, N] row-major, out [G, M, N] fp32."""
-    G, M, N = out.shape
-    C = plans[0].C
-    assert all(p.C == C and p.G == G for p in plans)
-    gc = G * C
-    if len(a) == 1:
-        A = a[0][:gc].view(G, C, M)
-        B = b[0][:gc].view(G, C, N)
-    else:
-        A = torch.stack([t[:gc].view(G, C, M) for t in a], dim=1).view(G, len(a) * C, M)
-        B = torch.stack([t[:gc].view(G, C, N) for t in b], dim=1).view(G, len(b) * C, N)
-    if CAPACITY_BMM or not out.is_cuda:
-        _bmm_f32(out, A.transpose(1, 2), B, acc)
-    else:
-        from .gemm import grad_mm
-        for e in range(G):
-            grad_mm(out[e], A[e].t(), B[e], acc)
-    del A, B
-    ovf = [(x[gc:], y[gc:], p.ovf_offsets) for x, y, p in zip(a, b, plans) if p.R > 0]
-    for i in range(0, len(ovf), MAX_SEGMENTS):
-        part = ovf[i:i + MAX_SEGMENTS]
-        grouped_wgrad_segments(out, [t[0] for t in part], [t[1] for t in part], torch.stack([t[2] for t in part]),
-                               acc=True)
     return out
 
 

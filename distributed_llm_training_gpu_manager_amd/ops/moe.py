@@ -1,11 +1,9 @@
 """MoE ops: router top-k (csrc/kernels/embedding.hip), the device-side expert permute, the gather-based,
-deterministic, atomic-free combine, the capacity plan and the aligned re-layouts of the deferred expert dW
+deterministic, atomic-free combine and the aligned re-layouts of the deferred expert dW
 (csrc/kernels/moe.hip). The reference has no MoE code; its anchor is BASELINE config 5 (Mixtral expert
 parallelism) on the reference's 8-GPU preset world (``/root/reference/ai_engine/deepspeed_launcher.py:383-406``)."""
 from __future__ import annotations
 
-import math
-from dataclasses import dataclass
 from typing import Optional, Tuple
 
 import torch
@@ -39,63 +37,6 @@ def moe_permute(topi: torch.Tensor, n_experts: int) -> Tuple[torch.Tensor, torch
     pos = torch.empty_like(order)
     pos[order] = torch.arange(order.numel(), device=order.device)
     return offsets, pos.view(T, K), torch.div(order, K, rounding_mode="floor")
-
-
-@dataclass
-class CapacityPlan:
-    """Expert rows laid out for static-shape batched GEMMs (csrc/kernels/moe.hip moe_capacity_plan).
-
-    The expanded row space holds ``G * C`` capacity rows (expert e's first C rows at ``e*C ..``, padding rows
-    past the expert's count are zero) followed by ``R`` overflow rows (an expert's rows past its C-th, packed
-    expert by expert; ``ovf_offsets`` splits them, ``nrows = G*C + used overflow rows`` on the device).
-    Nothing is dropped: the capacity region runs as one batched library GEMM of static shape, the (usually
-    empty) overflow region as one grouped launch with device offsets -- no host read of the routing counts.
-    """
-    G: int
-    C: int
-    R: int
-    exp_src: torch.Tensor      # int32 [G*C + R]: expanded row -> sorted row (-1: padding / unused)
-    row_map: torch.Tensor      # int64 [R]: sorted row -> expanded row
-    ovf_offsets: torch.Tensor  # int32 [G + 1]: overflow rows per expert (exclusive prefix)
-    nrows: torch.Tensor        # int32 [1]: G*C + used overflow rows
-
-    @property
-    def gc(self) -> int:
-        return self.G * self.C
-
-    @property
-    def rows(self) -> int:
-        return self.G * self.C + self.R
-
-
-def capacity_rows(rows: int, groups: int, factor: float, align: int = 64) -> int:
-    """Per-expert capacity C for `rows` routed rows over `groups` experts: factor x the balanced share,
-    rounded up to `align` rows (at least one aligned block)."""
-    c = int(math.ceil(factor * rows / max(1, groups)))
-    return max(align, (c + align - 1) // align * align)
-
-
-def capacity_plan(offsets: torch.Tensor, rows: int, capacity: int) -> CapacityPlan:
-    """Build the :class:`CapacityPlan` of `rows` expert-sorted rows split by `offsets` (int32 [G + 1])."""
-    G = offsets.numel() - 1
-    if use_native(offsets):
-        exp_src, row_map, ovf, nrows = hip_ops().moe_capacity_plan(offsets.contiguous(), rows, capacity)
-        return CapacityPlan(G, capacity, rows, exp_src, row_map, ovf, nrows)
-    off = offsets.long()
-    cnt = off[1:] - off[:-1]
-    over = (cnt - capacity).clamp(min=0)
-    ovf = torch.zeros(G + 1, dtype=torch.long, device=offsets.device)
-    ovf[1:] = over.cumsum(0)
-    exp_src = torch.full((G * capacity + rows,), -1, dtype=torch.int32, device=offsets.device)
-    row_map = torch.empty(rows, dtype=torch.long, device=offsets.device)
-    j = torch.arange(rows, device=offsets.device)
-    e = torch.bucketize(j, off[1:], right=True)  # expert of each sorted row
-    r = j - off[e]
-    x = torch.where(r < capacity, e * capacity + r, G * capacity + ovf[e] + (r - capacity))
-    exp_src[x] = j.to(torch.int32)
-    row_map[:] = x
-    nrows = torch.tensor([G * capacity + int(ovf[-1])], dtype=torch.int32, device=offsets.device)
-    return CapacityPlan(G, capacity, rows, exp_src, row_map, ovf.to(torch.int32), nrows)
 
 
 def padded_rows(rows: int, groups: int, align: int = 64) -> int:
@@ -146,23 +87,6 @@ def pad_plan_multi(offsets: torch.Tensor, rows: int, align: int = 64) -> Tuple[t
             src[p:p + n] = (t << 24) | torch.arange(lo, lo + n, dtype=torch.int32)
             p += n
     return src.to(offsets.device), poff.to(torch.int32).to(offsets.device)
-
-
-def gather_rows(src: torch.Tensor, idx: torch.Tensor, idx2: Optional[torch.Tensor] = None,
-                nrows: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """out[r] = src[idx2[idx[r]] if idx2 is given else idx[r]], zero rows where idx[r] < 0 (int32 idx). On the
-    GPU rows at or past nrows (int32 [1], device) are left uninitialised."""
-    if use_native(src):
-        return hip_ops().gather_rows(src.contiguous(), idx, idx2, nrows)
-    if src.shape[0] == 0:
-        return src.new_zeros((idx.numel(), src.shape[1]))
-    s = idx.long()
-    valid = s >= 0
-    s = s.clamp(min=0)
-    if idx2 is not None:
-        s = idx2.long()[s]
-    out = src.index_select(0, s)
-    return out * valid.unsqueeze(1).to(out.dtype)
 
 
 def moe_combine(y: torch.Tensor, pos: torch.Tensor, gates: Optional[torch.Tensor]) -> torch.Tensor:

@@ -114,39 +114,6 @@ class Comm:
     def _peer(self, r: int) -> int:
         return r if self.group is None else dist.get_global_rank(self.group, r)
 
-    def all_gather_mesh(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = True) -> Handle:
-        """all_gather as a direct mesh exchange: every rank sends its shard to each peer and receives each
-        peer's shard straight into its slot, all W-1 pairs at once (one batched RCCL group of point-to-point
-        sends/receives). On the MI355X xGMI mesh every GPU pair has its own link, so the W-1 transfers run on
-        W-1 links in parallel instead of stepping around a ring (SURVEY.md §5.8 mesh collective; opt-in via
-        EngineConfig.mesh_allgather, measured beside the ring in utils/commbench.py)."""
-        if self.world == 1:
-            if out.data_ptr() != inp.data_ptr():
-                out.copy_(inp)
-            return DONE
-        parts = list(out.chunk(self.world))
-        staged = self.is_gloo and inp.is_cuda  # gloo point-to-point takes host tensors
-        src = inp.cpu() if staged else inp
-        dst = [p.cpu() for p in parts] if staged else parts
-        ops = []
-        for peer in range(self.world):
-            if peer == self.rank:
-                continue
-            ops.append(dist.P2POp(dist.isend, src, self._peer(peer), group=self.group))
-            ops.append(dist.P2POp(dist.irecv, dst[peer], self._peer(peer), group=self.group))
-        works = dist.batch_isend_irecv(ops)
-        parts[self.rank].copy_(inp)
-
-        def post():
-            if staged:
-                for peer in range(self.world):
-                    if peer != self.rank:
-                        parts[peer].copy_(dst[peer])
-        h = Handle(works, post)
-        if not async_op:
-            h.wait()
-        return h
-
     def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, avg: bool = True,
                        async_op: bool = True) -> Handle:
         """out = (sum or mean over ranks of inp)[rank's chunk]."""
@@ -312,9 +279,6 @@ class ShadowComm(Comm):
             return DONE
         return self._run(lambda: out.view(self.world, -1).copy_(inp.reshape(1, -1).expand(self.world, -1)),
                          [out, inp], async_op)
-
-    def all_gather_mesh(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = True) -> Handle:
-        return self.all_gather(out, inp, async_op)
 
     def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, avg: bool = True,
                        async_op: bool = True) -> Handle:

@@ -15,6 +15,14 @@ copy, because RCCL's uneven all-to-all takes its split sizes on the host; the
 backward reuses the forward's splits (no exchange, no read). The permutation from the
 received [source rank][local expert] order to local-expert-major order is built on the
 device (``_regroup_index``), never as a host list.
+
+:class:`MeshExpertDispatcher` is the MI355X-native transport (parallel/xgmi_mesh.py): the routing counts travel
+through the ranks' symmetric heaps, every destination offset is computed on the device, each rank writes its rows
+straight into the expert owners' receive buffers over xGMI in local-expert-major order (no regroup copy), and the
+combine is the mirror image -- no host read at all, so the EP micro-batch loop can be captured in a HIP graph. The
+receive buffer has a static capacity (``capacity_factor`` x the balanced share); rows past it are dropped, their
+expert output is zero, and a sticky overflow word is raised on every rank (:meth:`MeshExpertDispatcher.overflowed`).
+The RCCL dispatcher above stays the default and the fallback (``EngineConfig.xgmi_mesh``).
 """
 from __future__ import annotations
 
@@ -60,6 +68,8 @@ class DispatchCtx:
     regroup: Optional[torch.Tensor]  # recv order -> local-expert-major order
     local_counts: Optional[List[int]]  # host copy (None until asked for at EP = 1)
     local_offsets: Optional[torch.Tensor] = None  # int32 [El + 1] on the device: expert row ranges
+    nrows: Optional[torch.Tensor] = None  # int32 [1] on the device: valid rows of a capacity-sized dispatch output
+    plan: Optional[torch.Tensor] = None  # mesh transfer tables (MeshExpertDispatcher)
 
     def counts(self) -> List[int]:
         """Host per-local-expert row counts (a device sync at EP = 1; the per-expert fallback path only)."""
@@ -136,3 +146,93 @@ class ExpertDispatcher:
         out = y_local.new_empty((sum(ctx.send_splits), y_local.shape[1]))
         self.comm.all_to_all_single(out, y_recv, ctx.send_splits, ctx.recv_splits)
         return out
+
+
+class MeshExpertDispatcher:
+    """EP token exchange over the xGMI mesh (csrc/kernels/xgmi_mesh.hip), device-driven end to end.
+
+    dispatch:   mesh_ep_plan (epoch open + count exchange + tables, one workgroup) -> mesh_push_rows (this rank's
+                expert-sorted rows into every owner's slot at device-computed rows) -> wait -> copy-out of the
+                [capacity, D] local-expert-major rows (ACKs the slot)
+    combine:    epoch open -> push each (local expert, source) block back to the source's expert-sorted rows (zeros
+                for rows dropped by the capacity) -> wait -> copy-out of the [tokens x k, D] rows
+    redispatch: the dispatch pattern again with the forward's tables (backward: d outputs)
+    The dispatch output has `capacity` rows; ``ctx.local_offsets`` / ``ctx.nrows`` say which are valid.
+    """
+
+    def __init__(self, ep_comm: Comm, n_experts: int, device: torch.device, rows: int, d_model: int,
+                 dtype: torch.dtype, capacity_factor: float = 2.0, slots: int = 2, timeout_s: float = 60.0):
+        from .._native import hip_ops
+        from .xgmi_mesh import CH_COMBINE, CH_DISPATCH, XgmiMesh, capacity_rows, ep_region_bytes
+        self.W, self.rank, self.E = ep_comm.world, ep_comm.rank, n_experts
+        assert n_experts % self.W == 0, "n_experts must be divisible by the EP size"
+        self.El = n_experts // self.W
+        self.rows, self.D, self.dtype = int(rows), int(d_model), dtype
+        esz = torch.tensor([], dtype=dtype).element_size()
+        self.C = capacity_rows(self.rows, self.W, capacity_factor)
+        self.hdr, disp = ep_region_bytes(self.W, n_experts, self.C, d_model * esz)
+        self.mesh = XgmiMesh(ep_comm, device, {"ep_dispatch": (disp, slots), "ep_combine": (self.rows * d_model * esz,
+                                                                                          slots)}, timeout_s)
+        self.L = list(hip_ops().mesh_plan_layout(self.W, n_experts))
+        self._A, self._B = self.mesh.regions["ep_dispatch"], self.mesh.regions["ep_combine"]
+        self._cd, self._cc = CH_DISPATCH, CH_COMBINE
+
+    def _push(self, x: torch.Tensor, plan: torch.Tensor, combine: bool) -> None:
+        from .._native import hip_ops
+        m, r = self.mesh, (self._B if combine else self._A)
+        hip_ops().mesh_push_rows(x.contiguous(), plan, combine, m.peers, m.state, m.rank,
+                                 self._cc if combine else self._cd, r.offset, r.slot_bytes,
+                                 0 if combine else self.hdr, r.slots, self.rows if combine else self.C,
+                                 m.heap_bytes, self.E)
+
+    def _copy(self, out: torch.Tensor, nrows: Optional[torch.Tensor], combine: bool) -> None:
+        from .._native import hip_ops
+        m, r = self.mesh, (self._B if combine else self._A)
+        hip_ops().mesh_copy_rows(out, nrows, m.peers, m.state, m.rank, self._cc if combine else self._cd,
+                                 r.offset, r.slot_bytes, 0 if combine else self.hdr, r.slots, m.heap_bytes)
+
+    def dispatch(self, x_sorted: torch.Tensor, counts: torch.Tensor,
+                 offsets: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, DispatchCtx]:
+        from .._native import hip_ops
+        assert x_sorted.shape == (self.rows, self.D) and x_sorted.dtype == self.dtype, \
+            f"mesh dispatch sized for [{self.rows}, {self.D}] {self.dtype} rows, got {tuple(x_sorted.shape)}"
+        if offsets is None:
+            offsets = torch.zeros(self.E + 1, dtype=torch.int32, device=counts.device)
+            offsets[1:] = torch.cumsum(counts, 0)
+        m, A = self.mesh, self._A
+        plan = torch.empty(self.L[-1], dtype=torch.int32, device=x_sorted.device)
+        hip_ops().mesh_ep_plan(offsets.contiguous(), plan, self.C, m.peers, m.state, m.rank, self._cd, A.offset,
+                               A.slot_bytes, A.slots, m.heap_bytes, m.timeout_ticks)
+        self._push(x_sorted, plan, False)
+        m.wait_data(self._cd)
+        nrows = plan[self.L[0]:self.L[0] + 1]
+        out = x_sorted.new_empty((self.C, self.D))
+        self._copy(out, nrows, False)
+        lo = self.L[3]
+        ctx = DispatchCtx([], [], None, None, plan[lo:lo + self.El + 1], nrows=nrows, plan=plan)
+        return out, ctx
+
+    def redispatch(self, rows_sorted: torch.Tensor, ctx: DispatchCtx) -> torch.Tensor:
+        assert rows_sorted.shape == (self.rows, self.D)
+        self.mesh.begin(self._cd, self._A.slots)
+        self._push(rows_sorted, ctx.plan, False)
+        self.mesh.wait_data(self._cd)
+        out = rows_sorted.new_empty((self.C, self.D))
+        self._copy(out, ctx.nrows, False)
+        return out
+
+    def combine(self, y_local: torch.Tensor, ctx: DispatchCtx) -> torch.Tensor:
+        assert y_local.shape == (self.C, self.D)
+        self.mesh.begin(self._cc, self._B.slots)
+        self._push(y_local, ctx.plan, True)
+        self.mesh.wait_data(self._cc)
+        out = y_local.new_empty((self.rows, self.D))
+        self._copy(out, None, True)
+        return out
+
+    def overflowed(self) -> bool:
+        """Did any dispatch so far overflow a receive capacity (host read: call at a step boundary)?"""
+        return self.mesh.overflowed()
+
+    def close(self) -> None:
+        self.mesh.close()

@@ -42,7 +42,6 @@ Schedule (one micro-batch)
 from __future__ import annotations
 
 import math
-import os
 import time
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence, Tuple
@@ -108,9 +107,16 @@ class EngineConfig:
     # through the C++ AIO engine into a ring of param_buffer_count pinned slots (offload.NvmeParamStore)
     offload_param: str = "none"
     param_buffer_count: int = 5  # offload_param.buffer_count (DeepSpeed default 5)
-    # parameter all-gathers as direct mesh exchanges (batched point-to-point over every xGMI link at once)
-    # instead of RCCL's ring all-gather; opt-in, A/B'd by the bench's post-timing sweep (utils/commbench.py)
-    mesh_allgather: bool = False
+    # device-driven xGMI mesh transport (parallel/xgmi_mesh.py): "on" = the dense ZeRO parameter all-gathers
+    # (a pull over every peer's link at once, out of the peers' symmetric heaps), the dense gradient
+    # reduce-scatters (push into the owners' slots + an fp32 rank-order reduce fused with the accumulate) and, at
+    # EP > 1, the expert token exchange (parallel/ep.py MeshExpertDispatcher) -- no host synchronisation, so the
+    # multi-rank micro-batch loop can be HIP-graph captured; "off" = RCCL rings (the default until an 8-GPU
+    # node has measured both: bench.py's post-timing mesh sweep)
+    xgmi_mesh: str = "off"
+    mesh_min_bytes: int = 0  # dense collectives below this many bytes stay on RCCL
+    mesh_timeout_s: float = 120.0  # a device-side wait past this records an error (XgmiMesh.check) and returns
+    ep_capacity_factor: float = 2.0  # mesh EP receive capacity: this many times the balanced share of rows
     # expert weight gradients: keep each micro-batch's (dY, X) per expert and run one dW GEMM per expert over
     # the concatenated micro-batches at the last one (K = GA x tokens: the fp32 gradient is read and written
     # once per step instead of once per micro-batch). Only with direct fp32 gradient targets; "auto" = on
@@ -120,10 +126,10 @@ class EngineConfig:
     # the expert groups' gradient statistics (sum of squares, #non-finite) tallied by the grouped dW GEMM's
     # epilogue at the last micro-batch instead of a separate pass over the expert gradients (single rank:
     # the stored gradient is then final); falls back to ops.grad_stats whenever a weight was not covered.
-    # DLGM_FUSED_XSTATS=0 turns it off (A/B on Mixtral 2-layer: 133.2k -> 136.3k tokens/s, identical grad norm;
-    # profiles/fused_expert_stats_ab_r03.json)
-    fused_expert_grad_stats: bool = os.environ.get("DLGM_FUSED_XSTATS", "1") != "0"
+    # A/B on Mixtral 2-layer: 133.2k -> 136.3k tokens/s, identical grad norm (profiles/fused_expert_stats_ab_r03.json)
+    fused_expert_grad_stats: bool = True
     nvme_path: Optional[str] = None
+    param_nvme_path: Optional[str] = None  # offload_param.nvme_path (defaults to nvme_path)
     # ZeRO-2/3 gradients: True = accumulate fp32 locally and reduce-scatter once per optimizer step;
     # False = reduce-scatter every micro-batch (DeepSpeed); "hbm" = True when GA > 1 and the full fp32
     # gradient fits in local_grad_hbm_fraction of the device
@@ -148,7 +154,7 @@ class EngineConfig:
     # while the caches fit in this fraction of HBM (Llama-3-8B: 14 GiB) and in what the HBM plan leaves
     tcache_hbm_fraction: float = 0.08
     # W^T cache also for expert-stacked [E, out, in] weights of never-gathered groups (expert dX GEMMs read
-    # K-contiguous weights), within tcache_hbm_fraction of the device (env DLGM_EXPERT_WT=0 turns it off)
+    # K-contiguous weights), within tcache_hbm_fraction of the device
     expert_weight_cache: bool = True
     init_device: str = "auto"  # "cpu" gives bit-identical init on any device (tests); auto: cpu below 1e9 params
     # replay the GA micro-batches of a step (forward + backward + gradient accumulation) as ONE captured
@@ -215,6 +221,14 @@ class _Scaled:
 
     def __init__(self, t: torch.Tensor, factor: float, keep: Any = None):
         self.t, self.factor, self.keep = t, factor, keep
+
+
+class _MeshRS:
+    """Pending mesh reduce-scatter of a pooled bf16 gradient buffer (already accumulated into the shard by the
+    reduce kernel): the buffer returns to the pool once the collective completed."""
+
+    def __init__(self, src: torch.Tensor):
+        self.src = src
 
 
 class LossScaler:
@@ -344,6 +358,9 @@ class ZeroEngine:
             g.gfull_off = goff
             goff += g.numel if g.P > 1 else 0
         self.gfull_total = goff
+        self.mesh = None
+        self.ep_mesh = None
+        self._init_mesh(model_cfg)
         # compute dtype: bf16, or fp16 for the DeepSpeed "fp16" block -- every HIP kernel has an f16
         # instantiation (f16 MFMA in attention) and the dynamic loss scaler guards the fp16 range
         self.dtype = torch.float16 if cfg.fp16 else torch.bfloat16
@@ -357,7 +374,7 @@ class ZeroEngine:
         self._pver = 0  # bumped whenever the bf16 compute copy changes
         self._tcache: Dict[int, Tuple[int, Dict[str, torch.Tensor]]] = {}
         self._tnames: Dict[int, List[Tuple[str, Tuple[int, ...]]]] = {}
-        self._expert_wt = cfg.expert_weight_cache and os.environ.get("DLGM_EXPERT_WT", "1") != "0"
+        self._expert_wt = cfg.expert_weight_cache
         if cfg.transposed_weight_cache:
             # 2-D weights always; expert-stacked [E, out, in] weights within tcache_hbm_fraction of the device
             budget = (cfg.tcache_hbm_fraction * torch.cuda.get_device_properties(device).total_memory
@@ -410,6 +427,51 @@ class ZeroEngine:
         self.timers = PhaseTimers(device, enabled=cfg.wall_clock_breakdown)
         self.hooks: List[Any] = []  # callables(engine, metrics) after each step (NaN trap, monitors)
         self.pre_step_hooks: List[Any] = []  # callables(engine) before the optimizer touches master/m/v
+
+    def _init_mesh(self, model_cfg: ModelConfig) -> None:
+        """Build the xGMI mesh heaps (cfg.xgmi_mesh == "on"): the world heap holds this rank's bf16 parameter
+        partition (peers pull their gathers from it) and the reduce-scatter slots; the EP heap the token slots."""
+        c = self.cfg
+        if c.xgmi_mesh not in ("on", "off"):
+            raise ValueError(f"xgmi_mesh must be 'on' or 'off', got {c.xgmi_mesh!r}")
+        if c.xgmi_mesh != "on" or not self.is_cuda_dev() or self.W == 1:
+            return
+        if self.comm.backend not in ("nccl", "gloo") or c.offload_optimizer != "none" or c.offload_param != "none":
+            return  # shadow ranks / host-resident partitions keep the RCCL path
+        from .xgmi_mesh import XgmiMesh, rs_region_bytes
+        dense = [g for g in self.groups if self._mesh_group(g)]
+        regions = {"p16": (self.shard_total * 2, 1)}
+        if dense and self.stage in (2, 3):
+            regions["rs"] = (rs_region_bytes(self.W, max(g.shard_numel for g in dense)), 2)
+        self.mesh = XgmiMesh(self.comm, self.device, regions, c.mesh_timeout_s)
+        if self.ep_size > 1 and self.ep_comm is not None and self.ep_comm.world > 1:
+            from .ep import MeshExpertDispatcher
+            dt = torch.float16 if c.fp16 else torch.bfloat16
+            self.ep_mesh = MeshExpertDispatcher(self.ep_comm, model_cfg.n_experts, self.device,
+                                                c.tokens_per_micro * model_cfg.top_k, model_cfg.d_model, dt,
+                                                c.ep_capacity_factor, timeout_s=c.mesh_timeout_s)
+
+    def is_cuda_dev(self) -> bool:
+        return self.device.type == "cuda"
+
+    def _mesh_group(self, g: "FlatGroup") -> bool:
+        """Dense group partitioned over the whole world: its gathers / reductions can ride the world mesh."""
+        return g.kind != "expert" and g.P == self.W and g.P > 1 and g.comm is self.comm
+
+    def _mesh_ok(self, g: "FlatGroup", t: torch.Tensor) -> bool:
+        return (self.mesh is not None and self._mesh_group(g)
+                and t.numel() * t.element_size() >= self.cfg.mesh_min_bytes)
+
+    def check_transport(self) -> None:
+        """Raise if a mesh wait timed out; warn once if an EP dispatch overflowed its capacity (host reads)."""
+        for m in (self.mesh, self.ep_mesh.mesh if self.ep_mesh is not None else None):
+            if m is not None:
+                m.check()
+        if self.ep_mesh is not None and self.ep_mesh.overflowed() and not getattr(self, "_ovf_warned", False):
+            import warnings
+            self._ovf_warned = True
+            warnings.warn(f"mesh EP dispatch overflowed its receive capacity ({self.ep_mesh.C} rows, "
+                          f"ep_capacity_factor {self.cfg.ep_capacity_factor}): dropped rows got zero expert output")
 
     def _split_persistent(self, groups, stages):
         """stage3_param_persistence_threshold: move each unit's small tensors (norm weights, biases) into a
@@ -466,7 +528,7 @@ class ZeroEngine:
         self.param_nvme = None
         if self.param_host and self.cfg.offload_param == "nvme":
             from .offload import NvmeParamStore
-            self.param_nvme = NvmeParamStore(n, self.dtype, self.cfg.nvme_path, self.rank,
+            self.param_nvme = NvmeParamStore(n, self.dtype, self.cfg.param_nvme_path or self.cfg.nvme_path, self.rank,
                                              max(g.shard_numel for g in self.groups),
                                              buffer_count=self.cfg.param_buffer_count, cuda=self.is_cuda,
                                              aio_threads=self.cfg.aio_threads,
@@ -478,6 +540,8 @@ class ZeroEngine:
             self.p16_shard = torch.zeros(n, dtype=self.dtype, pin_memory=self.is_cuda)
             self._h2d = torch.cuda.Stream(dev) if self.is_cuda else None
             self._p16_ready = None  # event: host bf16 partition final (after the device AdamW's D2H)
+        elif self.mesh is not None:  # peers pull their gathers straight out of this rank's heap
+            self.p16_shard = self.mesh.region_tensor("p16", self.dtype, n)
         else:
             self.p16_shard = torch.zeros(n, dtype=self.dtype, device=dev)
         self.p16_full = None
@@ -544,7 +608,20 @@ class ZeroEngine:
         elif self.param_host:
             self._p16_to_host()
         else:
+            self._mesh_quiesce()
             ops.cast_f32_bf16_(self.p16_shard, self.master)  # bf16 or fp16 compute copy
+            self._mesh_publish()
+
+    def _mesh_quiesce(self) -> None:
+        """Mesh: before this rank overwrites its parameter partition, every rank finished its reads of it."""
+        if self.mesh is not None:
+            cur = torch.cuda.current_stream(self.device)
+            cur.wait_stream(self.mesh.stream("ag"))
+            self.mesh.quiesce()
+
+    def _mesh_publish(self) -> None:
+        if self.mesh is not None:
+            self.mesh.publish()
 
     def _p16_to_host(self) -> None:
         """offload_param with the optimizer on the device: bf16(master) chunk by chunk into a device scratch,
@@ -608,8 +685,9 @@ class ZeroEngine:
 
     # ------------------------------------------------------------------ params
     def _all_gather(self, g: FlatGroup, out: torch.Tensor, shard: torch.Tensor) -> Handle:
-        if self.cfg.mesh_allgather:
-            return g.gcomm.all_gather_mesh(out, shard, async_op=True)
+        if self._mesh_ok(g, out):
+            m = self.mesh
+            return m.run_async(lambda: m.all_gather_pull(out, shard), [out])
         return g.gcomm.all_gather(out, shard, async_op=True)
 
     def _shard16(self, g: FlatGroup) -> torch.Tensor:
@@ -776,7 +854,15 @@ class ZeroEngine:
             # EP size so expert grads are the global mean like the dense grads (which are AVG-reduced)
             tgt.mul_(1.0 / self.ep_size)
         avg, post = not self.cfg.prescale_gradients, self._post(g)
-        if g.P > 1 and self.local_grads and self.cfg.comm_dtype != tgt.dtype:
+        if (g.P > 1 and self.local_grads and self.cfg.comm_dtype == torch.bfloat16 and tgt.dtype == torch.float32
+                and self._mesh_ok(g, tgt)):
+            # mesh: the fp32 accumulator is cast to bf16 on the fly as it is pushed; the reduce writes the shard
+            shard_tgt = self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
+            scale = (1.0 / g.comm.world if avg else 1.0) * post
+            m = self.mesh
+            h = m.run_async(lambda: m.reduce_scatter(shard_tgt, tgt, scale, False), [tgt, shard_tgt], "rs")
+            pending.append((h, _Scaled(shard_tgt, 1.0, tgt)))
+        elif g.P > 1 and self.local_grads and self.cfg.comm_dtype != tgt.dtype:
             # ZeRO-2/3 local accumulation: one reduce-scatter per step in comm_dtype (half the bytes of
             # fp32), then the shard is written (beta = 0) from the reduced chunk
             src = tgt.to(self.cfg.comm_dtype)
@@ -801,6 +887,12 @@ class ZeroEngine:
         beta = 0.0 if first_micro else 1.0
         alpha = (1.0 / self.ep_size if g.kind == "expert" else 1.0) * self._post(g)
         shard_tgt = self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
+        if gbuf.dtype == torch.bfloat16 and self.cfg.comm_dtype == torch.bfloat16 and self._mesh_ok(g, gbuf):
+            scale = alpha * (1.0 / g.comm.world if not self.cfg.prescale_gradients else 1.0)
+            m = self.mesh
+            h = m.run_async(lambda: m.reduce_scatter(shard_tgt, gbuf, scale, beta == 1.0), [gbuf, shard_tgt], "rs")
+            pending.append((h, _MeshRS(gbuf)))
+            return
         src = gbuf
         if self.cfg.comm_dtype != gbuf.dtype:
             src = gbuf.to(self.cfg.comm_dtype)
@@ -828,6 +920,8 @@ class ZeroEngine:
             if isinstance(payload, _Scaled):
                 if payload.factor != 1.0:
                     payload.t.mul_(payload.factor)
+            elif isinstance(payload, _MeshRS):
+                self._release_gbuf(payload.src)  # the push has read it: back to the pool
             elif isinstance(payload, tuple):
                 shard_tgt, out, beta, src, alpha = payload[:5]  # payload[5]: input kept alive until here
                 ops.accumulate_(shard_tgt, out, alpha, beta)
@@ -841,7 +935,7 @@ class ZeroEngine:
         if self.cfg.prescale_gradients:
             gs /= self.cfg.gradient_predivide_factor  # pre-divided before the SUM reductions
         return StepContext(batch=B, seq_len=S, input_ids=ids, labels=labels, grad_scale=gs, rope=self.rope,
-                           ep_group=self.ep_comm, sp_group=self.sp_comm,
+                           ep_group=self.ep_comm, sp_group=self.sp_comm, ep_dispatcher=self.ep_mesh,
                            loss_scale=self.scaler.state[0:1] if self.scaler is not None else None)
 
     def micro_step(self, ids: torch.Tensor, labels: torch.Tensor, first: bool, last: bool) -> torch.Tensor:
@@ -1018,6 +1112,7 @@ class ZeroEngine:
         if self.offload is not None:
             self._offload_step(lr, float(sst[1]) if sst is not None else 1.0)
         else:
+            self._mesh_quiesce()
             ops.adamw_step_(self.master, self.exp_avg, self.exp_avg_sq, self.grad_shard,
                             None if self.param_host else self.p16_shard,
                             self.stats, lr=lr,
@@ -1025,6 +1120,7 @@ class ZeroEngine:
                             step=self.step_count, grad_scale=1.0, max_norm=cfg.grad_clip, scale_state=sst)
             if self.param_host:
                 self._p16_to_host()
+            self._mesh_publish()
         self._pver += 1  # the compute copy changes below: transposed caches are stale
         if self.stage == 3:
             self._live.clear()  # (micro_step(last=True) already dropped them; direct callers may not have)
@@ -1087,12 +1183,29 @@ class ZeroEngine:
         per-phase timers (host-side event bookkeeping). The fp16 loss scale is a device word
         (LossScaler.state), so the fp16 path replays the same graph at every scale."""
         c = self.cfg
-        from ..ops import gemm_mfma as gm
-        moe_ok = not self.has_experts or (self.ep_size == 1 and gm.GROUPED)
-        return (c.hip_graphs and self.is_cuda and self.W == 1 and moe_ok and self.offload is None
+        moe_ok = not self.has_experts or self.ep_size == 1 or self.ep_mesh is not None
+        return (c.hip_graphs and self.is_cuda and (self.W == 1 or self._loop_on_mesh()) and moe_ok
+                and self.offload is None
                 and not self.param_host
                 and not c.cpu_checkpointing and not self.timers.enabled
                 and self.sp_size == 1 and self._graph_state != "failed")
+
+    def _loop_on_mesh(self) -> bool:
+        """W > 1: does every collective of the micro-batch loop ride the device-driven mesh (so the loop has
+        no host-side collective and can be captured)? Dense groups partitioned over the world (gathers and
+        bf16 reductions on the mesh), experts on their EP ranks only (EP == W: nothing to reduce), no
+        replicated group (those all-reduce on RCCL), ZeRO-2/3."""
+        if self.mesh is None or self.stage not in (2, 3) or self.cfg.comm_dtype != torch.bfloat16:
+            return False
+        if self.cfg.mesh_min_bytes > 0 or self.sp_size > 1:
+            return False
+        for g in self.groups:
+            if g.kind == "expert":
+                if g.P > 1 or g.comm.world > 1 or self.ep_mesh is None:
+                    return False
+            elif not self._mesh_group(g):
+                return False
+        return True
 
     def _graphed_micro_loop(self, micro_batches: Sequence[Tuple[torch.Tensor, torch.Tensor]]) -> None:
         """Capture the micro-batch loop once per batch shape (after one eager warm-up step that creates
@@ -1117,18 +1230,28 @@ class ZeroEngine:
             torch.cuda.synchronize(self.device)
             torch.cuda.empty_cache()  # hand the eager step's cached activation blocks to the graph pool
             graph = torch.cuda.CUDAGraph()
+            err = None
             try:
                 with torch.cuda.graph(graph):
                     self._micro_loop(static)
             except Exception as e:  # an op that cannot be captured: stay eager for the rest of the run
+                err = f"{type(e).__name__}: {e}"
+            if self.W > 1:
+                # every rank replays the same collective sequence: capture is all or nothing (host collective,
+                # outside the captured region, once per batch shape)
+                ok = torch.tensor([0.0 if err else 1.0], device=self.device)
+                self.comm.all_reduce(ok, async_op=False).wait()
+                if float(ok) < self.W and err is None:
+                    err = "another rank could not capture its micro-batch loop"
+            if err is not None:
                 self._graph_state = "failed"
                 self._tcache.clear()
                 import warnings
-                warnings.warn(f"HIP graph capture failed ({type(e).__name__}: {e}); running eagerly")
+                warnings.warn(f"HIP graph capture failed ({err}); running eagerly")
                 torch.cuda.synchronize(self.device)
                 self._micro_loop(micro_batches)
                 return
-            self._graph = {"key": key, "graph": graph, "static": static}
+            self._graph = {"key": key, "graph": graph, "static": static, "xstats_ok": self._xstats_ok}
             g = self._graph
         for (si, sl), (ids, labels) in zip(g["static"], micro_batches):
             if si.data_ptr() != ids.data_ptr():
@@ -1136,6 +1259,8 @@ class ZeroEngine:
                 sl.copy_(labels, non_blocking=True)
         g["graph"].replay()
         self._tcache = {gi: (self._pver, c) for gi, (_, c) in self._tcache.items()}
+        # the captured loop's last micro-batch tallied the fused expert statistics iff it did at capture time
+        self._xstats_ok = g["xstats_ok"]
 
     # ------------------------------------------------------------------ helpers
     def full_params(self) -> Dict[str, torch.Tensor]:

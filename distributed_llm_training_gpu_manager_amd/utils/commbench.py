@@ -13,9 +13,10 @@ import torch
 
 from ..parallel.comm import DONE, Comm
 
-FACTOR = {"all_gather": lambda w: (w - 1) / w, "mesh_all_gather": lambda w: (w - 1) / w,
-          "ipc_mesh_all_gather": lambda w: (w - 1) / w, "reduce_scatter": lambda w: (w - 1) / w,
+FACTOR = {"all_gather": lambda w: (w - 1) / w, "ipc_mesh_all_gather": lambda w: (w - 1) / w,
+          "reduce_scatter": lambda w: (w - 1) / w, "ipc_mesh_reduce_scatter": lambda w: (w - 1) / w,
           "all_to_all": lambda w: (w - 1) / w, "all_reduce": lambda w: 2 * (w - 1) / w}
+MESH_OPS = ("ipc_mesh_all_gather", "ipc_mesh_reduce_scatter")
 
 
 def run(op: str, comm: Comm, nbytes: int, device, dtype, iters: int, warmup: int) -> float:
@@ -35,18 +36,24 @@ def _run(op: str, comm: Comm, nbytes: int, device, dtype, iters: int, warmup: in
         inp = torch.randn(n // W, device=device).to(dtype)
         out = torch.empty(n, device=device, dtype=dtype)
         fn = lambda: comm.all_gather(out, inp, async_op=False)  # noqa: E731
-    elif op == "mesh_all_gather":
-        inp = torch.randn(n // W, device=device).to(dtype)
-        out = torch.empty(n, device=device, dtype=dtype)
-        fn = lambda: comm.all_gather_mesh(out, inp, async_op=True)  # noqa: E731
     elif op == "ipc_mesh_all_gather":
-        # peer-write mesh over HIP IPC symmetric buffers (parallel/xgmi_mesh.py); opt-in, GPU only: not part of
-        # bench.py's default post-timing sweep (a new transport must not put the result line at risk)
+        # device-driven pull from every peer's symmetric heap (parallel/xgmi_mesh.py); GPU only. bench.py runs the
+        # mesh rows in a child process after its result line is out (a new transport never risks the number)
         from ..parallel.xgmi_mesh import XgmiMesh
-        inp = torch.randn(n // W, device=device).to(dtype)
-        mesh = XgmiMesh(comm, n * esz, device)
+        m = n // W * esz
+        mesh = XgmiMesh(comm, device, {"p16": (m, 1)})
         mesh_ref.append(mesh)
-        fn = lambda: (mesh.all_gather(inp), DONE)[1]  # noqa: E731
+        shard = mesh.region_tensor("p16", dtype, n // W)
+        shard.copy_(torch.randn(n // W, device=device).to(dtype))
+        out = torch.empty(n, device=device, dtype=dtype)
+        fn = lambda: (mesh.all_gather_pull(out, shard), DONE)[1]  # noqa: E731
+    elif op == "ipc_mesh_reduce_scatter":
+        from ..parallel.xgmi_mesh import XgmiMesh, rs_region_bytes
+        mesh = XgmiMesh(comm, device, {"rs": (rs_region_bytes(W, n // W), 2)})
+        mesh_ref.append(mesh)
+        inp = torch.randn(n, device=device).to(dtype)
+        out = torch.empty(n // W, device=device, dtype=dtype)
+        fn = lambda: (mesh.reduce_scatter(out, inp, 1.0, False), DONE)[1]  # noqa: E731
     elif op == "reduce_scatter":
         inp = torch.randn(n, device=device).to(dtype)
         out = torch.empty(n // W, device=device, dtype=dtype)
@@ -77,7 +84,7 @@ def _run(op: str, comm: Comm, nbytes: int, device, dtype, iters: int, warmup: in
 
 
 def sweep(comm: Comm, device,
-          ops: Sequence[str] = ("all_gather", "mesh_all_gather", "reduce_scatter", "all_reduce", "all_to_all"),
+          ops: Sequence[str] = ("all_gather", "reduce_scatter", "all_reduce", "all_to_all"),
           sizes_mb: Sequence[float] = (16, 64, 256), dtype=torch.bfloat16, iters: int = 5,
           warmup: int = 2) -> List[Dict]:
     rows = []

@@ -26,7 +26,7 @@ def tuned_files(model: Optional[str] = None) -> List[str]:
 
 def enable_tuned_gemms(model: Optional[str] = None) -> List[str]:
     """Enable TunableOp in read-only mode with the tuned results for `model` (all files if None)."""
-    if not torch.cuda.is_available() or os.environ.get("DLGM_TUNED_GEMMS", "1") == "0":
+    if not torch.cuda.is_available():
         return []
     files = [f for f in tuned_files(model) if f not in _loaded]
     if not files and not _loaded:

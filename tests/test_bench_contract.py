@@ -69,7 +69,21 @@ def test_bench_torchrun_two_ranks():
     _check(out, 2, 2, 1)
     assert out["extra"]["zero3_allgathers_per_step"] > 0  # partitioned: the residency plan gathers once per unit
     ops = {r["op"] for r in out["extra"]["comm_busbw"]}  # the post-timing RCCL/xGMI sweep (gloo here)
-    assert ops == {"all_gather", "mesh_all_gather", "reduce_scatter", "all_reduce", "all_to_all"}
+    assert ops == {"all_gather", "reduce_scatter", "all_reduce", "all_to_all"}
+
+
+def test_bench_mesh_sweep_child_keeps_one_result_line():
+    """--mesh-sweep on: after the result line each rank starts tools/mesh_sweep.py as a child process (a fresh
+    process group on an agreed port); its report goes to stderr, stdout still holds exactly one JSON line."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", *TINY[:-2], "--comm-sweep", "off",
+           "--mesh-sweep", "on"]
+    res = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
+    assert res.returncode == 0, res.stderr[-3000:]
+    assert len([ln for ln in res.stdout.splitlines() if ln.startswith("{")]) == 1, res.stdout
+    sweep = [ln for ln in res.stderr.splitlines() if ln.startswith("[mesh-sweep] ")]
+    assert len(sweep) == 1, res.stderr[-3000:]
+    assert json.loads(sweep[0][len("[mesh-sweep] "):])["world"] == 2
 
 
 TINY = ["--steps", "2", "--warmup", "1", "--model", "llama-tiny", "--seq", "64", "--ga", "2", "--comm-sweep", "off"]

@@ -329,38 +329,3 @@ def test_zero3_world2_resident_transposed_cache_is_transparent(tmp_path):
         d = (res[True]["params"][k] - v).abs()
         assert float(d.max()) <= 2 * 1e-2 * 3 + 1e-3, k
         assert float((d > 1e-3).float().mean()) < 0.02, k
-
-
-def _mesh_worker(rank, world, port, out_path):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    comm = Comm()
-    x = torch.arange(5, dtype=torch.float32) + 10 * rank
-    out = torch.empty(5 * world)
-    comm.all_gather_mesh(out, x).wait()
-    ref = torch.cat([torch.arange(5, dtype=torch.float32) + 10 * r for r in range(world)])
-    assert torch.equal(out, ref)
-    res = {}
-    for mesh in (False, True):
-        torch.manual_seed(0)
-        cfg = _cfg(3, 1)
-        cfg.mesh_allgather = mesh
-        eng = ZeroEngine(get_config("llama-tiny"), cfg, torch.device("cpu"), Comm())
-        for mbs in _data("llama-tiny", 2, world):
-            t = mbs[rank]
-            eng.train_step([(t[:, :-1], t[:, 1:])])
-        res[mesh] = eng.full_params()
-    if rank == 0:
-        torch.save(res, out_path)
-    dist.barrier()
-    dist.destroy_process_group()
-
-
-def test_mesh_allgather_matches_ring_world3(tmp_path):
-    """The direct mesh all-gather (batched point-to-point with every peer) equals the ring all-gather, as a
-    collective and as the ZeRO-3 parameter gather of a training run."""
-    out = str(tmp_path / "mesh.pt")
-    mp.spawn(_mesh_worker, args=(3, _free_port(), out), nprocs=3, join=True)
-    res = torch.load(out, weights_only=True)
-    for k, v in res[False].items():
-        assert torch.equal(res[True][k], v), k

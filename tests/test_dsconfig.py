@@ -46,3 +46,33 @@ def test_aio_and_mi355x_blocks():
     assert cfg.hip_graphs is False
     assert cfg.comm_dtype == torch.float32
     assert any("A20" in n for n in notes)
+
+
+def test_gather_16bit_weights_key_controls_module_capture(tmp_path):
+    """zero_optimization.stage3_gather_16bit_weights_on_model_save (DeepSpeed default False) decides whether a
+    stage-3 save gathers the 16-bit module into mp_rank_00_model_states.pt."""
+    from distributed_llm_training_gpu_manager_amd.ckpt.checkpoint import AsyncCheckpointer
+    from distributed_llm_training_gpu_manager_amd.models import get_config
+    from distributed_llm_training_gpu_manager_amd.parallel.zero import ZeroEngine
+    base = {"zero_optimization": {"stage": 3}, "train_micro_batch_size_per_gpu": 1}
+    cfg, _ = engine_config_from_ds(base, seq_len=32)
+    assert cfg.gather_16bit_weights_on_model_save is False
+    for flag in (False, True):
+        ds = {**base, "zero_optimization": {"stage": 3, "stage3_gather_16bit_weights_on_model_save": flag}}
+        cfg, _ = engine_config_from_ds(ds, seq_len=32)
+        assert cfg.gather_16bit_weights_on_model_save is flag
+        cfg.init_device = "cpu"
+        eng = ZeroEngine(get_config("llama-tiny"), cfg, torch.device("cpu"))
+        d = tmp_path / str(flag)
+        ck = AsyncCheckpointer(eng, str(d), shm=False)
+        ck.save(1, {"step": 1}, blocking=True)
+        ck.close()
+        meta = torch.load(d / "global_step1" / "mp_rank_00_model_states.pt", weights_only=True)
+        assert (meta.get("module") is not None) is flag
+
+
+def test_offload_param_nvme_path_is_its_own():
+    ds = {"zero_optimization": {"stage": 3, "offload_optimizer": {"device": "nvme", "nvme_path": "/nvme0"},
+                                "offload_param": {"device": "nvme", "nvme_path": "/nvme1"}}}
+    cfg, _ = engine_config_from_ds(ds, seq_len=32)
+    assert cfg.nvme_path == "/nvme0" and cfg.param_nvme_path == "/nvme1"

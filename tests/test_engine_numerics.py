@@ -71,19 +71,6 @@ def test_mixtral_manual_backward_matches_autograd_gpu():
     _check("cuda", "mixtral-tiny", tol=1e-1)
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("grouped,wgrad", [(True, True), (False, True), (False, False)])
-def test_mixtral_expert_gemm_modes_match_autograd_gpu(monkeypatch, grouped, wgrad):
-    """Experts as grouped MFMA launches (device offsets from moe_permute, no host read of the counts; with GA 2
-    the deferred grouped dW over both micro-batches), the grouped weight gradients only, and the per-expert
-    hipBLASLt loop."""
-    from distributed_llm_training_gpu_manager_amd.ops import gemm_mfma as gm
-    monkeypatch.setattr(gm, "CAPACITY", False)
-    monkeypatch.setattr(gm, "GROUPED", grouped)
-    monkeypatch.setattr(gm, "GROUPED_WGRAD", wgrad)
-    _check("cuda", "mixtral-tiny", tol=1e-1)
-
-
 @pytest.mark.parametrize("aux", [0.0, 0.02])
 def test_moe_block_exact_in_fp32(aux):
     """The hand-written MoE forward/backward (router top-2, dispatch, experts, combine, aux loss)
@@ -309,17 +296,13 @@ def test_llama_chunked_head_matches_autograd_gpu(monkeypatch):
     _check("cuda")
 
 
-@pytest.mark.parametrize("kmajor", [False, True])
-def test_mixtral_grouped_deferred_wgrad_matches_per_micro_batch_cpu(monkeypatch, kmajor):
+def test_mixtral_grouped_deferred_wgrad_matches_per_micro_batch_cpu(monkeypatch):
     """The grouped expert path (device offsets) with the weight gradients deferred to the step's last
     micro-batch -- one segmented grouped dW GEMM per weight over every stashed micro-batch's rows -- equals the
     per-micro-batch grouped dW. CPU run of the same code (grouped ops' reference path)."""
     from distributed_llm_training_gpu_manager_amd.models.mixtral import MixtralBlock
     from distributed_llm_training_gpu_manager_amd.parallel.zero import EngineConfig, ZeroEngine
-    from distributed_llm_training_gpu_manager_amd.ops import gemm_mfma as gm
-    monkeypatch.setattr(gm, "CAPACITY", False)
-    monkeypatch.setattr(gm, "KMAJOR_DW", kmajor)  # stash transposed into the aligned re-layout, or token-major
-    monkeypatch.setattr(MixtralBlock, "_grouped", lambda self, x, wgrad=False: True)
+    monkeypatch.setattr(MixtralBlock, "_grouped", lambda self, x: True)
     mc = get_config("mixtral-tiny")
     g = torch.Generator().manual_seed(4)
     data = [torch.randint(0, mc.vocab_size, (2, 33), generator=g) for _ in range(3)]
@@ -341,17 +324,13 @@ def test_mixtral_grouped_deferred_wgrad_matches_per_micro_batch_cpu(monkeypatch,
         assert err < 1e-2, (k, err)
 
 
-@pytest.mark.parametrize("ga,kmajor", [(1, True), (3, True), (3, False)])
-def test_mixtral_fused_expert_grad_stats_match_grad_stats_cpu(monkeypatch, ga, kmajor):
+@pytest.mark.parametrize("ga", [1, 3])
+def test_mixtral_fused_expert_grad_stats_match_grad_stats_cpu(monkeypatch, ga):
     """The expert gradients' statistics tallied by the last grouped dW launch of the step (non-deferred at
-    GA 1, the K-major deferred flush at GA 3) equal ops.grad_stats over the expert groups; the token-major
-    segmented flush does not tally and falls back to the separate pass."""
+    GA 1, the K-major deferred flush at GA 3) equal ops.grad_stats over the expert groups."""
     from distributed_llm_training_gpu_manager_amd.models.mixtral import MixtralBlock
     from distributed_llm_training_gpu_manager_amd.parallel.zero import EngineConfig, ZeroEngine
-    from distributed_llm_training_gpu_manager_amd.ops import gemm_mfma as gm
-    monkeypatch.setattr(gm, "CAPACITY", False)
-    monkeypatch.setattr(gm, "KMAJOR_DW", kmajor)
-    monkeypatch.setattr(MixtralBlock, "_grouped", lambda self, x, wgrad=False: True)
+    monkeypatch.setattr(MixtralBlock, "_grouped", lambda self, x: True)
     mc = get_config("mixtral-tiny")
     g = torch.Generator().manual_seed(5)
     data = [torch.randint(0, mc.vocab_size, (2, 33), generator=g) for _ in range(ga)]
@@ -361,7 +340,7 @@ def test_mixtral_fused_expert_grad_stats_match_grad_stats_cpu(monkeypatch, ga, k
     for i, t in enumerate(data):
         eng.micro_step(t[:, :-1], t[:, 1:], first=i == 0, last=i == ga - 1)
     fused = eng._xstats_ok
-    assert fused == (ga == 1 or kmajor)
+    assert fused
     eng._global_grad_stats()
     st_fused = eng.stats[:2].clone()
     eng._xstats_ok = False

@@ -212,9 +212,8 @@ def _defer_worker(rank, world, port, model, dw, out):
             flushes[0] += 1
             return orig(self, g)
         return spy
-    # the per-expert path's flush, or the capacity layout's (DLGM_MOE_GROUPED=cap)
+    # the per-expert (CPU) path's flush
     mixtral.MixtralBlock._flush_wgrad = counted(mixtral.MixtralBlock._flush_wgrad)
-    mixtral.MixtralBlock._flush_wgrad_cap = counted(mixtral.MixtralBlock._flush_wgrad_cap)
     _init(rank, world, port)
     eng = ZeroEngine(_model(model), _cfg(3, 3, expert_parallel_size=world, defer_expert_wgrad=dw),
                      torch.device("cpu"), Comm())

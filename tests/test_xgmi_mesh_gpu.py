@@ -1,9 +1,17 @@
-"""Peer-write mesh all-gather over HIP IPC symmetric buffers (parallel/xgmi_mesh.py, csrc/kernels/xgmi_mesh.hip).
+"""The device-driven xGMI mesh transport (parallel/xgmi_mesh.py, csrc/kernels/xgmi_mesh.hip) and the EP dispatcher
+built on it (parallel/ep.py MeshExpertDispatcher).
 
-Ranks share one MI355X here (IPC within one device; gloo carries the handle exchange and the barriers -- RCCL
-refuses two ranks on one GPU): every rank exports its buffer, maps every peer's, and its push kernel writes its
-shard into all peers' buffers. Checked bit-exactly against the concatenation of every rank's shard, over several
-consecutive gathers (the entry barrier must keep a push from overwriting a slot a peer is still reading)."""
+Ranks share one MI355X here (IPC within one device; gloo carries the handle exchange -- RCCL refuses two ranks on
+one GPU). Every rank maps every peer's heap and the kernels move data and flags exactly as on an 8-GPU node; only
+the wire differs. Checks, all bit-exact:
+* all-gather (pull): == concatenation of every rank's shard, over several versions (quiesce / publish ordering);
+* reduce-scatter (push + fp32 reduce): == the fp32 rank-order sum of the bf16-rounded chunks, times the scale,
+  (+ the previous value when accumulating), from fp32 and from bf16 inputs, several epochs through 2 slots;
+* EP dispatch / redispatch / combine: == the RCCL-path dispatcher (ExpertDispatcher over the same ranks), with an
+  expert that receives no rows, and with a receive capacity too small (dropped rows come back as zeros, the overflow
+  word is raised on every rank);
+* the MoE EP micro-batch path replays from a captured HIP graph.
+"""
 import os
 import socket
 
@@ -23,35 +31,148 @@ def _free_port() -> int:
     return port
 
 
-def _shard(rank, it, n):
-    g = torch.Generator().manual_seed(1000 * it + rank)
-    return torch.randn(n, generator=g).to(torch.bfloat16)
-
-
-def _worker(rank, world, port, n, iters, out_path):
+def _init(rank, world, port):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    from distributed_llm_training_gpu_manager_amd.parallel.comm import Comm
-    from distributed_llm_training_gpu_manager_amd.parallel.xgmi_mesh import XgmiMesh
-    mesh = XgmiMesh(Comm(), world * n * 2, dev)
-    ok = True
-    for it in range(iters):
-        got = mesh.all_gather(_shard(rank, it, n).to(dev)).cpu()
-        want = torch.cat([_shard(r, it, n) for r in range(world)])
-        ok = ok and torch.equal(got, want)
-    mesh.close()
+    return dev
+
+
+def _finish(rank, ok, out_path, extra=None):
     flag = torch.tensor([1 if ok else 0])
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
     if rank == 0:
-        torch.save({"ok": int(flag)}, out_path)
+        torch.save({"ok": int(flag), **(extra or {})}, out_path)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n", [(2, 4096), (4, 1 << 20)])
-def test_ipc_mesh_all_gather_matches_concat(tmp_path, world, n):
+def _vec(seed, n, dtype=torch.bfloat16):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(n, generator=g).to(dtype)
+
+
+def _zero_worker(rank, world, port, n, iters, out_path):
+    dev = _init(rank, world, port)
+    from distributed_llm_training_gpu_manager_amd.parallel.comm import Comm
+    from distributed_llm_training_gpu_manager_amd.parallel.xgmi_mesh import XgmiMesh, rs_region_bytes
+    mesh = XgmiMesh(Comm(), dev, {"p16": (n * 2, 1), "rs": (rs_region_bytes(world, n), 2)}, timeout_s=20)
+    shard = mesh.region_tensor("p16", torch.bfloat16, n)
+    ok = True
+    msgs = []
+    for it in range(iters):
+        # optimizer-style update of this rank's partition: quiesce (peers done with the old version), write, publish
+        mesh.quiesce()
+        shard.copy_(_vec(1000 * it + rank, n).to(dev))
+        mesh.publish()
+        out = torch.empty(world * n, dtype=torch.bfloat16, device=dev)
+        mesh.all_gather_pull(out, shard)
+        want = torch.cat([_vec(1000 * it + r, n) for r in range(world)])
+        if not torch.equal(out.cpu(), want):
+            ok = False
+            msgs.append(f"ag it{it}")
+        # reduce-scatter from fp32 (cast on the fly) and from bf16, accumulating into an fp32 shard
+        for src_dtype in (torch.float32, torch.bfloat16):
+            xs = [_vec(7 * it + 100 * r + 1, world * n, torch.float32) for r in range(world)]
+            if src_dtype == torch.bfloat16:
+                xs = [x.to(torch.bfloat16) for x in xs]
+            prev = _vec(99 + rank + it, n, torch.float32)
+            acc = it % 2 == 1
+            scale = 1.0 / world
+            o = prev.clone().to(dev)
+            mesh.reduce_scatter(o, xs[rank].to(dev), scale, acc)
+            chunks = [x.to(torch.bfloat16).float()[rank * n:(rank + 1) * n] for x in xs]
+            ref = chunks[0].clone()
+            for c in chunks[1:]:
+                ref = ref + c
+            ref = ref * torch.tensor(scale, dtype=torch.float32)
+            if acc:
+                ref = prev + ref
+            if not torch.equal(o.cpu(), ref):
+                ok = False
+                msgs.append(f"rs it{it} {src_dtype} maxdiff {float((o.cpu() - ref).abs().max())}")
+    torch.cuda.synchronize()
+    mesh.check()
+    mesh.close()
+    _finish(rank, ok, out_path, {"msgs": msgs} if rank == 0 else None)
+
+
+@pytest.mark.parametrize("world,n", [(2, 4096), (4, 1 << 18)])
+def test_mesh_all_gather_and_reduce_scatter_bit_exact(tmp_path, world, n):
     out = str(tmp_path / "mesh.pt")
-    mp.spawn(_worker, args=(world, _free_port(), n, 3, out), nprocs=world, join=True)
-    assert torch.load(out, weights_only=True)["ok"] == 1
+    mp.spawn(_zero_worker, args=(world, _free_port(), n, 4, out), nprocs=world, join=True)
+    res = torch.load(out, weights_only=True)
+    assert res["ok"] == 1, res.get("msgs")
+
+
+def _routing(rank, T, K, E, seed, skew):
+    g = torch.Generator().manual_seed(seed + 17 * rank)
+    if skew:  # nearly every slot to expert 0: the owner of expert 0 overflows its capacity
+        topi = torch.zeros(T, K, dtype=torch.long)
+        topi[:, 1] = 1 + torch.randint(0, E - 2, (T,), generator=g)
+    else:  # expert E-1 never chosen (an empty expert on its owner)
+        scores = torch.rand(T, E - 1, generator=g)
+        topi = scores.topk(K, dim=-1).indices
+    return topi
+
+
+def _ep_worker(rank, world, port, E, T, K, D, factor, skew, out_path):
+    dev = _init(rank, world, port)
+    from distributed_llm_training_gpu_manager_amd.ops.moe import moe_permute
+    from distributed_llm_training_gpu_manager_amd.parallel.comm import Comm
+    from distributed_llm_training_gpu_manager_amd.parallel.ep import ExpertDispatcher, MeshExpertDispatcher
+    comm = Comm()
+    ref = ExpertDispatcher(comm, E)
+    mesh = MeshExpertDispatcher(comm, E, dev, T * K, D, torch.bfloat16, capacity_factor=factor, timeout_s=20)
+    C = mesh.C
+    ok, msgs = True, []
+    for it in range(3):
+        topi = _routing(rank, T, K, E, 100 * it, skew).to(dev)
+        offsets, pos, tok = moe_permute(topi, E)
+        counts = (offsets[1:] - offsets[:-1]).long()
+        x = _vec(1000 * it + rank, T * K * D).view(T * K, D).to(dev)
+        xr, cr = ref.dispatch(x, counts, offsets)
+        xm, cm = mesh.dispatch(x, counts, offsets)
+        total = xr.shape[0]
+        keep = min(total, C)
+        if int(cm.nrows) != keep or not torch.equal(xm[:keep].cpu(), xr[:keep].cpu()):
+            ok = False
+            msgs.append(f"dispatch it{it} total {total} C {C} nrows {int(cm.nrows)}")
+        want_off = torch.clamp(cr.local_offsets.cpu(), max=C)
+        if not torch.equal(cm.local_offsets.cpu(), want_off):
+            ok = False
+            msgs.append(f"offsets it{it} {cm.local_offsets.tolist()} vs {want_off.tolist()}")
+        # an "expert" computation on the valid rows; rows past the capacity were never received -> zero back
+        yr = xr * 3 + 1
+        yr[keep:] = 0
+        ym = torch.zeros_like(xm)
+        ym[:keep] = xm[:keep] * 3 + 1
+        outr = ref.combine(yr, cr)
+        outm = mesh.combine(ym, cm)
+        if not torch.equal(outm.cpu(), outr.cpu()):
+            ok = False
+            msgs.append(f"combine it{it}")
+        dy = _vec(5000 + 1000 * it + rank, T * K * D).view(T * K, D).to(dev)
+        dr = ref.redispatch(dy, cr)
+        dm = mesh.redispatch(dy, cm)
+        if not torch.equal(dm[:keep].cpu(), dr[:keep].cpu()):
+            ok = False
+            msgs.append(f"redispatch it{it}")
+    torch.cuda.synchronize()
+    mesh.mesh.check()
+    ovf = mesh.overflowed()
+    if ovf != bool(skew):
+        ok = False
+        msgs.append(f"overflow flag {ovf} (skew {skew})")
+    mesh.close()
+    _finish(rank, ok, out_path, {"msgs": msgs} if rank == 0 else None)
+
+
+@pytest.mark.parametrize("world,E,factor,skew", [(2, 4, 4.0, False), (4, 8, 4.0, False), (4, 4, 4.0, False),
+                                                 (4, 8, 0.5, True)])
+def test_mesh_expert_dispatch_matches_rccl_dispatcher(tmp_path, world, E, factor, skew):
+    out = str(tmp_path / "ep.pt")
+    mp.spawn(_ep_worker, args=(world, _free_port(), E, 96, 2, 128, factor, skew, out), nprocs=world, join=True)
+    res = torch.load(out, weights_only=True)
+    assert res["ok"] == 1, res.get("msgs")

@@ -29,7 +29,8 @@ def train_argv(a, extra):
     return [sys.executable, "-m", "distributed_llm_training_gpu_manager_amd.train", "--model", a.model,
             "--seq-len", str(a.seq), "--micro-batch", "1", "--grad-accum", str(a.ga), "--zero-stage", "3",
             "--lr", "3e-5", *(["--n-layers", str(a.n_layers)] if a.n_layers else []),
-            "--keep-last", str(a.keep_last), "--ckpt-shm", a.ckpt_shm, "--ckpt-disk", str(a.ckpt_disk), *extra]
+            "--keep-last", str(a.keep_last), "--ckpt-shm", a.ckpt_shm, "--ckpt-disk", str(a.ckpt_disk),
+            *a.extra.split(), *extra]
 
 
 def run(argv, timeout):
@@ -122,11 +123,13 @@ def main():
     ap.add_argument("--keep-last", type=int, default=1)
     ap.add_argument("--ckpt-shm", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--ckpt-disk", type=int, default=1, help="0: /dev/shm snapshot tier only (no disk tags)")
+    ap.add_argument("--extra", default="", help="more trainer arguments, e.g. '--shadow-world 8 --shadow-rank 0' "
+                    "(rank 0 of an 8-rank job alone on this GPU: the 70B config-4 drill at true per-rank size)")
     ap.add_argument("--out", default="gpurun_out/drills.json")
     ap.add_argument("--work", default=None)
     a = ap.parse_args()
     work = a.work or tempfile.mkdtemp(prefix="dlgm_drill_")
-    res = {"model": a.model, "n_layers": a.n_layers or "preset", "seq": a.seq, "ga": a.ga,
+    res = {"model": a.model, "n_layers": a.n_layers or "preset", "seq": a.seq, "ga": a.ga, "extra": a.extra,
            "keep_last": a.keep_last, "ckpt_shm": a.ckpt_shm, "ckpt_disk": a.ckpt_disk,
            "data": "synthetic token ids, random-init weights"}
     for d in a.drills.split(","):
