@@ -21,16 +21,19 @@
 //  * Work ordering: causal blocks are launched heaviest-first, and blocks that
 //    share one (batch, kv-head) -- i.e. the same K/V stream -- are grouped on one
 //    XCD (blockIdx % 8 labels an XCD) so the K/V re-reads of the GQA group hit L2.
-//  * Backward = three deterministic passes, no atomics (an atomic-dQ single pass would move
+//  * Backward = two deterministic passes, no atomics (an atomic-dQ single pass would move
 //    2.15 GB of fp32 adds per Llama-3-8B layer at S = 8192, >= 1.65 ms at the chip-wide
 //    float-atomic rate):
-//      delta = rowsum(dO * O);
+//      dQ (first): one workgroup per (b, q head, 128 queries), the forward's structure; it also computes
+//        delta = rowsum(dO * O) for its rows (it holds dO in registers) and writes the [-delta, -lse/scale]
+//        rows dK/dV starts its accumulators from; dS^T is used in place as the B operand of dQ^T += K^T dS^T;
 //      dK/dV: one workgroup per (b, q head, 128 keys), the wave's 32 keys on the MFMA lanes,
 //        K in registers, V in LDS, S^T / dP^T computed with the key on the lane so they feed
 //        dV^T / dK^T as accumulator operands; fp32 per-q-head partials, summed over the GQA
-//        group by gqa_reduce into the packed dqkv;
-//      dQ: one workgroup per (b, q head, 128 queries), the forward's structure, dS^T used in
-//        place as the B operand of dQ^T += K^T dS^T.
+//        group by gqa_reduce into the packed dqkv.
+//    Measured and removed (round 3): a separate delta launch (the fused one saves it), dQ on a side stream beside
+//    dK/dV (2.20 vs 1.92 ms: both fill the chip), dQ from a dS^T stored by dK/dV (dQ 750 -> 519 us but dK/dV
+//    1116 -> 1307 us for 2.15 GB of dS^T writes at the board's power limit: +0.1-0.2 % end to end for +2.3 GiB).
 #include <torch/all.h>
 #include <c10/hip/HIPStream.h>
 #include <cstdlib>
@@ -403,39 +406,6 @@ __global__ __launch_bounds__(kFwdThreads, 2) void flash_fwd_kernel(FwdParams<E> 
 // Backward
 // ----------------------------------------------------------------------------------
 
-// nd[b, hq, q] = -sum_d dO[b,q,hq,d] * O[b,q,hq,d] and nls[b, hq, q] = -lse / scale (nls = nd + B*Hq*S):
-// the start values of the backward's dP and S accumulators, stored ready to use so that the dK/dV
-// loop loads them into the MFMA C operands with no negation or scaling per tile. A row of D bf16 is
-// D/8 lanes x 16 B, so a wave64 covers 64 / (D/8) rows at once (4 at D = 128, 8 at D = 64): every lane
-// loads, and the row sum is a shuffle over the row's lane group only.
-template <typename E, int D>
-__global__ __launch_bounds__(256) void flash_bwd_delta_kernel(const E* __restrict__ dout, const E* __restrict__ out,
-                                                              const float* __restrict__ lse, float* __restrict__ nd,
-                                                              float neg_inv_scale, int B, int S, int Hq,
-                                                              int64_t do_ss, int64_t do_sh, int64_t do_sb) {
-  constexpr int LPR = D / 8;             // lanes per row
-  constexpr int RPB = 256 / LPR;         // rows per block
-  const int sub = threadIdx.x % LPR;
-  const int64_t row = (int64_t)blockIdx.x * RPB + threadIdx.x / LPR;  // row over (b, q, hq)
-  const bool ok = row < (int64_t)B * S * Hq;
-  const int64_t rr = ok ? row : 0;
-  const int hq = rr % Hq;
-  const int64_t bq = rr / Hq;
-  const int q = bq % S, b = bq / S;
-  const f32x8 a = load8f(dout + b * do_sb + (int64_t)q * do_ss + hq * do_sh + sub * 8);
-  const f32x8 c = load8f(out + rr * D + sub * 8);
-  float acc = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) acc += a[j] * c[j];
-#pragma unroll
-  for (int o = LPR / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-  if (ok && sub == 0) {
-    const int64_t o = ((int64_t)b * Hq + hq) * S + q;
-    nd[o] = -acc;
-    nd[(int64_t)B * Hq * S + o] = lse[o] * neg_inv_scale;
-  }
-}
-
 template <typename E>
 struct BwdParams {
   const E* q;
@@ -443,13 +413,11 @@ struct BwdParams {
   const E* v;
   const E* dout;
   const float* lse;    // [B, Hq, S], natural log of sum exp(scale * s)
-  const float* delta;  // [2, B, Hq, S]: -delta, then -lse / scale (flash_bwd_delta_kernel, or the dQ pass itself)
+  const float* delta;  // [2, B, Hq, S]: -delta, then -lse / scale (written by the dQ pass, read by dK/dV)
   const E* o;          // forward output [B, S, Hq, D] contiguous (read by the dQ pass that computes delta)
   E* dq;            // [B, S, Hq, D]
   float* dk_part;      // [group, B, S, Hkv, D] fp32 partials (one per q head of the GQA group)
   float* dv_part;
-  E* ds;            // dS^T (unscaled) written by dK/dV for the dQ pass, or nullptr: [B, Hq, S/32 key blocks,
-                    // S/32 query blocks, 32 keys, 32 queries] -- one 2 KiB block per (32 keys, 32 queries)
   E* dk;            // [B, S, Hkv, D] (written directly when group == 1)
   E* dv;
   int64_t q_sb, q_ss, q_sh;
@@ -494,9 +462,8 @@ constexpr int kKvBQ = 32;
 // HP: q heads per workgroup (2 when the GQA group is even): the heads of a pair share this block's K / V, so
 // the workgroup walks both heads' query tiles into one dK/dV accumulator -- half the fp32 partials written
 // and summed by gqa_reduce, half the K / V block loads.
-template <typename E, int D, bool TAIL, bool STORE_DS = false, int HP = 1>
+template <typename E, int D, bool TAIL, int HP = 1>
 __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams<E> p) {
-  static_assert(!(STORE_DS && HP > 1), "the stored-dS path runs one head per workgroup");
   constexpr int KK = D / 16;
   constexpr int DT = D / 32;
   constexpr int QT = kKvBQ * D;
@@ -572,31 +539,11 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
     }
   };
 
-  // STORE_DS: the previous active tile's packed dS^T row, stored once this tile's DMA wait is behind us
-  uint4 ds_pend[2];
-  int ds_q0 = 0;
-  bool ds_has = false;
-  // blocked dS^T: this wave's 32 keys x 32 queries of one tile are one contiguous 2 KiB block (whole cache
-  // lines: a row-major [key][query] image took 64-byte pieces of 32 rows per tile and cost +25 % in dK/dV)
-  E* const ds_row = STORE_DS ? p.ds + ((((int64_t)b * p.Hq + hq) * (p.S / 32) + kw0 / 32) * (p.S / 32)) * 1024 +
-                                   r * 32 + 8 * h
-                             : nullptr;
-  auto flush_ds = [&]() {
-    if constexpr (STORE_DS) {
-      if (uniform(ds_has)) {
-        E* dst = ds_row + (ds_q0 / 32) * 1024;
-        *reinterpret_cast<uint4*>(dst) = ds_pend[0];
-        *reinterpret_cast<uint4*>(dst + 16) = ds_pend[1];
-        ds_has = false;
-      }
-    }
-  };
   // unrolled by two: the LDS buffer is a compile-time constant in each copy (immediate ds_read offsets)
   auto tile = [&](auto bufc, int j) {
     constexpr int buf = decltype(bufc)::value;
     vm_drain();  // this tile's LDS-DMA has landed ...
     __syncthreads();  // ... for every wave, and the other buffer's readers are done
-    flush_ds();
     if (j + 1 < ntot) stage(buf ^ 1, j + 1);
     const int t = t0 + (HP > 1 ? j % nt_h : j);
     const int q0 = t * kKvBQ;
@@ -644,23 +591,6 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
         dpacc[i] = ds.x;
         dpacc[i + 1] = ds.y;
       }
-      if constexpr (STORE_DS) {
-        // dS^T row `key`, queries q0 .. q0 + 31: the accumulator is already key-on-lane, so this is the widened
-        // epilogue store (two 16-byte stores per lane, 64 contiguous bytes per key row). Packed now, stored
-        // at the start of the NEXT tile: vmcnt also counts stores on gfx950, so a store issued in this tile
-        // would hold up the next tile's wait for its LDS-DMA by the store's write-acknowledge latency.
-#pragma unroll
-        for (int k = 0; k < 4; k += 2) {
-          vec4_t<E> va = {(E)dpacc[4 * k], (E)dpacc[4 * k + 1], (E)dpacc[4 * k + 2], (E)dpacc[4 * k + 3]};
-          vec4_t<E> vb = {(E)dpacc[4 * k + 4], (E)dpacc[4 * k + 5], (E)dpacc[4 * k + 6], (E)dpacc[4 * k + 7]};
-          const uint2 a = __builtin_bit_cast(uint2, va), c = __builtin_bit_cast(uint2, vb);
-          const auto sx = __builtin_amdgcn_permlane32_swap(a.x, c.x, false, false);
-          const auto sy = __builtin_amdgcn_permlane32_swap(a.y, c.y, false, false);
-          ds_pend[k >> 1] = make_uint4(sx[0], sy[0], sx[1], sy[1]);
-        }
-        ds_q0 = q0;
-        ds_has = true;
-      }
       vec8_t<E> pfr[2], dsf[2];
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
@@ -694,7 +624,6 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
     tile(std::integral_constant<int, 0>{}, j);
     if (j + 1 < ntot) tile(std::integral_constant<int, 1>{}, j + 1);
   }
-  flush_ds();
   if (group == HP) {  // one partial per kv head: written directly (the lane-pair swaps of the widened store
                       // need every lane, in or out of range)
     store_rows_bf16<DT>(p.dk + ((int64_t)b * p.S + key) * p.dkv_ss + hk * D, dkt, p.scale, h, key < p.S);
@@ -746,19 +675,15 @@ constexpr int kDqThreads = 256;
 constexpr int kDqBQ = 128;
 constexpr int kDqBKV = 64;
 
-// DELTA: this pass also computes delta = rowsum(dO * O) for its query rows (it holds dO in registers already)
-// and writes the [-delta, -lse/scale] rows the dK/dV pass reads -- no separate delta launch; the dQ pass then
-// runs first.
-template <typename E, int D, bool TAIL, bool FROM_DS = false, bool DELTA = false>
+// The pass also computes delta = rowsum(dO * O) for its query rows (it holds dO in registers already) and
+// writes the [-delta, -lse/scale] rows the dK/dV pass reads -- no separate delta launch; dQ runs first.
+template <typename E, int D, bool TAIL>
 __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams<E> p) {
-  static_assert(!(FROM_DS && DELTA), "the stored-dS dQ pass runs after dK/dV");
   constexpr int KK = D / 16;
   constexpr int DT = D / 32;
   constexpr int TILE = kDqBKV * D;
-  // FROM_DS: the second image is the dS^T tile [64 keys][128 queries] (written by dK/dV), read with the same
-  // transposed LDS reads as the K^T operand, so its fragments come out in the k order the MFMA pairs with K^T
-  constexpr int SLOT = FROM_DS ? TILE + kDqBKV * kDqBQ : 2 * TILE;
-  __shared__ __attribute__((aligned(16))) E smem[2 * SLOT];  // [buf][K | V or dS^T]
+  constexpr int SLOT = 2 * TILE;
+  __shared__ __attribute__((aligned(16))) E smem[2 * SLOT];  // [buf][K | V]
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -783,7 +708,7 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams<E
 
   vec8_t<E> qf[KK], dof[KK];
   float lse2 = 0.f, nd = 0.f;
-  if constexpr (!FROM_DS) {
+  {
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
       const bool ok = qcol < p.S;
@@ -792,7 +717,7 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams<E
     }
     const int64_t rowc = ((int64_t)b * p.Hq + hq) * p.S;
     lse2 = qcol < p.S ? p.lse[rowc + qcol] * kLog2e : INFINITY;
-    if constexpr (DELTA) {
+    {
       // this lane holds dO[qcol][16kk + 8h .. +7]: the matching O chunks, a 64-term dot, the other half-wave's 64
       float acc = 0.f;
       if (qcol < p.S) {
@@ -810,8 +735,6 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams<E
         dl[rowc + qcol] = nd;
         dl[(int64_t)p.B * p.Hq * p.S + rowc + qcol] = p.lse[rowc + qcol] * p.neg_inv_scale;
       }
-    } else {
-      nd = qcol < p.S ? p.delta[rowc + qcol] : 0.f;  // -delta
     }
   }
 
@@ -833,31 +756,10 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams<E
   }
   const TileDma<E, D, kDqBKV, 1, TAIL> kdma(kb, p.k_ss, p.S, w, lane);
   const TileDma<E, D, kDqBKV, 0, TAIL> vdma(vb, p.v_ss, p.S, w, lane);
-  // FROM_DS: the [64 keys][128 queries] dS^T tile gathered from eight 2 KiB blocks into a transposed-read
-  // image (the K-style recipe: 16 B per lane landing lane-linearly, the swizzle on the SOURCE offset). Lane
-  // (rin, phys) of piece j fills image row 4w + rin + 16j, physical chunk phys with logical chunk
-  // lc = swz_tr(row, phys); rows 32.. come from the next key block, so a piece's source offset is the
-  // lane's offset plus a per-piece and a per-tile scalar.
-  const int nqb = p.S / 32;
-  const E* dsl = FROM_DS ? p.ds + ((int64_t)b * p.Hq + hq) * p.S * p.S : p.k;
-  uint32_t ds_lane = 0;
-  if constexpr (FROM_DS) {
-    const int rin = lane / 16, phys = lane % 16;
-    const int lc = swz_tr<kDqBQ>(rin, phys);
-    ds_lane = (uint32_t)(((lc >> 2) * 1024 + (lc & 3) * 8 + (4 * w + rin) * 32) * 2);
-  }
   auto stage = [&](int buf, int t) {
     E* img = smem + buf * SLOT;
     kdma.issue(img, t * kDqBKV);
-    if constexpr (FROM_DS) {
-      const uint32_t soff_t = (uint32_t)(((2 * t) * nqb + q0 / 32) * 1024 * 2);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        dma16(dsl, (int)((int64_t)p.S * p.S * 2), ds_lane,
-              soff_t + (uint32_t)(((j & 1) * 16 * 32 + (j >> 1) * nqb * 1024) * 2), img + TILE + (w + 4 * j) * 512);
-    } else {
-      vdma.issue(img + TILE, t * kDqBKV);
-    }
+    vdma.issue(img + TILE, t * kDqBKV);
   };
   // unrolled by two: the LDS buffer is a compile-time constant in each copy (immediate ds_read offsets)
   auto tile = [&](auto bufc, int t) {
@@ -870,31 +772,6 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams<E
       const E* kt = smem + buf * SLOT;
       const E* vt = kt + TILE;
       vec8_t<E> dsf[2][2];
-      if constexpr (FROM_DS) {
-        const int col = 32 * w + 16 * (g & 1) + 4 * (i16 & 3);  // this wave's 32 query columns
-        const int ch = col >> 3, within = col & 7;
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const int r1 = 32 * u + 16 * s2 + 4 * h + (i16 >> 2);
-            const int r2 = r1 + 8;
-            dsf[u][s2] = cat(lds_read_tr(vt + r1 * kDqBQ + swz_tr<kDqBQ>(r1, ch) * 8 + within),
-                             lds_read_tr(vt + r2 * kDqBQ + swz_tr<kDqBQ>(r2, ch) * 8 + within));
-          }
-        // diagonal tiles: dS^T blocks above the diagonal were never written (the dK/dV wave skipped them)
-        if (uniform(p.causal && kv0 + kDqBKV - 1 > q0w)) {
-#pragma unroll
-          for (int u = 0; u < 2; ++u)
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-              for (int j = 0; j < 8; ++j) {
-                const int kv = kv0 + 32 * u + 16 * s2 + 8 * (j >> 2) + 4 * h + (j & 3);
-                if (kv > qcol) dsf[u][s2][j] = (E)0.f;
-              }
-        }
-      } else {
       f32x16 s[2] = {(f32x16)(0.f), (f32x16)(0.f)};
       f32x16 dp[2] = {(f32x16)(0.f), (f32x16)(0.f)};
 #pragma unroll
@@ -935,7 +812,6 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams<E
                                 (E)s[u][8 * s2 + 3], (E)s[u][8 * s2 + 4], (E)s[u][8 * s2 + 5],
                                 (E)s[u][8 * s2 + 6], (E)s[u][8 * s2 + 7]};
       }
-      }  // FROM_DS
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         const int col = dt * 32 + 16 * (g & 1) + 4 * (i16 & 3);
@@ -959,42 +835,6 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams<E
     if (t + 1 < nt) tile(std::integral_constant<int, 1>{}, t + 1);
   }
   store_rows_bf16<DT>(p.dq + ((int64_t)b * p.S + qcol) * p.dq_ss + hq * D, dqt, p.scale, h, qcol < p.S);
-}
-
-// DLGM_ATTN_BWD_STREAMS=1: the dQ pass on a side stream beside dK/dV. Off by default: measured at S 8192,
-// 32/8 heads the concurrent passes took 2.20 ms against 1.92 ms back to back (they contend for the same CUs
-// and L2; each already fills the chip with 2048 workgroups).
-// DLGM_ATTN_DQ_FROM_DS=1: dQ from the dS^T blocks the dK/dV pass stores (read per call, so a test or a
-// run can switch it). Off by default: at S 8192, 32/8 heads the dQ pass drops 750 -> 519 us but dK/dV
-// rises 1116 -> 1307 us for its 2.15 GB of dS^T writes (the board is at its power limit), and the
-// headline step moved 0.1-0.2 % for +2.3 GiB of peak memory (profiles/attn_experiments_r01.md).
-bool dq_from_ds() {
-  const char* e = std::getenv("DLGM_ATTN_DQ_FROM_DS");
-  return e != nullptr && std::atoi(e) != 0;
-}
-
-// DLGM_ATTN_DELTA_IN_DQ=0: the separate delta launch before dK/dV (default 1: the dQ pass computes delta)
-bool delta_in_dq() {
-  const char* e = std::getenv("DLGM_ATTN_DELTA_IN_DQ");
-  return e == nullptr || std::atoi(e) != 0;
-}
-
-bool bwd_two_streams() {
-  static const bool on = [] {
-    const char* e = std::getenv("DLGM_ATTN_BWD_STREAMS");
-    return e != nullptr && std::atoi(e) != 0;
-  }();
-  return on;
-}
-
-// fork / join events of the backward, one pair per device (re-recorded every call; a wait is enqueued
-// before the next record, so reuse is ordered)
-hipEvent_t bwd_event(int which) {
-  static hipEvent_t ev[64][2] = {};
-  int dev = 0;
-  DLGM_CHECK_HIP(hipGetDevice(&dev));
-  if (ev[dev][which] == nullptr) DLGM_CHECK_HIP(hipEventCreateWithFlags(&ev[dev][which], hipEventDisableTiming));
-  return ev[dev][which];
 }
 
 void check_qkv(const at::Tensor& t, const char* name) {
@@ -1084,14 +924,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
   if (B == 0 || S == 0) return {dq.zero_(), dk.zero_(), dv.zero_()};
   auto delta = at::empty({2, B, Hq, S}, q.options().dtype(at::kFloat));  // -delta, -lse/scale
   const bool tail = S % 128 != 0;
-  // dQ from the stored dS^T (DLGM_ATTN_DQ_FROM_DS, full tiles only): the dK/dV pass writes dS^T blocks and
-  // the dQ pass stages them instead of recomputing S, P and dP
-  // the dS^T buffer is B*Hq*S^2 16-bit values (4.3 GB for Llama-3-8B at S 8192): long sequences fall back
-  // the dQ pass addresses each head's dS^T region through a 32-bit buffer resource: also bound it per head
-  const bool from_ds = !tail && dq_from_ds() && (int64_t)B * Hq * S * S * 2 <= (int64_t(16) << 30) &&
-                       (int64_t)S * S * 2 < (int64_t(1) << 31);
-  // two q heads per dK/dV workgroup when the GQA group is even (one head with the stored-dS path)
-  const int hp = (group % 2 == 0 && !from_ds) ? 2 : 1;
+  // two q heads per dK/dV workgroup when the GQA group is even
+  const int hp = group % 2 == 0 ? 2 : 1;
   const int nparts = group / hp;  // fp32 dK/dV partials summed by gqa_reduce
   at::Tensor dk_part, dv_part;
   if (nparts > 1) {
@@ -1099,7 +933,6 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
     dv_part = at::empty({nparts, B, S, Hkv, D}, q.options().dtype(at::kFloat));
   }
   auto stream = c10::hip::getCurrentHIPStream();
-  const int64_t rows = (int64_t)B * S * Hq;
   TORCH_CHECK(k.scalar_type() == q.scalar_type() && v.scalar_type() == q.scalar_type() &&
                   dout.scalar_type() == q.scalar_type() && out.scalar_type() == q.scalar_type(),
               "flash_attn_bwd: mixed dtypes");
@@ -1108,59 +941,21 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
   DLGM_DISPATCH_16(q.scalar_type(), E, {
     auto dop = reinterpret_cast<const E*>(dout.data_ptr());
     auto outp = reinterpret_cast<const E*>(out.data_ptr());
-    // dK/dV and dQ are independent passes over the same inputs: optionally the dQ pass runs on a side stream
-    // (forked and joined with events, so it also works under HIP graph capture)
-    const bool fork = bwd_two_streams() && !from_ds;
-    // default: the dQ pass computes delta itself and runs first (no delta launch)
-    const bool fused = !from_ds && !fork && delta_in_dq();
-    if (!fused) {
-      if (D == 128)
-        flash_bwd_delta_kernel<E, 128><<<(rows + 15) / 16, 256, 0, stream>>>(
-            dop, outp, lse.data_ptr<float>(), delta.data_ptr<float>(), (float)(-1.0 / softmax_scale), B, S, Hq,
-            dout.stride(1), dout.stride(2), dout.stride(0));
-      else
-        flash_bwd_delta_kernel<E, 64><<<(rows + 31) / 32, 256, 0, stream>>>(
-            dop, outp, lse.data_ptr<float>(), delta.data_ptr<float>(), (float)(-1.0 / softmax_scale), B, S, Hq,
-            dout.stride(1), dout.stride(2), dout.stride(0));
-      DLGM_CHECK_HIP(hipGetLastError());
-    }
     BwdParams<E> p{reinterpret_cast<const E*>(q.data_ptr()), reinterpret_cast<const E*>(k.data_ptr()),
                    reinterpret_cast<const E*>(v.data_ptr()), dop, lse.data_ptr<float>(), delta.data_ptr<float>(),
                    outp, reinterpret_cast<E*>(dq.data_ptr()), nparts > 1 ? dk_part.data_ptr<float>() : nullptr,
-                   nparts > 1 ? dv_part.data_ptr<float>() : nullptr, /*ds=*/nullptr, reinterpret_cast<E*>(dk.data_ptr()),
+                   nparts > 1 ? dv_part.data_ptr<float>() : nullptr, reinterpret_cast<E*>(dk.data_ptr()),
                    reinterpret_cast<E*>(dv.data_ptr()), q.stride(0), q.stride(1), q.stride(2), k.stride(0),
                    k.stride(1), k.stride(2), v.stride(0), v.stride(1), v.stride(2), dout.stride(0), dout.stride(1),
                    dout.stride(2), dq_ss, dkv_ss, B, S, Hq, Hkv, (float)softmax_scale,
                    (float)(softmax_scale * kLog2e), (float)(-1.0 / softmax_scale), causal};
-    at::Tensor dsT;
-    if (from_ds) {
-      dsT = at::empty({B, Hq, S, S}, q.options());
-      p.ds = reinterpret_cast<E*>(dsT.data_ptr());
-    }
-    hipStream_t qs = stream;
-    if (fork) {
-      qs = c10::hip::getStreamFromPool(false, q.get_device()).stream();
-      DLGM_CHECK_HIP(hipEventRecord(bwd_event(0), stream));
-      DLGM_CHECK_HIP(hipStreamWaitEvent(qs, bwd_event(0), 0));
-    }
     // one (dK/dV, dQ) pair of launches per head dim / tail instantiation
     auto run = [&](auto dc, auto tc) {
       constexpr int DD = decltype(dc)::value;
       constexpr bool TT = decltype(tc)::value;
-      auto dkdv = [&]() {
-        if (hp == 2) flash_bwd_dkdv_kernel<E, DD, TT, false, 2><<<kv_blocks, kKvThreads, 0, stream>>>(p);
-        else flash_bwd_dkdv_kernel<E, DD, TT><<<kv_blocks, kKvThreads, 0, stream>>>(p);
-      };
-      if (fused) {
-        flash_bwd_dq_kernel<E, DD, TT, false, true><<<dq_blocks, kDqThreads, 0, stream>>>(p);
-        dkdv();
-      } else if (from_ds && !TT) {
-        flash_bwd_dkdv_kernel<E, DD, false, true><<<kv_blocks, kKvThreads, 0, stream>>>(p);
-        flash_bwd_dq_kernel<E, DD, false, true><<<dq_blocks, kDqThreads, 0, stream>>>(p);
-      } else {
-        dkdv();
-        flash_bwd_dq_kernel<E, DD, TT><<<dq_blocks, kDqThreads, 0, qs>>>(p);
-      }
+      flash_bwd_dq_kernel<E, DD, TT><<<dq_blocks, kDqThreads, 0, stream>>>(p);
+      if (hp == 2) flash_bwd_dkdv_kernel<E, DD, TT, 2><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+      else flash_bwd_dkdv_kernel<E, DD, TT><<<kv_blocks, kKvThreads, 0, stream>>>(p);
     };
     if (D == 128) {
       if (tail) run(std::integral_constant<int, 128>{}, std::true_type{});
@@ -1170,10 +965,6 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
       else run(std::integral_constant<int, 64>{}, std::false_type{});
     }
     DLGM_CHECK_HIP(hipGetLastError());
-    if (fork) {
-      DLGM_CHECK_HIP(hipEventRecord(bwd_event(1), qs));
-      DLGM_CHECK_HIP(hipStreamWaitEvent(stream, bwd_event(1), 0));
-    }
     if (nparts > 1) {
       const int64_t n = (int64_t)B * S * Hkv * D;
       const int64_t grid = std::min<int64_t>((n / 8 + 255) / 256, 4096);

@@ -170,6 +170,8 @@ class Trainer:
             self.ecfg.hip_graphs = True
         if getattr(args, "xgmi_mesh", None):
             self.ecfg.xgmi_mesh = args.xgmi_mesh
+        if getattr(args, "activation_checkpointing", False):
+            self.ecfg.activation_checkpointing = True  # the reference's 70b preset sets it (deepspeed_launcher.py:402)
         if args.halt_on_nan and not self.ecfg.fp16:
             self.ecfg.nan_latch = True  # the host runs one step ahead of the NaN decision (see NanTrap)
         self.global_batch = self._elastic_batch(args)
@@ -472,6 +474,7 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--shadow-world", type=int, default=0,
                     help="simulate rank --shadow-rank of a job of this many ranks alone on one GPU (true-size state)")
     ap.add_argument("--shadow-rank", type=int, default=0)
+    ap.add_argument("--activation-checkpointing", action="store_true", help="block recompute in the backward")
     ap.add_argument("--dump-state", default=None, help="directory: each rank saves rc / last step / its partition")
     a, unknown = ap.parse_known_args(argv)
     return a

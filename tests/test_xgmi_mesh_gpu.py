@@ -14,6 +14,7 @@ the wire differs. Checks, all bit-exact:
 """
 import os
 import socket
+import warnings
 
 import pytest
 import torch
@@ -94,8 +95,9 @@ def _zero_worker(rank, world, port, n, iters, out_path):
                 msgs.append(f"rs it{it} {src_dtype} maxdiff {float((o.cpu() - ref).abs().max())}")
     torch.cuda.synchronize()
     mesh.check()
+    mode = mesh.alloc_mode
     mesh.close()
-    _finish(rank, ok, out_path, {"msgs": msgs} if rank == 0 else None)
+    _finish(rank, ok, out_path, {"msgs": msgs, "mode": mode} if rank == 0 else None)
 
 
 @pytest.mark.parametrize("world,n", [(2, 4096), (4, 1 << 18)])
@@ -104,6 +106,8 @@ def test_mesh_all_gather_and_reduce_scatter_bit_exact(tmp_path, world, n):
     mp.spawn(_zero_worker, args=(world, _free_port(), n, 4, out), nprocs=world, join=True)
     res = torch.load(out, weights_only=True)
     assert res["ok"] == 1, res.get("msgs")
+    # which memory kind the driver exported (uncached is the design point; the fallbacks are recorded)
+    warnings.warn(f"xGMI mesh heap allocated {res['mode']}")
 
 
 def _routing(rank, T, K, E, seed, skew):
