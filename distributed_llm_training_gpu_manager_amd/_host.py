@@ -76,7 +76,7 @@ def lib():
 
 CHUNK = 64 << 20
 # checkpoint I/O + CRC threads: 16 = the CPU share of one GPU on an 8-GPU MI355X node
-THREADS = int(os.environ.get("DLGM_CKPT_THREADS", str(max(4, min(16, (os.cpu_count() or 8) // 2)))))
+THREADS = max(4, min(16, (os.cpu_count() or 8) // 2))  # checkpoint I/O / CRC threads
 
 
 def algo() -> str:

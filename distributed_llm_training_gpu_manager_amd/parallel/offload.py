@@ -29,7 +29,7 @@ from __future__ import annotations
 
 import os
 import time
-from typing import List, Optional
+from typing import Dict, List, Optional, Tuple
 
 import torch
 
@@ -242,6 +242,10 @@ class NvmeParamStore:
 
     * gather: the group's shard is read file -> slot (buffered I/O), then the engine copies it H2D on its
       side stream and all-gathers; a slot is reused only after the H2D that read it has completed (event);
+    * read-ahead: the order of the gathers repeats every step (the residency plan is static), so each read
+      also issues the AIO read of the shard that followed it last time into the next free slot; the gather
+      of that shard then only waits for I/O that has been running meanwhile (DeepSpeed's offload_param
+      prefetches partitions ahead of use the same way). A step's writes invalidate read-aheads in flight;
     * after each optimizer step: the new 16-bit values are produced slot by slot (device cast + D2H, or the
       host AdamW's output) and written back with the writes of ``buffer_count - 1`` slots in flight.
 
@@ -270,7 +274,12 @@ class NvmeParamStore:
         self._used: List[Optional["torch.cuda.Event"]] = [None] * nb  # last H2D out of the slot
         self._writes: List[Optional[int]] = [None] * nb                # AIO write ticket out of the slot
         self._next = 0
-        self.stats = {"read_GiB": 0.0, "write_GiB": 0.0, "io_wait_s": 0.0}
+        self._ahead: Dict[Tuple[int, int], Tuple[int, int]] = {}  # (off, n) -> (slot, AIO read ticket)
+        self._slot_key: List[Optional[Tuple[int, int]]] = [None] * nb  # read-ahead a slot holds
+        self._follow: Dict[Tuple[int, int], Tuple[int, int]] = {}  # access -> the access after it last time
+        self._prev: Optional[Tuple[int, int]] = None
+        self.read_ahead = nb > 2  # one slot in use, one being filled, one for the H2D still draining
+        self.stats = {"read_GiB": 0.0, "write_GiB": 0.0, "io_wait_s": 0.0, "read_ahead_hits": 0, "reads": 0}
 
     def _wait(self, ticket: int) -> None:
         t0 = time.perf_counter()
@@ -286,23 +295,55 @@ class NvmeParamStore:
         if self._writes[i] is not None:
             self._wait(self._writes[i])
             self._writes[i] = None
+        key = self._slot_key[i]
+        if key is not None:  # an unused read-ahead in this slot: let it finish, then forget it
+            self._wait(self._ahead.pop(key)[1])
+            self._slot_key[i] = None
         return i
 
     def read(self, off: int, n: int):
-        """Read elements [off, off + n) into a free slot; returns (slot index, host view)."""
+        """Read elements [off, off + n) into a slot (or take the read-ahead of it); returns (slot, host view)."""
         assert n <= self.slot_elems, (n, self.slot_elems)
-        i = self._take()
+        key = (off, n)
+        self.stats["reads"] += 1
+        if key in self._ahead:
+            i, tk = self._ahead.pop(key)
+            self._slot_key[i] = None
+            self._wait(tk)
+            self.stats["read_ahead_hits"] += 1
+        else:
+            i = self._take()
+            self._wait(self.aio.read(self.fh, self.slots[i][:n], off * self.esize))
+            self.stats["read_GiB"] += n * self.esize / 2 ** 30
         t = self.slots[i][:n]
-        self._wait(self.aio.read(self.fh, t, off * self.esize))
-        self.stats["read_GiB"] += n * self.esize / 2 ** 30
+        if self._prev is not None:
+            self._follow[self._prev] = key
+        self._prev = key
+        nxt = self._follow.get(key)
+        if self.read_ahead and nxt is not None and nxt not in self._ahead and nxt != key:
+            j = self._take()
+            if j == i:  # never refill the slot just handed out (only possible with a 1-slot ring)
+                return i, t
+            self._ahead[nxt] = (j, self.aio.read(self.fh, self.slots[j][:nxt[1]], nxt[0] * self.esize))
+            self._slot_key[j] = nxt
+            self.stats["read_GiB"] += nxt[1] * self.esize / 2 ** 30
         return i, t
 
     def release_after(self, i: int, ev) -> None:
         """The slot may be refilled once `ev` (the H2D copy out of it) has completed."""
         self._used[i] = ev
 
+    def drop_read_ahead(self) -> None:
+        """Forget the read-aheads in flight (the partition is about to change under them)."""
+        for key, (i, tk) in list(self._ahead.items()):
+            self._wait(tk)
+            self._slot_key[i] = None
+        self._ahead.clear()
+        self._prev = None
+
     def write(self, produce) -> None:
         """Stream the whole partition back: produce(off, ln, slot_view) fills each slot-sized piece."""
+        self.drop_read_ahead()
         for off in range(0, self.n, self.slot_elems):
             ln = min(self.slot_elems, self.n - off)
             i = self._take()

@@ -1102,6 +1102,8 @@ class ZeroEngine:
     def _optimizer_step(self) -> Dict[str, Any]:
         for hk in self.pre_step_hooks:
             hk(self)
+        if self.param_nvme is not None:  # the partition file changes below: read-aheads in flight are stale
+            self.param_nvme.drop_read_ahead()
         self.step_count += 1
         cfg = self.cfg
         self._global_grad_stats()

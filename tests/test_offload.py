@@ -143,3 +143,25 @@ def test_aio_engine_roundtrip(tmp_path):
         assert float(tail.abs().sum()) == 0.0
         aio.close(h, fsync=True)
     aio.shutdown()
+
+
+def test_nvme_param_store_read_ahead(tmp_path):
+    """offload_param=nvme read-ahead: the second pass over the same gather order is served by reads
+    issued one access ahead; a write of the partition invalidates read-aheads in flight (new bytes are read)."""
+    from distributed_llm_training_gpu_manager_amd.parallel.offload import NvmeParamStore
+    n, piece = 4096, 512
+    st = NvmeParamStore(n, torch.float32, str(tmp_path), 0, piece, buffer_count=4, aio_threads=2,
+                        aio_block_size=4096)
+    order = [(off, piece) for off in (0, 1024, 2048, 512, 3584)]
+
+    def fill(base):
+        st.write(lambda off, ln, slot: slot.copy_(torch.arange(off, off + ln, dtype=torch.float32) + base))
+
+    for step, base in enumerate((0.0, 0.5, 7.0)):
+        fill(base)
+        for off, ln in order:
+            i, t = st.read(off, ln)
+            assert torch.equal(t, torch.arange(off, off + ln, dtype=torch.float32) + base), (step, off)
+    # step 0 learns the order; steps 1 and 2 hit on every access after the first
+    assert st.stats["read_ahead_hits"] == 2 * (len(order) - 1), st.stats
+    st.close()
