@@ -2,6 +2,11 @@
 // exported with HIP IPC and mapped by every peer, plus the kernels that move data through it and the flags that
 // order it -- no host synchronisation, no library, capturable in a HIP graph.
 //
+// Shadow mode (state word kStShadow = 1; one rank of a world-W job alone on one GPU, every peer address = this
+// rank's heap): a producer writes "peer" t's flag / slot as if it were rank t (so every wait completes and every
+// slot is written once), the EP tables describe this rank receiving its own rows from every source -- true-size,
+// deterministic traffic for the per-rank timing and stream-ordering rehearsals of the shadow rank.
+//
 // Heap (one allocation per rank, the same layout on every rank; offsets chosen by parallel/xgmi_mesh.py):
 //   [0, kFlagBytes)      u64 flags[kind][channel][source rank], written by the SOURCE rank into this rank's heap
 //   regions              ZeRO bf16 parameter shard (pulled by peers), reduce-scatter slots, EP dispatch / combine
@@ -54,6 +59,7 @@ constexpr int kStEpoch = 0;    // [kMaxCh] transfers started per channel
 constexpr int kStVer = 16;     // parameter version
 constexpr int kStErr = 17;     // sticky: 1 = a wait timed out
 constexpr int kStOvf = 18;     // sticky: 1 = an EP dispatch overflowed the receive capacity
+constexpr int kStShadow = 19;  // 1 = shadow rank (parallel/comm.py ShadowComm): every "peer" is this rank's heap
 constexpr int kStPushCtr = 32; // [kMaxCh] last-block counters of the push kernels
 constexpr int kStCopyCtr = 48; // [kMaxCh] last-block counters of the consuming kernels
 constexpr int kStateWords = 64;
@@ -116,7 +122,8 @@ __device__ void last_block_signal(int64_t* st, int ctr, const int64_t* peers, in
     }
   }
   __syncthreads();
-  if (last && (int)threadIdx.x < W) store_flag(flag_at(peers[threadIdx.x], kind, ch, me), (uint64_t)value);
+  const int who = get_word(st, kStShadow) ? (int)threadIdx.x : me;
+  if (last && (int)threadIdx.x < W) store_flag(flag_at(peers[threadIdx.x], kind, ch, who), (uint64_t)value);
 }
 
 // ------------------------------------------------------------------------------------------------ sync
@@ -133,7 +140,7 @@ __global__ __launch_bounds__(64) void mesh_sync_kernel(int64_t* st, const int64_
   const int64_t v = get_word(st, val);
   if (store_kind >= 0) {
     release_system();
-    if (t < W) store_flag(flag_at(peers[t], store_kind, ch, me), (uint64_t)v);
+    if (t < W) store_flag(flag_at(peers[t], store_kind, ch, get_word(st, kStShadow) ? t : me), (uint64_t)v);
   }
   if (wait_kind >= 0) {
     bool ok = true;
@@ -181,7 +188,8 @@ __global__ __launch_bounds__(kThreads) void mesh_rs_push_kernel(const TI* __rest
                                                                 int64_t* st, int ch, int me, int W) {
   const int p = blockIdx.y;
   const int64_t e = get_word(st, kStEpoch + ch);
-  bf16* dst = reinterpret_cast<bf16*>(peers[p] + region_off + (e % S) * slot_bytes + me * rank_stride);
+  const int row = get_word(st, kStShadow) ? p : me;
+  bf16* dst = reinterpret_cast<bf16*>(peers[p] + region_off + (e % S) * slot_bytes + row * rank_stride);
   const TI* src = x + (int64_t)p * n;
   const int64_t n8 = n / 8, stride = (int64_t)gridDim.x * kThreads;
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n8; i += stride)
@@ -350,6 +358,7 @@ __global__ __launch_bounds__(kThreads) void mesh_ep_plan_kernel(const int* __res
   __shared__ int64_t e_sh;
   const int t = threadIdx.x;
   const int El = E / W;
+  const bool shadow = get_word(st, kStShadow) != 0;
   if (t == 0) {
     const int64_t e = get_word(st, kStEpoch + ch) + 1;
     set_word(st, kStEpoch + ch, e);
@@ -364,12 +373,12 @@ __global__ __launch_bounds__(kThreads) void mesh_ep_plan_kernel(const int* __res
   for (int i = t; i < W * E; i += kThreads) {
     const int p = i / E, x = i - p * E;
     int* hdr = reinterpret_cast<int*>(peers[p] + region_off + (e % S) * slot_bytes);
-    hdr[me * E + x] = offsets[x + 1] - offsets[x];
+    hdr[(shadow ? p : me) * E + x] = offsets[x + 1] - offsets[x];
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   release_system();
-  if (t < W) store_flag(flag_at(peers[t], kCnt, ch, me), (uint64_t)e);
+  if (t < W) store_flag(flag_at(peers[t], kCnt, ch, shadow ? t : me), (uint64_t)e);
   ok = true;
   if (t < W) ok = wait_ge(flag_at(peers[me], kCnt, ch, t), e, timeout);
   if (!ok) set_word(st, kStErr, 1);
@@ -401,8 +410,37 @@ __global__ __launch_bounds__(kThreads) void mesh_ep_plan_kernel(const int* __res
   plan[L.total_full] = total_me;
   if (any_ovf) set_word(st, kStOvf, 1);
   for (int j = 0; j <= El; ++j) plan[L.loff + j] = min(j < El ? pos(me, 0, j) : total_me, C);
-  // dispatch: one segment per global expert x, this rank's rows offsets[x] .. to owner x / El
   int vs = 0, srow = 0;
+  if (shadow) {
+    // this rank receives its own rows of each local expert j from every source s (W x El = E segments), and the
+    // combine sends back only its own block: every written row has one writer, the traffic is true size
+    auto own = [&](int x) { int o = 0; for (int xx = 0; xx < x; ++xx) o += M[me * E + xx]; return o; };
+    for (int j = 0; j < El; ++j)
+      for (int s2 = 0; s2 < W; ++s2) {
+        const int k = j * W + s2, x = me * El + j, n = M[me * E + x], at = pos(me, s2, j), val = clampv(at, n);
+        plan[L.d_vs + k] = vs;
+        plan[L.d_src + k] = own(x);
+        plan[L.d_val + k] = val;
+        plan[L.d_rank + k] = me;
+        plan[L.d_row + k] = at;
+        vs += val;
+      }
+    plan[L.d_vs + E] = vs;
+    vs = 0;
+    for (int j = 0; j < El; ++j)
+      for (int s2 = 0; s2 < W; ++s2) {
+        const int k = j * W + s2, x = me * El + j, n = s2 == me ? M[me * E + x] : 0, at = pos(me, s2, j);
+        plan[L.c_vs + k] = vs;
+        plan[L.c_src + k] = at;
+        plan[L.c_val + k] = clampv(at, n);
+        plan[L.c_rank + k] = me;
+        plan[L.c_row + k] = own(x);
+        vs += n;
+      }
+    plan[L.c_vs + El * W] = vs;
+    return;
+  }
+  // dispatch: one segment per global expert x, this rank's rows offsets[x] .. to owner x / El
   for (int x = 0; x < E; ++x) {
     const int p = x / El, j = x - p * El, n = M[me * E + x];
     const int at = pos(p, me, j), val = clampv(at, n);

@@ -46,7 +46,7 @@ from .._native import hip_ops
 from .comm import Comm, Handle
 
 CNT, DATA, ACK, VER, RDONE = 0, 1, 2, 3, 4
-ST_EPOCH, ST_VER, ST_ERR, ST_OVF = 0, 16, 17, 18
+ST_EPOCH, ST_VER, ST_ERR, ST_OVF, ST_SHADOW = 0, 16, 17, 18, 19
 CH_RS, CH_DISPATCH, CH_COMBINE = 0, 1, 2
 ALIGN = 4096
 ALLOC_MODES = ("uncached", "fine-grained", "coarse-grained")
@@ -80,6 +80,13 @@ class XgmiMesh:
         assert device.type == "cuda", "the xGMI mesh needs GPU memory"
         self.comm, self.device = comm, device
         self.W, self.rank = comm.world, comm.rank
+        # shadow rank (ShadowComm: rank r of a world-W job alone on this GPU): every "peer" heap is this rank's own
+        # and the kernels write peer t's flags / slots as if they were rank t (csrc/kernels/xgmi_mesh.hip) --
+        # true-size traffic and the same stream ordering, no IPC. Its collectives run on the mesh streams after a
+        # `delay_cycles` spin (async_mode) or inline on the caller's stream (sync), like ShadowComm's.
+        self.shadow = getattr(comm, "backend", "") == "shadow"
+        self.inline = self.shadow and not getattr(comm, "async_mode", False)
+        self.delay_cycles = int(getattr(comm, "delay_cycles", 0)) if self.shadow else 0
         ops = hip_ops()
         off = _round(int(ops.mesh_flag_bytes()))
         self.regions: Dict[str, Region] = {}
@@ -90,14 +97,16 @@ class XgmiMesh:
         self.heap_bytes = off
         layouts: List[Optional[list]] = [None] * self.W
         mine = [(r.name, r.slot_bytes, r.slots, r.offset) for r in self.regions.values()]
-        if self.W > 1:
+        if self.W > 1 and not self.shadow:
             dist.all_gather_object(layouts, mine, group=comm.group)
             assert all(x == mine for x in layouts), f"mesh: heap layouts differ across ranks: {layouts}"
         self.heap, self.alloc_mode = self._alloc(ops, alloc_mode)
         self._opened: List[int] = []
         ptrs = [0] * self.W
         ptrs[self.rank] = int(self.heap.data_ptr())
-        if self.W > 1:
+        if self.shadow:
+            ptrs = [int(self.heap.data_ptr())] * self.W
+        elif self.W > 1:
             handles: List[Optional[list]] = [None] * self.W
             dist.all_gather_object(handles, ops.ipc_handle(self.heap).tolist(), group=comm.group)
             with torch.cuda.device(device):
@@ -108,13 +117,15 @@ class XgmiMesh:
                         ptrs[r] = p
         self.peers = torch.tensor(ptrs, dtype=torch.int64, device=device)
         self.state = torch.zeros(int(ops.mesh_state_words()), dtype=torch.int64, device=device)
+        if self.shadow:
+            self.state[ST_SHADOW] = 1
         self.timeout_ticks = int(timeout_s * 100e6)  # s_memrealtime runs at 100 MHz on MI355X
         # one stream per traffic class (parameter gathers / gradient reductions), like the engine's two RCCL
         # communicators: a prefetch gather and a reduce-scatter run concurrently
         self._streams: Dict[str, torch.cuda.Stream] = {k: torch.cuda.Stream(device) for k in ("ag", "rs")}
         self.closed = False
         self.issued = 0
-        if self.W > 1:  # nobody may write into a heap before every rank mapped every heap
+        if self.W > 1 and not self.shadow:  # nobody may write into a heap before every rank mapped every heap
             self.host_barrier()
 
     # ------------------------------------------------------------------ setup
@@ -126,7 +137,7 @@ class XgmiMesh:
             for m in order:
                 try:
                     buf = ops.ipc_alloc(self.heap_bytes, m)
-                    if self.W > 1:
+                    if self.W > 1 and not self.shadow:
                         ops.ipc_handle(buf)  # exportable?
                     return buf, ALLOC_MODES[m]
                 except RuntimeError as e:  # try the next memory kind
@@ -135,7 +146,7 @@ class XgmiMesh:
 
     def host_barrier(self) -> None:
         torch.cuda.synchronize(self.device)
-        if self.W > 1:
+        if self.W > 1 and not self.shadow:
             if self.comm.backend == "nccl":
                 t = torch.zeros(1, device=self.device)
                 dist.all_reduce(t, group=self.comm.group)
@@ -186,10 +197,15 @@ class XgmiMesh:
         """Run `fn` on the mesh stream after the work queued on the current stream (as RCCL orders a
         collective), keep `tensors` alive for it, and return a Handle whose wait() orders the waiting stream
         after it (no host synchronisation)."""
+        if self.inline:  # synchronous shadow rank: on the caller's stream
+            fn()
+            return Handle()
         cur = torch.cuda.current_stream(self.device)
         s = self.stream(key)
         s.wait_stream(cur)
         with torch.cuda.stream(s):
+            if self.delay_cycles:
+                torch.cuda._sleep(self.delay_cycles)  # a consumer that forgets to wait reads stale data, every run
             fn()
             ev = torch.cuda.Event()
             ev.record(s)
@@ -241,7 +257,8 @@ class XgmiMesh:
         for p in self._opened:
             ops.ipc_close(p)
         self._opened = []
-        self.host_barrier()
+        if not self.shadow:
+            self.host_barrier()
         self.closed = True
 
 

@@ -436,8 +436,9 @@ class ZeroEngine:
             raise ValueError(f"xgmi_mesh must be 'on' or 'off', got {c.xgmi_mesh!r}")
         if c.xgmi_mesh != "on" or not self.is_cuda_dev() or self.W == 1:
             return
-        if self.comm.backend not in ("nccl", "gloo") or c.offload_optimizer != "none" or c.offload_param != "none":
-            return  # shadow ranks / host-resident partitions keep the RCCL path
+        if self.comm.backend not in ("nccl", "gloo", "shadow") or c.offload_optimizer != "none" or \
+                c.offload_param != "none":
+            return  # host-resident partitions keep the RCCL path
         from .xgmi_mesh import XgmiMesh, rs_region_bytes
         dense = [g for g in self.groups if self._mesh_group(g)]
         regions = {"p16": (self.shard_total * 2, 1)}

@@ -15,8 +15,9 @@ from ..parallel.comm import DONE, Comm
 
 FACTOR = {"all_gather": lambda w: (w - 1) / w, "ipc_mesh_all_gather": lambda w: (w - 1) / w,
           "reduce_scatter": lambda w: (w - 1) / w, "ipc_mesh_reduce_scatter": lambda w: (w - 1) / w,
-          "all_to_all": lambda w: (w - 1) / w, "all_reduce": lambda w: 2 * (w - 1) / w}
-MESH_OPS = ("ipc_mesh_all_gather", "ipc_mesh_reduce_scatter")
+          "all_to_all": lambda w: (w - 1) / w, "ipc_mesh_all_to_all": lambda w: (w - 1) / w,
+          "all_reduce": lambda w: 2 * (w - 1) / w}
+MESH_OPS = ("ipc_mesh_all_gather", "ipc_mesh_reduce_scatter", "ipc_mesh_all_to_all")
 
 
 def run(op: str, comm: Comm, nbytes: int, device, dtype, iters: int, warmup: int) -> float:
@@ -54,6 +55,18 @@ def _run(op: str, comm: Comm, nbytes: int, device, dtype, iters: int, warmup: in
         inp = torch.randn(n, device=device).to(dtype)
         out = torch.empty(n // W, device=device, dtype=dtype)
         fn = lambda: (mesh.reduce_scatter(out, inp, 1.0, False), DONE)[1]  # noqa: E731
+    elif op == "ipc_mesh_all_to_all":
+        # the EP token exchange (parallel/ep.py MeshExpertDispatcher) with balanced routing: E = 2W experts, every
+        # expert gets the same number of 4096-wide rows, one dispatch = device count exchange + push + copy-out
+        from ..parallel.ep import MeshExpertDispatcher
+        D, E = 4096, 2 * W
+        rows = max(E, n // D // E * E)
+        disp = MeshExpertDispatcher(comm, E, device, rows, D, dtype, capacity_factor=1.0)
+        mesh_ref.append(disp.mesh)
+        x = torch.randn(rows, D, device=device).to(dtype)
+        offsets = (torch.arange(E + 1, device=device) * (rows // E)).to(torch.int32)
+        counts = (offsets[1:] - offsets[:-1]).long()
+        fn = lambda: (disp.dispatch(x, counts, offsets), DONE)[1]  # noqa: E731
     elif op == "reduce_scatter":
         inp = torch.randn(n, device=device).to(dtype)
         out = torch.empty(n // W, device=device, dtype=dtype)

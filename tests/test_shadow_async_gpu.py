@@ -39,6 +39,7 @@ def _run(model, world, async_mode, steps=3, ga=2, **kw):
     torch.cuda.synchronize()
     issued = comm.issued + sum(getattr(c, "issued", 0) for c in {id(x): x for x in _comms(eng)}.values()
                                if c is not comm)
+    issued += eng.mesh.issued if eng.mesh is not None else 0  # collectives the xGMI mesh ran on its streams
     return {k: getattr(eng, k).detach().cpu().clone() for k in STATE}, issued
 
 
@@ -62,6 +63,16 @@ CASES = {
     "zero3_nonresident_local": dict(zero_stage=3, max_live_parameters=0, max_reuse_distance=0,
                                     local_grad_accum=True),
     "zero3_offload_param": dict(zero_stage=3, offload_param="cpu", local_grad_accum=False),
+    # the device-driven xGMI mesh transport in shadow mode (parallel/xgmi_mesh.py): gathers pulled and gradients
+    # push-reduced on the mesh's own streams after the spin, versus inline on the compute stream
+    "zero2_mesh": dict(zero_stage=2, local_grad_accum=False, xgmi_mesh="on"),
+    "zero2_local_mesh": dict(zero_stage=2, local_grad_accum=True, xgmi_mesh="on"),
+    "zero3_resident_mesh": dict(zero_stage=3, local_grad_accum=False, xgmi_mesh="on"),
+    "zero3_resident_local_mesh": dict(zero_stage=3, local_grad_accum=True, xgmi_mesh="on"),
+    "zero3_nonresident_mesh": dict(zero_stage=3, max_live_parameters=0, max_reuse_distance=0, local_grad_accum=False,
+                                   xgmi_mesh="on"),
+    "zero3_nonresident_local_mesh": dict(zero_stage=3, max_live_parameters=0, max_reuse_distance=0,
+                                         local_grad_accum=True, xgmi_mesh="on"),
 }
 
 
@@ -74,9 +85,9 @@ def test_async_shadow_is_bit_identical_llama(case):
         assert torch.equal(ref[k], got[k]), (case, k, float((ref[k].float() - got[k].float()).abs().max()))
 
 
-@pytest.mark.parametrize("stage", [2, 3])
-def test_async_shadow_is_bit_identical_mixtral_ep4(stage):
-    kw = dict(zero_stage=stage, expert_parallel_size=4, local_grad_accum=False)
+@pytest.mark.parametrize("stage,mesh", [(2, "off"), (3, "off"), (2, "on"), (3, "on")])
+def test_async_shadow_is_bit_identical_mixtral_ep4(stage, mesh):
+    kw = dict(zero_stage=stage, expert_parallel_size=4, local_grad_accum=False, xgmi_mesh=mesh)
     ref, _ = _run("mixtral-tiny", 4, False, **kw)
     got, n_async = _run("mixtral-tiny", 4, True, **kw)
     assert n_async > 0

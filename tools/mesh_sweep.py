@@ -29,7 +29,8 @@ def main() -> int:
     comm = Comm()
     rows = []
     if env.device.type == "cuda" and env.world > 1:
-        rows = sweep(comm, env.device, ops=MESH_OPS + ("all_gather", "reduce_scatter"), sizes_mb=(16, 64, 256))
+        rows = sweep(comm, env.device, ops=MESH_OPS + ("all_gather", "reduce_scatter", "all_to_all"),
+                     sizes_mb=(16, 64, 256))
     if env.rank == 0:
         rec = {"mesh_sweep": rows, "world": env.world}
         print("[mesh-sweep] " + json.dumps(rec), flush=True)
