@@ -120,6 +120,8 @@ def main() -> int:
                     help="run the ZeRO collectives over the device-driven xGMI mesh instead of RCCL rings")
     ap.add_argument("--defer-expert-wgrad", default="auto", choices=["auto", "on", "off"],
                     help="MoE: expert dW once per step over the concatenated micro-batches")
+    ap.add_argument("--optimizer-overlap", default="on", choices=["on", "off"],
+                    help="ZeRO-3: per-group AdamW on a side stream, overlapping the next step's forward")
     ap.add_argument("--telemetry-interval", type=float, default=2.0)
     ap.add_argument("--n-layers", type=int, default=0,
                     help="override the preset's layer count (kernel profiling of big models on one GPU only; "
@@ -154,7 +156,8 @@ def main() -> int:
                         max_reuse_distance=_knob(args.reuse_distance),
                         local_grad_accum={"on": True, "off": False}.get(args.local_grads, args.local_grads),
                         hip_graphs=args.hip_graphs, fp16=args.dtype == "fp16", xgmi_mesh=args.xgmi_mesh,
-                        defer_expert_wgrad={"on": True, "off": False}.get(args.defer_expert_wgrad, "auto"))
+                        defer_expert_wgrad={"on": True, "off": False}.get(args.defer_expert_wgrad, "auto"),
+                        optimizer_overlap=args.optimizer_overlap == "on")
     t0 = time.time()
     eng = ZeroEngine(mcfg, ecfg, env.device, comm)
     if env.device.type == "cuda":

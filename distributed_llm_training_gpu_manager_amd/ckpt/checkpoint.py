@@ -349,6 +349,7 @@ class AsyncCheckpointer:
         self._saves += 1
         if not self.active:
             return tag
+        self.engine.join_optimizer()  # an overlapped optimizer update may still be writing the state
         if self.busy:  # previous write-out still streaming from the snapshot buffer
             self.wait()
         save_id = f"{step}.{self._restart}.{self._saves}"
@@ -625,6 +626,7 @@ class AsyncCheckpointer:
         when all ranks hold the same newest step, else the disk tags newest first; a candidate that fails
         on any rank is rolled back on all of them (recorded in ``self.rollbacks``)."""
         self.rollbacks = []
+        self.engine.join_optimizer()
         self.restore_stats: Dict[str, Any] = {}
         agree = _Agree(self.engine)
         auto = tag in ("auto", "latest")

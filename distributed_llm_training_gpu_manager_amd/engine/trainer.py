@@ -408,6 +408,7 @@ class Trainer:
         if getattr(a, "dump_state", None):
             # per-rank outcome for multi-rank drills: exit code, last step read, this rank's fp32 partition
             os.makedirs(a.dump_state, exist_ok=True)
+            self.engine.join_optimizer()
             torch.save({"rc": rc, "rank": self.env.rank, "last_step": self.log[-1]["step"] if self.log else start,
                         "step_count": self.engine.step_count, "master": self.engine.master.detach().cpu().clone()},
                        os.path.join(a.dump_state, f"rank{self.env.rank}.pt"))

@@ -128,6 +128,11 @@ class EngineConfig:
     # the stored gradient is then final); falls back to ops.grad_stats whenever a weight was not covered.
     # A/B on Mixtral 2-layer: 133.2k -> 136.3k tokens/s, identical grad norm (profiles/fused_expert_stats_ab_r03.json)
     fused_expert_grad_stats: bool = True
+    # ZeRO-3 on the device (no offload, no mesh): the AdamW of step s runs on a side stream as one launch per
+    # parameter group in forward order, and step s+1's forward waits for each group's update where it fetches
+    # the group instead of for the whole update -- the bandwidth-bound optimizer overlaps the first layers'
+    # compute (element for element the same arithmetic as the single flat launch)
+    optimizer_overlap: bool = True
     nvme_path: Optional[str] = None
     param_nvme_path: Optional[str] = None  # offload_param.nvme_path (defaults to nvme_path)
     # ZeRO-2/3 gradients: True = accumulate fp32 locally and reduce-scatter once per optimizer step;
@@ -290,9 +295,33 @@ def lr_at(cfg: EngineConfig, step: int) -> float:
     return hi * frac  # WarmupDecayLR: linear decay to 0 at total_num_steps
 
 
+def _state_tensor(name: str) -> property:
+    """An engine state tensor (fp32 master / moments / gradient partition, compute copy) read from outside the
+    step: waits for an overlapped optimizer update still writing it (cfg.optimizer_overlap). The fetch path reads
+    the raw tensor after waiting for its own group only."""
+    key = "_st_" + name
+
+    def get(self):
+        if self.__dict__.get("_opt_pending"):
+            self.join_optimizer()
+        return self.__dict__[key]
+
+    def put(self, v) -> None:
+        self.__dict__[key] = v
+    return property(get, put)
+
+
 class ZeroEngine:
+    master = _state_tensor("master")
+    exp_avg = _state_tensor("exp_avg")
+    exp_avg_sq = _state_tensor("exp_avg_sq")
+    grad_shard = _state_tensor("grad_shard")
+    p16_shard = _state_tensor("p16_shard")
+
     def __init__(self, model_cfg: ModelConfig, cfg: EngineConfig, device: torch.device, comm: Optional[Comm] = None,
                  ep_comm: Optional[Comm] = None):
+        self._opt_pending: Dict[int, Any] = {}  # group -> event of its overlapped update (cfg.optimizer_overlap)
+        self._opt_stream = None
         self.mcfg, self.cfg, self.device = model_cfg, cfg, device
         self.comm = comm or Comm()
         self.W, self.rank = self.comm.world, self.comm.rank
@@ -415,6 +444,10 @@ class ZeroEngine:
             for gi in gis:
                 self._bwd_last_visit[gi] = min(si, self._bwd_last_visit.get(gi, si))
         self._live: Dict[int, Tuple[torch.Tensor, Handle]] = {}
+        first_use: List[int] = []
+        for _, gis in self.stages:
+            first_use += [gi for gi in gis if gi not in first_use]
+        self._opt_order = first_use + [g.idx for g in self.groups if g.idx not in first_use]
         self._build_live_plan()
         if cfg.transposed_weight_cache and self.stage == 3:
             self._add_resident_tcache()
@@ -603,6 +636,7 @@ class ZeroEngine:
         self._p16_from_master()
 
     def _p16_from_master(self) -> None:
+        self.join_optimizer()
         self._pver = getattr(self, "_pver", 0) + 1
         if self.offload is not None:
             self.offload.push_params(self.p16_shard)
@@ -692,11 +726,14 @@ class ZeroEngine:
         return g.gcomm.all_gather(out, shard, async_op=True)
 
     def _shard16(self, g: FlatGroup) -> torch.Tensor:
-        return self.p16_shard.narrow(0, g.shard_off, g.shard_numel)
+        return self._st_p16_shard.narrow(0, g.shard_off, g.shard_numel)  # (no join: _issue_gather waited)
 
     def _issue_gather(self, gi: int) -> None:
         if gi in self._live:
             return
+        ev = self._opt_pending.pop(gi, None)
+        if ev is not None:  # the group's overlapped optimizer update (and its bf16 copy) lands first
+            torch.cuda.current_stream(self.device).wait_event(ev)
         g = self.groups[gi]
         if self.stage < 3:
             flat = self.p16_full.narrow(0, g.full_off, g.numel)
@@ -1043,6 +1080,7 @@ class ZeroEngine:
 
     def sync_params_from_master(self) -> None:
         """Recompute the bf16 compute copies from the fp32 master (after restore / external edits)."""
+        self.join_optimizer()
         self._p16_from_master()
         if self.stage in (1, 2):
             hs = [self._all_gather(g, self.p16_full.narrow(0, g.full_off, g.numel), self._shard16(g))
@@ -1105,6 +1143,7 @@ class ZeroEngine:
             hk(self)
         if self.param_nvme is not None:  # the partition file changes below: read-aheads in flight are stale
             self.param_nvme.drop_read_ahead()
+        self.join_optimizer()
         self.step_count += 1
         cfg = self.cfg
         self._global_grad_stats()
@@ -1116,11 +1155,14 @@ class ZeroEngine:
             self._offload_step(lr, float(sst[1]) if sst is not None else 1.0)
         else:
             self._mesh_quiesce()
-            ops.adamw_step_(self.master, self.exp_avg, self.exp_avg_sq, self.grad_shard,
-                            None if self.param_host else self.p16_shard,
-                            self.stats, lr=lr,
-                            beta1=cfg.betas[0], beta2=cfg.betas[1], eps=cfg.eps, weight_decay=cfg.weight_decay,
-                            step=self.step_count, grad_scale=1.0, max_norm=cfg.grad_clip, scale_state=sst)
+            if self._opt_overlap_ok():
+                self._adamw_overlapped(lr, sst)
+            else:
+                ops.adamw_step_(self.master, self.exp_avg, self.exp_avg_sq, self.grad_shard,
+                                None if self.param_host else self.p16_shard,
+                                self.stats, lr=lr,
+                                beta1=cfg.betas[0], beta2=cfg.betas[1], eps=cfg.eps, weight_decay=cfg.weight_decay,
+                                step=self.step_count, grad_scale=1.0, max_norm=cfg.grad_clip, scale_state=sst)
             if self.param_host:
                 self._p16_to_host()
             self._mesh_publish()
@@ -1136,6 +1178,45 @@ class ZeroEngine:
         if self.scaler is not None:
             self.scaler.update_(self.stats)
         return {"lr": lr, "stats": self.stats}
+
+    def _opt_overlap_ok(self) -> bool:
+        return (self.cfg.optimizer_overlap and self.is_cuda and self.stage == 3 and self.offload is None
+                and not self.param_host and self.mesh is None)
+
+    def _adamw_overlapped(self, lr: float, sst: Optional[torch.Tensor]) -> None:
+        """cfg.optimizer_overlap: one AdamW launch per group on the optimizer stream, in forward order, each
+        followed by an event that the group's next fetch waits on (_issue_gather). The statistics and the
+        loss-scaler state are snapshotted first: the main stream moves on (scaler update, next step) at once."""
+        cfg = self.cfg
+        if self._opt_stream is None:
+            self._opt_stream = torch.cuda.Stream(self.device)
+            self._opt_stats = torch.empty_like(self.stats)
+            self._opt_sst = torch.empty_like(sst) if sst is not None else None
+        self._opt_stats.copy_(self.stats)
+        if sst is not None:
+            self._opt_sst.copy_(sst)
+        side = self._opt_stream
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            for gi in self._opt_order:
+                g = self.groups[gi]
+                if g.shard_numel > 0:
+                    sl = lambda t: t.narrow(0, g.shard_off, g.shard_numel)  # noqa: E731
+                    ops.adamw_step_(sl(self._st_master), sl(self._st_exp_avg), sl(self._st_exp_avg_sq),
+                                    sl(self._st_grad_shard), sl(self._st_p16_shard), self._opt_stats, lr=lr, beta1=cfg.betas[0],
+                                    beta2=cfg.betas[1], eps=cfg.eps, weight_decay=cfg.weight_decay,
+                                    step=self.step_count, grad_scale=1.0, max_norm=cfg.grad_clip,
+                                    scale_state=self._opt_sst)
+                ev = torch.cuda.Event()
+                ev.record(side)
+                self._opt_pending[gi] = ev
+
+    def join_optimizer(self) -> None:
+        """The current stream waits for the overlapped optimizer updates still pending: anything that reads or
+        writes master / moments / gradients / the compute copy outside the forward's fetches calls this."""
+        if self._opt_pending:
+            torch.cuda.current_stream(self.device).wait_stream(self._opt_stream)
+            self._opt_pending.clear()
 
     def _offload_step(self, lr: float, inv_scale: float) -> None:
         """Host AdamW over the offloaded partition; the clip / overflow decision needs the stats on the host
@@ -1218,6 +1299,7 @@ class ZeroEngine:
         The captured work writes only storage that outlives the graph (fp32 gradient shard, loss
         accumulator, the transposed-weight cache -- refreshed inside the graph at every replay, since
         its version is invalidated before the capture); activations live in the graph's private pool."""
+        self.join_optimizer()  # (a captured wait on an event recorded outside the capture is not allowed)
         key = tuple((tuple(i.shape), tuple(l.shape)) for i, l in micro_batches)
         g = self._graph
         if g is None or g["key"] != key:
@@ -1297,6 +1379,7 @@ class ZeroEngine:
         all-gathered, expert tensors concatenated over the EP ranks (global expert order). Collective -- every
         rank runs the whole loop; one group is materialised at a time (checkpoint module capture streams it).
         `dtype`: cast the shard first (16-bit module state: half the gather bytes)."""
+        self.join_optimizer()
         for g in self.groups:
             shard = buf.narrow(0, g.shard_off, g.shard_numel)
             if shard.device != self.device:  # offloaded optimizer state: collectives run on device tensors

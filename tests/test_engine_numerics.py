@@ -200,6 +200,31 @@ def test_hip_graph_replay_matches_eager_gpu(model, stage):
     assert err < 1e-4, err
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("model", ["llama-tiny", "mixtral-tiny"])
+def test_optimizer_overlap_matches_flat_update_gpu(model):
+    """cfg.optimizer_overlap (one AdamW launch per group on a side stream, each waited for at the group's next
+    fetch) trains the same model bit for bit as the single flat launch: losses, fp32 master, second moment and
+    the bf16 compute copy after several clipped steps."""
+    mc = get_config(model)
+    res = {}
+    for on in (False, True):
+        ec = EngineConfig(zero_stage=3, micro_batch_size=2, seq_len=64, grad_accum=3, lr=1e-3, grad_clip=0.5,
+                          scheduler="constant", init_device="cpu", optimizer_overlap=on)
+        eng = ZeroEngine(mc, ec, torch.device("cuda"))
+        g = torch.Generator().manual_seed(13)
+        losses = []
+        for _ in range(4):
+            toks = [torch.randint(0, mc.vocab_size, (2, 65), generator=g) for _ in range(3)]
+            m = eng.train_step([(t[:, :-1].cuda(), t[:, 1:].cuda()) for t in toks])
+            losses.append(float(m["loss"]))
+        assert (eng._opt_stream is not None) == on
+        res[on] = (losses, eng.master.cpu(), eng.exp_avg_sq.cpu(), eng.p16_shard.cpu())
+    assert res[True][0] == res[False][0]
+    for a, b in zip(res[True][1:], res[False][1:]):
+        assert torch.equal(a, b)
+
+
 def test_gpt2_kept_graph_matches_activation_checkpointing_cpu():
     """GPT-2 blocks keep their forward autograd graph; with activation checkpointing the engine re-runs
     the block right before its backward instead. Both must train identically."""
