@@ -33,30 +33,13 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restr
   // in 8 KB runs. Row-major over all the column tiles (28672 columns: 448 tiles) left ~37 row tiles in flight
   // and scattered the writes over every output row in 4.6 KB runs: 3.2 vs 4.9 TB/s (Mixtral dW re-layout).
   constexpr int64_t kSuper = 64;
-  for (int64_t t = wave; t < tiles; t += nwaves) {
+  auto tile_of = [&](int64_t t, int64_t& rt, int64_t& ct) {
     const int64_t sc = t / (tiles_r * kSuper), tt = t - sc * tiles_r * kSuper;
     const int64_t w = min(kSuper, tiles_c - sc * kSuper);
-    const int64_t r0 = (tt / w) * 64 + kr * 8, c0 = (sc * kSuper + tt % w) * 64 + kc * 8;
-    if (r0 >= R || c0 >= C) continue;  // R, C are multiples of 8: a chunk is wholly in or out
-    short8 v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (rows == nullptr) {
-        v[j] = *reinterpret_cast<const short8*>(x + (r0 + j) * ldx + c0);
-      } else {
-        const int src = rows[r0 + j];
-        if (srcs.n == 0) {
-          v[j] = src >= 0 ? *reinterpret_cast<const short8*>(x + (int64_t)src * ldx + c0) : (short8)(0);
-        } else {  // several sources: rows[] = (source << 24) | row; the source is picked among kernel arguments
-          const int si = src >= 0 ? (src >> 24) : 0;
-          const bf16* xs = srcs.p[0];
-#pragma unroll
-          for (int q = 1; q < 8; ++q) xs = si == q ? srcs.p[q] : xs;
-          v[j] = src >= 0 ? *reinterpret_cast<const short8*>(xs + (int64_t)(src & 0xFFFFFF) * ldx + c0)
-                          : (short8)(0);
-        }
-      }
-    }
+    rt = tt / w;
+    ct = sc * kSuper + tt % w;
+  };
+  auto store = [&](const short8 (&v)[8], int64_t r0, int64_t c0) {
     short8 o[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -64,6 +47,52 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restr
       for (int j = 0; j < 8; ++j) o[i][j] = v[j][i];
 #pragma unroll
     for (int i = 0; i < 8; ++i) *reinterpret_cast<short8*>(y + (c0 + i) * ldy + r0) = o[i];
+  };
+  if (rows == nullptr) {
+    for (int64_t t = wave; t < tiles; t += nwaves) {
+      int64_t rt, ct;
+      tile_of(t, rt, ct);
+      const int64_t r0 = rt * 64 + kr * 8, c0 = ct * 64 + kc * 8;
+      if (r0 >= R || c0 >= C) continue;  // R, C are multiples of 8: a chunk is wholly in or out
+      short8 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const short8*>(x + (r0 + j) * ldx + c0);
+      store(v, r0, c0);
+    }
+    return;
+  }
+  // remapped rows: lane l holds the source of the tile's row l (one load per lane instead of 8 dependent ones),
+  // fetched a tile ahead so the data loads do not wait behind the index load; rows[] = (source << 24) | row
+  auto idx_of = [&](int64_t t) -> int {
+    if (t >= tiles) return -1;
+    int64_t rt, ct;
+    tile_of(t, rt, ct);
+    const int64_t r = rt * 64 + lane;
+    return r < R ? rows[r] : -1;
+  };
+  int idx_next = idx_of(wave);
+  for (int64_t t = wave; t < tiles; t += nwaves) {
+    const int idx = idx_next;
+    idx_next = idx_of(t + nwaves);
+    int64_t rt, ct;
+    tile_of(t, rt, ct);
+    const int64_t r0 = rt * 64 + kr * 8, c0 = ct * 64 + kc * 8;
+    int srcj[8];  // (shuffled while every lane is active: a lane past the edge still serves its index)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) srcj[j] = __shfl(idx, kr * 8 + j);
+    if (r0 >= R || c0 >= C) continue;
+    short8 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int src = srcj[j];
+      const int si = srcs.n > 0 && src >= 0 ? (src >> 24) : 0;
+      const bf16* xs = srcs.n == 0 ? x : srcs.p[0];
+#pragma unroll
+      for (int q = 1; q < 8; ++q) xs = si == q ? srcs.p[q] : xs;
+      const int64_t row = srcs.n == 0 ? (int64_t)src : (int64_t)(src & 0xFFFFFF);
+      v[j] = src >= 0 ? *reinterpret_cast<const short8*>(xs + row * ldx + c0) : (short8)(0);
+    }
+    store(v, r0, c0);
   }
 }
 

@@ -35,6 +35,7 @@ from ..ops.gemm import grad_mm, transpose_multi
 from ..ops import gemm_mfma as gm
 from ..ops.moe import moe_combine, moe_combine_bwd, moe_permute, pad_plan_multi
 from ..parallel.ep import ExpertDispatcher
+from ..utils.streams import side_stream
 from .common import ParamSpec, Params, StepContext, Unit
 from .config import ModelConfig
 from .llama import LlamaBlock, LlamaEmbedding, LlamaHead
@@ -268,11 +269,29 @@ class MixtralBlock(LlamaBlock):
             # the last launch over a weight stores its final gradient: tally the statistics there
             xs = self._final_stats(ctx) if i + gm.MAX_SEGMENTS >= len(stash) else None
             src, poff = pad_plan_multi(offs, sum(int(t[0].shape[0]) for t in part))
-            for wname, ia, ib in (("w_down", 0, 1), ("w_gate_up", 2, 3)):
-                at_ = transpose_multi([t[ia] for t in part], src)
-                bt_ = transpose_multi([t[ib] for t in part], src)
-                gm.grouped_wgrad(g[wname], at_, bt_, poff, acc or i > 0, kmajor=True, stats=xs)
-                del at_, bt_
+            # the w_gate_up operands' re-layout (bandwidth-bound) runs on a side stream under the w_down dW GEMM
+            side = side_stream(src.device, "moe_dw")
+            cur = torch.cuda.current_stream(src.device) if side is not None else None
+            ops_d = (transpose_multi([t[0] for t in part], src), transpose_multi([t[1] for t in part], src))
+            if side is not None:
+                side.wait_stream(cur)
+                with torch.cuda.stream(side):
+                    ops_g = (transpose_multi([t[2] for t in part], src), transpose_multi([t[3] for t in part], src))
+                ev = torch.cuda.Event()
+                ev.record(side)
+                for t in part:  # stashed operands freed after the flush: keep them until the side copies ran
+                    t[2].record_stream(side)
+                    t[3].record_stream(side)
+            else:
+                ops_g = (transpose_multi([t[2] for t in part], src), transpose_multi([t[3] for t in part], src))
+            gm.grouped_wgrad(g["w_down"], ops_d[0], ops_d[1], poff, acc or i > 0, kmajor=True, stats=xs)
+            del ops_d
+            if side is not None:
+                cur.wait_event(ev)
+                for t in ops_g:  # allocated on the side stream, consumed here
+                    t.record_stream(cur)
+            gm.grouped_wgrad(g["w_gate_up"], ops_g[0], ops_g[1], poff, acc or i > 0, kmajor=True, stats=xs)
+            del ops_g
             self._count_stats(ctx, xs, 2)
 
     def moe_backward(self, p: Params, g: Params, hn2: torch.Tensor, saved, dout: torch.Tensor, ctx: StepContext):

@@ -41,6 +41,7 @@ Schedule (one micro-batch)
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import time
 from dataclasses import dataclass, field
@@ -402,6 +403,7 @@ class ZeroEngine:
         self._init_params()
         self._pver = 0  # bumped whenever the bf16 compute copy changes
         self._tcache: Dict[int, Tuple[int, Dict[str, torch.Tensor]]] = {}
+        self._tcache_ev: Dict[int, Any] = {}  # group -> event of a side-stream cache rebuild not yet waited for
         self._tnames: Dict[int, List[Tuple[str, Tuple[int, ...]]]] = {}
         self._expert_wt = cfg.expert_weight_cache
         if cfg.transposed_weight_cache:
@@ -773,13 +775,31 @@ class ZeroEngine:
                      for n, shp in self._tnames[gi]}
         if ver != self._pver:
             from ..ops.gemm import transpose
-            for n, shp in self._tnames[gi]:
-                if len(shp) == 3:
-                    for e in range(shp[0]):
-                        transpose(views[n][e], out=cache[n][e])
-                else:
-                    transpose(views[n], out=cache[n])
+            from ..utils.streams import side_stream
+            # only the backward's input-gradient GEMMs read the copies: the rebuild (bandwidth-bound) runs on a side
+            # stream beside the forward's compute and the group's next fetch (its backward visit) waits for it
+            side = side_stream(self.device, "tcache") if self.is_cuda else None
+            cur = torch.cuda.current_stream(self.device) if side is not None else None
+            if side is not None:
+                side.wait_stream(cur)
+            with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                for n, shp in self._tnames[gi]:
+                    if len(shp) == 3:
+                        for e in range(shp[0]):
+                            transpose(views[n][e], out=cache[n][e])
+                    else:
+                        transpose(views[n], out=cache[n])
+            if side is not None:
+                for n, _ in self._tnames[gi]:
+                    views[n].record_stream(side)  # a gathered buffer may be released before the copies run
+                ev = torch.cuda.Event()
+                ev.record(side)
+                self._tcache_ev[gi] = ev
             self._tcache[gi] = (self._pver, cache)
+        else:
+            ev = self._tcache_ev.pop(gi, None)
+            if ev is not None:
+                torch.cuda.current_stream(self.device).wait_event(ev)
         return {n + ".T": t for n, t in cache.items()}
 
     def release(self, gis) -> None:
@@ -1313,6 +1333,7 @@ class ZeroEngine:
                 self._tcache[gi] = (-1, self._tcache[gi][1])
             self._graph = None
             torch.cuda.synchronize(self.device)
+            self._tcache_ev.clear()  # (all side-stream rebuilds have run; a captured wait may not name them)
             torch.cuda.empty_cache()  # hand the eager step's cached activation blocks to the graph pool
             graph = torch.cuda.CUDAGraph()
             err = None

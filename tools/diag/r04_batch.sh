@@ -10,6 +10,8 @@ done
 echo "== probe done"
 timeout -k 10 400 python -u -m pytest tests/test_engine_numerics.py tests/test_kernels_gpu.py tests/test_gemm_mfma_gpu.py tests/test_moe_dw_layout.py -m gpu -x -q --timeout 120 --timeout-method thread -k "overlap or transpose or mfma or grouped or gemm or layout" > $O/pytest_overlap.log 2>&1 || { tail -30 $O/pytest_overlap.log; exit 1; }
 tail -2 $O/pytest_overlap.log
+timeout -k 10 600 python -u -m pytest tests/test_shadow_async_gpu.py tests/test_gpu_runtime.py tests/test_fp16_path.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_overlap2.log 2>&1 || { tail -30 $O/pytest_overlap2.log; exit 1; }
+tail -2 $O/pytest_overlap2.log
 for ov in on off on off; do
   timeout -k 10 400 python bench.py --model mixtral-8x7b --n-layers 2 --seq 4096 --ga 4 --steps 6 --warmup 2 --optimizer-overlap $ov --no-telemetry >> $O/mixtral_overlap_ab.jsonl 2>> $O/mixtral_overlap_ab.err
 done

@@ -71,6 +71,21 @@ def main():
         res[name] = {"ms": round(ms, 4), "TFs": round(2.0 * 4 * R * M * N / ms / 1e9, 1), "sha": _digest(out)}
         del a_t, b_t, out
 
+    # the engine's dW path: the step's 4 micro-batches re-laid into ONE K-major operand (transpose_multi), one
+    # grouped-K launch per weight (mode 2)
+    from distributed_llm_training_gpu_manager_amd.ops.gemm import transpose_multi
+    from distributed_llm_training_gpu_manager_amd.ops.moe import pad_plan_multi
+    offs_m = torch.stack([offs] * 4)
+    src_m, poff_m = pad_plan_multi(offs_m, 4 * R)
+    for name, M in (("dw1_w13", 2 * F), ("dw1_w2", d)):
+        N = F if M == d else d
+        at = transpose_multi([torch.randn(R, M, device=dev).to(torch.bfloat16) for _ in range(4)], src_m)
+        bt = transpose_multi([torch.randn(R, N, device=dev).to(torch.bfloat16) for _ in range(4)], src_m)
+        out = torch.zeros(E, M, N, device=dev)
+        ms = _time(lambda: gm.grouped_wgrad(out, at, bt, poff_m, acc=True, kmajor=True), max(2, iters // 3))
+        res[name] = {"ms": round(ms, 4), "TFs": round(2.0 * 4 * R * M * N / ms / 1e9, 1), "sha": _digest(out)}
+        del at, bt, out
+
     a = torch.randn(R, d, device=dev).to(torch.bfloat16)
     b = torch.randn(2 * F, d, device=dev).to(torch.bfloat16)
     o = torch.empty(R, 2 * F, device=dev, dtype=torch.bfloat16)
@@ -88,6 +103,10 @@ def main():
         y = transpose_multi(xs, src_m)
         res[name] = {"ms": round(ms, 4), "TBs": round(2.0 * 2 * y.numel() / ms / 1e9, 2), "sha": _digest(y)}
         del xs, y
+    big = torch.randn(4 * R, 2 * F, device=dev).to(torch.bfloat16)  # tmulti_dgu's shape without the remap
+    ms = _time(lambda: transpose(big), iters)
+    res["t_big"] = {"ms": round(ms, 4), "TBs": round(2.0 * 2 * big.numel() / ms / 1e9, 2)}
+    del big
     w = torch.randn(2 * F, d, device=dev).to(torch.bfloat16)
     wt = torch.empty(d, 2 * F, device=dev, dtype=torch.bfloat16)
     ms = _time(lambda: transpose(w, out=wt), iters)
