@@ -230,8 +230,15 @@ __device__ __forceinline__ void vm_wait() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int MODE, bool AK, bool BKM, int EPI, int SC>
+template <int MODE, bool AK, bool BKM, int EPI>
 __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
+  // DMA placement (tools/gemm_sched_ab.py, profiles/gemm_sched_ab_r04.jsonl, random operands, bit-identical output):
+  //   SC 0: one half-tile per phase (B1 | A1 | A0 | B0), phase reads 12 / 4 / 8 / 0 -- grouped-K (dW) modes, where it
+  //         measured 4-6 % faster than SC 1;
+  //   SC 1: two half-tiles in phases 2 and 4 only (B1 A1 of t+1 | B0 A0 of t+2), none beside phase 1's 12 reads --
+  //         dense and grouped-M, 2-4 % faster than SC 0. (Also reading B half 0 of the next tile a phase early
+  //         into a second register set, phase reads 8 / 4 / 8 / 4, was slower than SC 1 on every shape.)
+  constexpr int SC = (MODE == kDense || MODE == kGroupM) ? 1 : 0;
   __shared__ __attribute__((aligned(1024))) char smem[4 * TILE_BYTES];  // [buf][A | B][half][16 KiB]
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -413,8 +420,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     };
     bf16x8 af[4][2], bq0[2][2], bq1[2][2];
-    bf16x8 bq0s[2][2][2];  // SC 1/2: B half 0 per K-tile parity (SC 2 reads the next tile's a phase early)
-    auto mma_q = [&](int mq, int nq, const bf16x8 (&b0r)[2][2]) {
+    auto mma = [&](int mq, int nq) {
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
@@ -422,10 +428,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j)
-            acc[4 * mq + i][2 * nq + j] = mfma16(nq ? bq1[j][s2] : b0r[j][s2], af[i][s2], acc[4 * mq + i][2 * nq + j]);
+            acc[4 * mq + i][2 * nq + j] = mfma16(nq ? bq1[j][s2] : bq0[j][s2], af[i][s2], acc[4 * mq + i][2 * nq + j]);
       __builtin_amdgcn_s_setprio(0);
     };
-    auto mma = [&](int mq, int nq) { mma_q(mq, nq, bq0); };
     // a partial M tile (a group's last row tile, or M % 256): a wave skips the MFMAs of its 64-row quadrants that
     // lie wholly past the valid rows (their outputs are never stored) -- the SIMD's MFMA pipe then serves the
     // partner wave alone. Barriers and DMA are unchanged, so the phase structure holds for every wave.
@@ -437,8 +442,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
       if (wr * 128 + mq * 64 < rv) mma(mq, nq);
       raw_barrier();
     };
-    // SC 1/2: the wait keeps the N youngest DMA instructions in flight when the newest stage call issued
-    auto phase_end_n = [&](auto nc, bool issued, int mq, int nq, const bf16x8 (&b0r)[2][2]) {
+    // SC 1: the wait keeps the N youngest DMA instructions in flight when the newest stage call issued (N 99: none)
+    auto phase_end_n = [&](auto nc, bool issued, int mq, int nq) {
       constexpr int N = decltype(nc)::value;
       if constexpr (N != 99) {
         if (issued)
@@ -448,7 +453,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
       }
       raw_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (wr * 128 + mq * 64 < rv) mma_q(mq, nq, b0r);
+      if (wr * 128 + mq * 64 < rv) mma(mq, nq);
       raw_barrier();
     };
     auto ktile = [&](auto bufc, int t) {
@@ -483,46 +488,29 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
       // phase 4: registers only -> quadrant (1, 0)
       phase_end(stage(1, 0, t + 2), 1, 0);
       } else {
-      // SC 1/2: DMA only in phases 2 (B1, A1 of t+1) and 4 (B0, A0 of t+2); SC 2 also reads B half 0 of t+1 in
-      // phase 4 into the other register set (phase reads 8 / 4 / 8 / 4 instead of 12 / 4 / 8 / 0)
-      auto& q0 = bq0s[buf];
-      auto& q0n = bq0s[buf ^ 1];
+      // SC 1: DMA only in phases 2 (B1, A1 of t+1) and 4 (B0, A0 of t+2). Waits: phase p's retires what
+      // phase p+1 reads, counted in DMA instructions issued after it (6 / 8 / none / 8)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        if constexpr (SC == 1) {
 #pragma unroll
-          for (int j = 0; j < 2; ++j) q0[j][s2] = frag<BKM, false>(b0, wc * 32 + 16 * j, s2, lane, kv);
-        }
+        for (int j = 0; j < 2; ++j) bq0[j][s2] = frag<BKM, false>(b0, wc * 32 + 16 * j, s2, lane, kv);
 #pragma unroll
         for (int i = 0; i < 4; ++i) af[i][s2] = frag<AK, false>(a0, wr * 64 + 16 * i, s2, lane, kv);
       }
-      phase_end_n(std::integral_constant<int, 6>{}, t + 1 < nk, 0, 0, q0);
+      phase_end_n(std::integral_constant<int, 6>{}, t + 1 < nk, 0, 0);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
         for (int j = 0; j < 2; ++j) bq1[j][s2] = frag<BKM, false>(b1, wc * 32 + 16 * j, s2, lane, kv);
       stage(1, 1, t + 1);
-      phase_end_n(std::integral_constant<int, 8>{}, stage(0, 1, t + 1), 0, 1, q0);
+      phase_end_n(std::integral_constant<int, 8>{}, stage(0, 1, t + 1), 0, 1);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
         for (int i = 0; i < 4; ++i) af[i][s2] = frag<AK, false>(a1, wr * 64 + 16 * i, s2, lane, kv);
-      if constexpr (SC == 2)
-        phase_end_n(std::integral_constant<int, 6>{}, t + 1 < nk, 1, 1, q0);
-      else
-        phase_end_n(std::integral_constant<int, 99>{}, true, 1, 1, q0);
-      if constexpr (SC == 2) {
-        if (t + 1 < nk) {
-          const char* b0n = region(buf ^ 1, 1, 0);
-          const int kvn = min(BK, k_hi - (k_lo + (t + 1) * BK));
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) q0n[j][s2] = frag<BKM, false>(b0n, wc * 32 + 16 * j, s2, lane, kvn);
-        }
-      }
+      phase_end_n(std::integral_constant<int, 99>{}, true, 1, 1);
       stage(1, 0, t + 2);
-      phase_end_n(std::integral_constant<int, 8>{}, stage(0, 0, t + 2), 1, 0, q0);
+      phase_end_n(std::integral_constant<int, 8>{}, stage(0, 0, t + 2), 1, 0);
       }
     };
     if constexpr (SC == 0) {
@@ -546,12 +534,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
     else
       vm_wait<0>();
     raw_barrier();
-    if constexpr (SC == 2) {
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) bq0s[0][j][s2] = frag<BKM, false>(region(0, 1, 0), wc * 32 + 16 * j, s2, lane, BK);
-    }
     }
     if (wr == 1) raw_barrier();  // wave row 1 runs one barrier behind
     for (int t = 0; t < nk; t += 2) {
@@ -642,30 +624,14 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 }
 
 
-template <int MODE, bool AK, bool BKM, int SC>
-void launch_sc(int epi, dim3 grid, hipStream_t st, const GemmArgs& a) {
-  if (epi == kStoreBf16)
-    gemm_mfma_kernel<MODE, AK, BKM, kStoreBf16, SC><<<grid, NTHR, 0, st>>>(a);
-  else if (epi == kStoreF32)
-    gemm_mfma_kernel<MODE, AK, BKM, kStoreF32, SC><<<grid, NTHR, 0, st>>>(a);
-  else
-    gemm_mfma_kernel<MODE, AK, BKM, kAccF32, SC><<<grid, NTHR, 0, st>>>(a);
-}
-
-int g_sched() {
-  static int v = [] { const char* e = getenv("DLGM_GEMM_SCHED"); return e ? atoi(e) : 0; }();
-  return v;
-}
-
 template <int MODE, bool AK, bool BKM>
 void launch_epi(int epi, dim3 grid, hipStream_t st, const GemmArgs& a) {
-  const int sc = g_sched();
-  if (sc == 1)
-    launch_sc<MODE, AK, BKM, 1>(epi, grid, st, a);
-  else if (sc == 2)
-    launch_sc<MODE, AK, BKM, 2>(epi, grid, st, a);
+  if (epi == kStoreBf16)
+    gemm_mfma_kernel<MODE, AK, BKM, kStoreBf16><<<grid, NTHR, 0, st>>>(a);
+  else if (epi == kStoreF32)
+    gemm_mfma_kernel<MODE, AK, BKM, kStoreF32><<<grid, NTHR, 0, st>>>(a);
   else
-    launch_sc<MODE, AK, BKM, 0>(epi, grid, st, a);
+    gemm_mfma_kernel<MODE, AK, BKM, kAccF32><<<grid, NTHR, 0, st>>>(a);
 }
 
 }  // namespace

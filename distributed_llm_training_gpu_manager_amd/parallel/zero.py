@@ -733,9 +733,8 @@ class ZeroEngine:
     def _issue_gather(self, gi: int) -> None:
         if gi in self._live:
             return
-        ev = self._opt_pending.pop(gi, None)
-        if ev is not None:  # the group's overlapped optimizer update (and its bf16 copy) lands first
-            torch.cuda.current_stream(self.device).wait_event(ev)
+        if self.groups[gi].P > 1:  # the gather reads the shard: the group's overlapped update lands first
+            self._wait_update(gi)
         g = self.groups[gi]
         if self.stage < 3:
             flat = self.p16_full.narrow(0, g.full_off, g.numel)
@@ -756,6 +755,7 @@ class ZeroEngine:
         out: Dict[str, torch.Tensor] = {}
         for gi in (gis if isinstance(gis, tuple) else (gis,)):
             self._issue_gather(gi)
+            self._wait_update(gi)  # (P == 1: the views ARE the shard; wait where they are used, not at prefetch)
             flat, h = self._live[gi]
             h.wait()
             if self.param_host and self.is_cuda:
@@ -893,7 +893,8 @@ class ZeroEngine:
         gradients, no scratch buffer and no separate accumulate pass.
         """
         if g.P == 1:
-            return self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
+            # (raw partition, no join: a group is written only after its forward fetch waited for its update)
+            return self._st_grad_shard.narrow(0, g.shard_off, g.shard_numel)
         if self.stage == 1 or self.local_grads:
             return self.grad_full.narrow(0, g.gfull_off, g.numel)
         return None
@@ -915,7 +916,7 @@ class ZeroEngine:
         if (g.P > 1 and self.local_grads and self.cfg.comm_dtype == torch.bfloat16 and tgt.dtype == torch.float32
                 and self._mesh_ok(g, tgt)):
             # mesh: the fp32 accumulator is cast to bf16 on the fly as it is pushed; the reduce writes the shard
-            shard_tgt = self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
+            shard_tgt = self._st_grad_shard.narrow(0, g.shard_off, g.shard_numel)
             scale = (1.0 / g.comm.world if avg else 1.0) * post
             m = self.mesh
             h = m.run_async(lambda: m.reduce_scatter(shard_tgt, tgt, scale, False), [tgt, shard_tgt], "rs")
@@ -925,11 +926,11 @@ class ZeroEngine:
             # fp32), then the shard is written (beta = 0) from the reduced chunk
             src = tgt.to(self.cfg.comm_dtype)
             out = torch.empty(g.shard_numel, dtype=src.dtype, device=self.device)
-            shard_tgt = self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
+            shard_tgt = self._st_grad_shard.narrow(0, g.shard_off, g.shard_numel)
             pending.append((g.comm.reduce_scatter(out, src, avg=avg, async_op=True),
                             (shard_tgt, out, 0.0, None, post, src)))
         elif g.P > 1:  # ZeRO-1 (or fp32 comm): reduce-scatter the local accumulator into this rank's shard
-            out = self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
+            out = self._st_grad_shard.narrow(0, g.shard_off, g.shard_numel)
             pending.append((g.comm.reduce_scatter(out, tgt, avg=avg, async_op=True), _Scaled(out, post, tgt)))
         elif g.comm.world > 1:  # ZeRO-0 / persistent (replicated) group: plain data parallel
             pending.append((g.comm.all_reduce(tgt, avg=avg, async_op=True), _Scaled(tgt, post)))
@@ -944,7 +945,7 @@ class ZeroEngine:
         g = self.groups[gi]
         beta = 0.0 if first_micro else 1.0
         alpha = (1.0 / self.ep_size if g.kind == "expert" else 1.0) * self._post(g)
-        shard_tgt = self.grad_shard.narrow(0, g.shard_off, g.shard_numel)
+        shard_tgt = self._st_grad_shard.narrow(0, g.shard_off, g.shard_numel)
         if gbuf.dtype == torch.bfloat16 and self.cfg.comm_dtype == torch.bfloat16 and self._mesh_ok(g, gbuf):
             scale = alpha * (1.0 / g.comm.world if not self.cfg.prescale_gradients else 1.0)
             m = self.mesh
@@ -1230,6 +1231,11 @@ class ZeroEngine:
                 ev = torch.cuda.Event()
                 ev.record(side)
                 self._opt_pending[gi] = ev
+
+    def _wait_update(self, gi: int) -> None:
+        ev = self._opt_pending.pop(gi, None)
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
 
     def join_optimizer(self) -> None:
         """The current stream waits for the overlapped optimizer updates still pending: anything that reads or

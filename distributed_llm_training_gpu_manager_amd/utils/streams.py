@@ -16,9 +16,6 @@ _STREAMS: Dict[Tuple[int, str], "torch.cuda.Stream"] = {}
 def side_stream(device: torch.device, name: str) -> Optional["torch.cuda.Stream"]:
     if device.type != "cuda" or torch.cuda.is_current_stream_capturing():
         return None
-    import os
-    if os.environ.get("DLGM_SIDE_STREAMS") == "0":  # TEMP A/B
-        return None
     idx = device.index if device.index is not None else torch.cuda.current_device()
     key = (idx, name)
     s = _STREAMS.get(key)
