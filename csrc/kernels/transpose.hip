@@ -26,18 +26,19 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restr
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const int64_t tiles_c = (C + 63) >> 6, tiles_r = (R + 63) >> 6, tiles = tiles_r * tiles_c;
+  // tile bookkeeping in 32 bits (a 64-bit divide is a long software sequence; tiles, R < 2^30 are checked on the host)
+  const int tiles_c = (int)((C + 63) >> 6), tiles_r = (int)((R + 63) >> 6), tiles = tiles_r * tiles_c;
   const int kr = lane >> 3, kc = lane & 7;  // row chunk, column chunk inside the 64x64 tile
   // tiles walk super-columns of kSuper column tiles, row tiles within: the ~16k waves in flight cover
   // ~256 row tiles x 64 column tiles, so every output row is written in ~32 KB runs and every input row read
-  // in 8 KB runs. Row-major over all the column tiles (28672 columns: 448 tiles) left ~37 row tiles in flight
-  // and scattered the writes over every output row in 4.6 KB runs: 3.2 vs 4.9 TB/s (Mixtral dW re-layout).
-  constexpr int64_t kSuper = 64;
-  auto tile_of = [&](int64_t t, int64_t& rt, int64_t& ct) {
-    const int64_t sc = t / (tiles_r * kSuper), tt = t - sc * tiles_r * kSuper;
-    const int64_t w = min(kSuper, tiles_c - sc * kSuper);
+  // in 8 KB runs
+  constexpr int kSuper = 64;
+  const int wv = (int)wave, nw = (int)nwaves;
+  auto tile_of = [&](int t, int& rt, int& ct) {
+    const int sc = t / (tiles_r * kSuper), tt = t - sc * tiles_r * kSuper;
+    const int w = min(kSuper, tiles_c - sc * kSuper);
     rt = tt / w;
-    ct = sc * kSuper + tt % w;
+    ct = sc * kSuper + (tt - rt * w);
   };
   auto store = [&](const short8 (&v)[8], int64_t r0, int64_t c0) {
     short8 o[8];
@@ -49,10 +50,10 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restr
     for (int i = 0; i < 8; ++i) *reinterpret_cast<short8*>(y + (c0 + i) * ldy + r0) = o[i];
   };
   if (rows == nullptr) {
-    for (int64_t t = wave; t < tiles; t += nwaves) {
-      int64_t rt, ct;
+    for (int t = wv; t < tiles; t += nw) {
+      int rt, ct;
       tile_of(t, rt, ct);
-      const int64_t r0 = rt * 64 + kr * 8, c0 = ct * 64 + kc * 8;
+      const int64_t r0 = (int64_t)rt * 64 + kr * 8, c0 = (int64_t)ct * 64 + kc * 8;
       if (r0 >= R || c0 >= C) continue;  // R, C are multiples of 8: a chunk is wholly in or out
       short8 v[8];
 #pragma unroll
@@ -61,37 +62,46 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restr
     }
     return;
   }
-  // remapped rows: lane l holds the source of the tile's row l (one load per lane instead of 8 dependent ones),
-  // fetched a tile ahead so the data loads do not wait behind the index load; rows[] = (source << 24) | row
-  auto idx_of = [&](int64_t t) -> int {
-    if (t >= tiles) return -1;
-    int64_t rt, ct;
+  // remapped rows: lane l resolves the source row pointer of the tile's row l once (rows[] = (source << 24) | row,
+  // or -1 for a zero row), a tile ahead so the data loads do not wait behind the index load; the 8 rows a lane
+  // reads are then fetched from their owners by two lane shuffles each
+  auto row_ptr = [&](int t) -> uint64_t {
+    if (t >= tiles) return 0;
+    int rt, ct;
     tile_of(t, rt, ct);
-    const int64_t r = rt * 64 + lane;
-    return r < R ? rows[r] : -1;
-  };
-  int idx_next = idx_of(wave);
-  for (int64_t t = wave; t < tiles; t += nwaves) {
-    const int idx = idx_next;
-    idx_next = idx_of(t + nwaves);
-    int64_t rt, ct;
-    tile_of(t, rt, ct);
-    const int64_t r0 = rt * 64 + kr * 8, c0 = ct * 64 + kc * 8;
-    int srcj[8];  // (shuffled while every lane is active: a lane past the edge still serves its index)
+    const int64_t r = (int64_t)rt * 64 + lane;
+    const int src = r < R ? rows[r] : -1;
+    if (src < 0) return 0;
+    const bf16* xs = x;
+    int64_t row = src;
+    if (srcs.n > 0) {
+      const int si = src >> 24;
+      xs = srcs.p[0];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) srcj[j] = __shfl(idx, kr * 8 + j);
+      for (int q = 1; q < 8; ++q) xs = si == q ? srcs.p[q] : xs;
+      row = src & 0xFFFFFF;
+    }
+    return reinterpret_cast<uint64_t>(xs + row * ldx);
+  };
+  uint64_t next = row_ptr(wv);
+  for (int t = wv; t < tiles; t += nw) {
+    const uint64_t mine = next;
+    next = row_ptr(t + nw);
+    int rt, ct;
+    tile_of(t, rt, ct);
+    const int64_t r0 = (int64_t)rt * 64 + kr * 8, c0 = (int64_t)ct * 64 + kc * 8;
+    uint64_t pj[8];  // (shuffled while every lane is active: a lane past the edge still serves its row)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int srcl = kr * 8 + j;
+      const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)mine, srcl), hi = (uint32_t)__shfl((int)(mine >> 32), srcl);
+      pj[j] = ((uint64_t)hi << 32) | lo;
+    }
     if (r0 >= R || c0 >= C) continue;
     short8 v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int src = srcj[j];
-      const int si = srcs.n > 0 && src >= 0 ? (src >> 24) : 0;
-      const bf16* xs = srcs.n == 0 ? x : srcs.p[0];
-#pragma unroll
-      for (int q = 1; q < 8; ++q) xs = si == q ? srcs.p[q] : xs;
-      const int64_t row = srcs.n == 0 ? (int64_t)src : (int64_t)(src & 0xFFFFFF);
-      v[j] = src >= 0 ? *reinterpret_cast<const short8*>(xs + row * ldx + c0) : (short8)(0);
-    }
+    for (int j = 0; j < 8; ++j)
+      v[j] = pj[j] ? *reinterpret_cast<const short8*>(reinterpret_cast<const bf16*>(pj[j]) + c0) : (short8)(0);
     store(v, r0, c0);
   }
 }
@@ -118,6 +128,7 @@ at::Tensor dlgm_transpose(const at::Tensor& x, const c10::optional<at::Tensor>& 
               "transpose: out must be a contiguous [C, R] tensor of x's dtype");
   if (R == 0 || C == 0) return y;
   const int64_t tiles = ((R + 63) / 64) * ((C + 63) / 64);
+  TORCH_CHECK(tiles < (int64_t(1) << 30) && R < (int64_t(1) << 30), "transpose: too many 64x64 tiles");
   const int64_t grid = std::min<int64_t>((tiles + 3) / 4, 256 * 16);
   transpose_bf16_kernel<<<grid, 256, 0, c10::hip::getCurrentHIPStream()>>>(
       reinterpret_cast<const bf16*>(x.data_ptr()), reinterpret_cast<bf16*>(y.data_ptr()), R, C, x.stride(0), R,
@@ -147,6 +158,7 @@ at::Tensor dlgm_transpose_multi(const std::vector<at::Tensor>& xs, const at::Ten
   at::Tensor y = at::empty({C, P}, x0.options());
   if (P == 0 || C == 0) return y;
   const int64_t tiles = ((P + 63) / 64) * ((C + 63) / 64);
+  TORCH_CHECK(tiles < (int64_t(1) << 30) && P < (int64_t(1) << 30), "transpose_multi: too many 64x64 tiles");
   const int64_t grid = std::min<int64_t>((tiles + 3) / 4, 256 * 16);
   transpose_bf16_kernel<<<grid, 256, 0, c10::hip::getCurrentHIPStream()>>>(
       reinterpret_cast<const bf16*>(x0.data_ptr()), reinterpret_cast<bf16*>(y.data_ptr()), P, C, x0.stride(0), P,
