@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 MODE=${1:-all}
 STEPS=${BENCH_STEPS:-3}
-run() { echo "== $*" ; "$@"; }
+run() { echo "== $*" >&2; "$@"; }
 if [ "$MODE" = "all" ] || [ "$MODE" = "test" ]; then
   run timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
   tail -30 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
