@@ -464,76 +464,76 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
       const char* b0 = region(buf, 1, 0);
       const char* b1 = region(buf, 1, 1);
       if constexpr (SC == 0) {
-      // phase 1: A half 0 + B half 0 -> quadrant (0, 0)
+        // phase 1: A half 0 + B half 0 -> quadrant (0, 0)
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
+        for (int s2 = 0; s2 < 2; ++s2) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) bq0[j][s2] = frag<BKM, false>(b0, wc * 32 + 16 * j, s2, lane, kv);
+          for (int j = 0; j < 2; ++j) bq0[j][s2] = frag<BKM, false>(b0, wc * 32 + 16 * j, s2, lane, kv);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) af[i][s2] = frag<AK, false>(a0, wr * 64 + 16 * i, s2, lane, kv);
-      }
-      phase_end(stage(1, 1, t + 1), 0, 0);
-      // phase 2: B half 1 -> quadrant (0, 1)
+          for (int i = 0; i < 4; ++i) af[i][s2] = frag<AK, false>(a0, wr * 64 + 16 * i, s2, lane, kv);
+        }
+        phase_end(stage(1, 1, t + 1), 0, 0);
+        // phase 2: B half 1 -> quadrant (0, 1)
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
+        for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) bq1[j][s2] = frag<BKM, false>(b1, wc * 32 + 16 * j, s2, lane, kv);
-      phase_end(stage(0, 1, t + 1), 0, 1);
-      // phase 3: A half 1 -> quadrant (1, 1)
+          for (int j = 0; j < 2; ++j) bq1[j][s2] = frag<BKM, false>(b1, wc * 32 + 16 * j, s2, lane, kv);
+        phase_end(stage(0, 1, t + 1), 0, 1);
+        // phase 3: A half 1 -> quadrant (1, 1)
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
+        for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) af[i][s2] = frag<AK, false>(a1, wr * 64 + 16 * i, s2, lane, kv);
-      phase_end(stage(0, 0, t + 2), 1, 1);
-      // phase 4: registers only -> quadrant (1, 0)
-      phase_end(stage(1, 0, t + 2), 1, 0);
+          for (int i = 0; i < 4; ++i) af[i][s2] = frag<AK, false>(a1, wr * 64 + 16 * i, s2, lane, kv);
+        phase_end(stage(0, 0, t + 2), 1, 1);
+        // phase 4: registers only -> quadrant (1, 0)
+        phase_end(stage(1, 0, t + 2), 1, 0);
       } else {
-      // SC 1: DMA only in phases 2 (B1, A1 of t+1) and 4 (B0, A0 of t+2). Waits: phase p's retires what
-      // phase p+1 reads, counted in DMA instructions issued after it (6 / 8 / none / 8)
+        // SC 1: DMA only in phases 2 (B1, A1 of t+1) and 4 (B0, A0 of t+2). Waits: phase p's retires what
+        // phase p+1 reads, counted in DMA instructions issued after it (6 / 8 / none / 8)
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
+        for (int s2 = 0; s2 < 2; ++s2) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) bq0[j][s2] = frag<BKM, false>(b0, wc * 32 + 16 * j, s2, lane, kv);
+          for (int j = 0; j < 2; ++j) bq0[j][s2] = frag<BKM, false>(b0, wc * 32 + 16 * j, s2, lane, kv);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) af[i][s2] = frag<AK, false>(a0, wr * 64 + 16 * i, s2, lane, kv);
-      }
-      phase_end_n(std::integral_constant<int, 6>{}, t + 1 < nk, 0, 0);
+          for (int i = 0; i < 4; ++i) af[i][s2] = frag<AK, false>(a0, wr * 64 + 16 * i, s2, lane, kv);
+        }
+        phase_end_n(std::integral_constant<int, 6>{}, t + 1 < nk, 0, 0);
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
+        for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) bq1[j][s2] = frag<BKM, false>(b1, wc * 32 + 16 * j, s2, lane, kv);
-      stage(1, 1, t + 1);
-      phase_end_n(std::integral_constant<int, 8>{}, stage(0, 1, t + 1), 0, 1);
+          for (int j = 0; j < 2; ++j) bq1[j][s2] = frag<BKM, false>(b1, wc * 32 + 16 * j, s2, lane, kv);
+        stage(1, 1, t + 1);
+        phase_end_n(std::integral_constant<int, 8>{}, stage(0, 1, t + 1), 0, 1);
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
+        for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) af[i][s2] = frag<AK, false>(a1, wr * 64 + 16 * i, s2, lane, kv);
-      phase_end_n(std::integral_constant<int, 99>{}, true, 1, 1);
-      stage(1, 0, t + 2);
-      phase_end_n(std::integral_constant<int, 8>{}, stage(0, 0, t + 2), 1, 0);
+          for (int i = 0; i < 4; ++i) af[i][s2] = frag<AK, false>(a1, wr * 64 + 16 * i, s2, lane, kv);
+        phase_end_n(std::integral_constant<int, 99>{}, true, 1, 1);
+        stage(1, 0, t + 2);
+        phase_end_n(std::integral_constant<int, 8>{}, stage(0, 0, t + 2), 1, 0);
       }
     };
     if constexpr (SC == 0) {
-    // prologue: the six half-tiles the loop expects in flight (in the loop's stage order)
-    stage(0, 0, 0);
-    stage(1, 0, 0);
-    stage(1, 1, 0);
-    stage(0, 1, 0);
-    stage(0, 0, 1);
-    wait(stage(1, 0, 1));
-    raw_barrier();
+      // prologue: the six half-tiles the loop expects in flight (in the loop's stage order)
+      stage(0, 0, 0);
+      stage(1, 0, 0);
+      stage(1, 1, 0);
+      stage(0, 1, 0);
+      stage(0, 0, 1);
+      wait(stage(1, 0, 1));
+      raw_barrier();
     } else {
-    // prologue: the queue of the steady state before tile 0 (B0 A0 | B1 A1 of 0 | B0 A0 of 1)
-    stage(1, 0, 0);
-    stage(0, 0, 0);
-    stage(1, 1, 0);
-    stage(0, 1, 0);
-    stage(1, 0, 1);
-    if (stage(0, 0, 1))
-      vm_wait<8>();
-    else
-      vm_wait<0>();
-    raw_barrier();
+      // prologue: the queue of the steady state before tile 0 (B0 A0 | B1 A1 of 0 | B0 A0 of 1)
+      stage(1, 0, 0);
+      stage(0, 0, 0);
+      stage(1, 1, 0);
+      stage(0, 1, 0);
+      stage(1, 0, 1);
+      if (stage(0, 0, 1))
+        vm_wait<8>();
+      else
+        vm_wait<0>();
+      raw_barrier();
     }
     if (wr == 1) raw_barrier();  // wave row 1 runs one barrier behind
     for (int t = 0; t < nk; t += 2) {
