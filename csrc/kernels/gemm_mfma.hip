@@ -555,6 +555,35 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
     }
   };
   constexpr bool KSTATS = (MODE == kGroupK || MODE == kGroupKSeg) && EPI != kStoreBf16;
+  if constexpr (EPI == kStoreBf16) {
+    // bf16 tile through LDS: the accumulators' native layout gives 8-byte stores of 16 rows x 32 B each; staged as
+    // a row-major [256][512 B] image (16-B chunk c of row r at c ^ (r & 31): conflict-free 8-byte writes and
+    // 16-byte reads), every wave then stores two whole 512-B rows per instruction
+    __syncthreads();  // every wave is done with the operand images (the last DMA was drained by vmcnt(0))
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+      const int mrow = wr * 128 + 16 * mi + i;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int byte = (wc * 64 + 16 * ni + 4 * g) * 2;  // within the 512-B row
+        const int ch = (byte >> 4) ^ (mrow & 31);
+        bf16x4 v = {(bf16)acc[mi][ni][0], (bf16)acc[mi][ni][1], (bf16)acc[mi][ni][2], (bf16)acc[mi][ni][3]};
+        *reinterpret_cast<bf16x4*>(smem + mrow * 512 + ch * 16 + (byte & 8)) = v;
+      }
+    }
+    __syncthreads();
+    const int half = lane >> 5, c = lane & 31;
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+      const int r = 32 * w + 2 * it + half;
+      if (r >= rows_valid) break;  // (rows are ascending in it: the rest of this wave's rows are past the end)
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + r * 512 + ((c ^ (r & 31)) << 4));
+      *reinterpret_cast<bf16x8*>(C + ((int64_t)(m0 + r) * p.ldc + n0 + c * 8) * 2) = v;
+    }
+    return;
+  }
+  // fp32 tiles store from the accumulators' layout (16-B stores of 16 rows x 64 B; an LDS-staged whole-row form
+  // measured neutral here, unlike the bf16 one)
 #pragma unroll
   for (int mi = 0; mi < 8; ++mi) {
     const int mrow = wr * 128 + 16 * mi + i;  // row within the block tile
@@ -575,14 +604,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
     }
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) {
-      const int n = n0 + wc * 64 + 16 * ni + 4 * g;
-      if constexpr (EPI == kStoreBf16) {
-        bf16x4 v = {(bf16)acc[mi][ni][0], (bf16)acc[mi][ni][1], (bf16)acc[mi][ni][2], (bf16)acc[mi][ni][3]};
-        *reinterpret_cast<bf16x4*>(C + (m * p.ldc + n) * 2) = v;
-      } else {
-        *reinterpret_cast<f32x4*>(C + (m * p.ldc + n) * 4) = acc[mi][ni];
-        if (KSTATS) tally(acc[mi][ni]);
-      }
+      *reinterpret_cast<f32x4*>(C + (m * p.ldc + n0 + wc * 64 + 16 * ni + 4 * g) * 4) = acc[mi][ni];
+      if (KSTATS) tally(acc[mi][ni]);
     }
   }
   if constexpr (KSTATS) {
@@ -671,6 +694,8 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_mfma: operands 16-byte aligned");
   }
   TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0 && ldc % 4 == 0, "gemm_mfma: leading strides must keep 16-B rows");
+  TORCH_CHECK(out32 || (ldc % 8 == 0 && reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0),
+              "gemm_mfma: a bf16 out needs 16-byte rows (the epilogue stores 16-B row chunks)");
   GemmArgs p{};
   p.a = reinterpret_cast<const bf16*>(a.data_ptr());
   p.b = reinterpret_cast<const bf16*>(b.data_ptr());
