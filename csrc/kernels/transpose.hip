@@ -108,7 +108,7 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restr
 
 }  // namespace
 
-// out[C, R] (contiguous) = x[R, C]^T; x may be a row-strided view (stride(1) == 1). With `rows` (int32 [R'],
+// out[C, R] = x[R, C]^T (a remapped out allocated here has its rows padded to 64 elements: a [C, R] view); x may be a row-strided view (stride(1) == 1). With `rows` (int32 [R'],
 // R' % 8 == 0) the transpose runs over a remapped row space: out[C, R'] with column r = x[rows[r]] (zeros for
 // rows[r] < 0) -- e.g. expert-sorted rows re-laid with every expert starting on an aligned column.
 at::Tensor dlgm_transpose(const at::Tensor& x, const c10::optional<at::Tensor>& out_opt,
@@ -123,15 +123,19 @@ at::Tensor dlgm_transpose(const at::Tensor& x, const c10::optional<at::Tensor>& 
   const int64_t R = remap ? rows_opt->numel() : x.size(0), C = x.size(1);
   TORCH_CHECK(R % 8 == 0 && C % 8 == 0 && x.stride(0) % 8 == 0, "transpose: dims and row stride must be multiples of 8");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "transpose: input must be 16-byte aligned");
-  at::Tensor y = out_opt.has_value() ? *out_opt : at::empty({C, R}, x.options());
-  TORCH_CHECK(y.sizes() == at::IntArrayRef({C, R}) && y.is_contiguous() && y.scalar_type() == x.scalar_type(),
-              "transpose: out must be a contiguous [C, R] tensor of x's dtype");
+  // a remapped (padded-layout) out that is allocated here gets its rows padded to whole 128-B lines: with
+  // R % 64 != 0 every 128-B chunk of a row would straddle two lines (a [28672, 33272] transpose ran at 3.1 TB/s
+  // against 4.7 TB/s at R = 32768). The plain transpose keeps a contiguous out (its R is a token count).
+  const int64_t ldy = out_opt.has_value() || !remap ? R : (R + 63) / 64 * 64;
+  at::Tensor y = out_opt.has_value() ? *out_opt : at::empty({C, ldy}, x.options()).narrow(1, 0, R);
+  TORCH_CHECK(y.sizes() == at::IntArrayRef({C, R}) && y.stride(0) == ldy && y.stride(1) == 1 &&
+                  y.scalar_type() == x.scalar_type(), "transpose: out must be a contiguous [C, R] tensor of x's dtype");
   if (R == 0 || C == 0) return y;
   const int64_t tiles = ((R + 63) / 64) * ((C + 63) / 64);
   TORCH_CHECK(tiles < (int64_t(1) << 30) && R < (int64_t(1) << 30), "transpose: too many 64x64 tiles");
   const int64_t grid = std::min<int64_t>((tiles + 3) / 4, 256 * 16);
   transpose_bf16_kernel<<<grid, 256, 0, c10::hip::getCurrentHIPStream()>>>(
-      reinterpret_cast<const bf16*>(x.data_ptr()), reinterpret_cast<bf16*>(y.data_ptr()), R, C, x.stride(0), R,
+      reinterpret_cast<const bf16*>(x.data_ptr()), reinterpret_cast<bf16*>(y.data_ptr()), R, C, x.stride(0), ldy,
       remap ? rows_opt->data_ptr<int>() : nullptr, Sources{{}, 0});
   DLGM_CHECK_HIP(hipGetLastError());
   return y;
@@ -155,13 +159,14 @@ at::Tensor dlgm_transpose_multi(const std::vector<at::Tensor>& xs, const at::Ten
     srcs.p[&x - &xs[0]] = reinterpret_cast<const bf16*>(x.data_ptr());
   }
   TORCH_CHECK(P % 8 == 0 && C % 8 == 0 && x0.stride(0) % 8 == 0, "transpose_multi: P, C and the row stride % 8");
-  at::Tensor y = at::empty({C, P}, x0.options());
+  const int64_t ldy = (P + 63) / 64 * 64;  // rows padded to whole 128-B lines (see dlgm_transpose)
+  at::Tensor y = at::empty({C, ldy}, x0.options()).narrow(1, 0, P);
   if (P == 0 || C == 0) return y;
   const int64_t tiles = ((P + 63) / 64) * ((C + 63) / 64);
   TORCH_CHECK(tiles < (int64_t(1) << 30) && P < (int64_t(1) << 30), "transpose_multi: too many 64x64 tiles");
   const int64_t grid = std::min<int64_t>((tiles + 3) / 4, 256 * 16);
   transpose_bf16_kernel<<<grid, 256, 0, c10::hip::getCurrentHIPStream()>>>(
-      reinterpret_cast<const bf16*>(x0.data_ptr()), reinterpret_cast<bf16*>(y.data_ptr()), P, C, x0.stride(0), P,
+      reinterpret_cast<const bf16*>(x0.data_ptr()), reinterpret_cast<bf16*>(y.data_ptr()), P, C, x0.stride(0), ldy,
       rows.data_ptr<int>(), srcs);
   DLGM_CHECK_HIP(hipGetLastError());
   return y;

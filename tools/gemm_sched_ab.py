@@ -106,6 +106,18 @@ def main():
     big = torch.randn(4 * R, 2 * F, device=dev).to(torch.bfloat16)  # tmulti_dgu's shape without the remap
     ms = _time(lambda: transpose(big), iters)
     res["t_big"] = {"ms": round(ms, 4), "TBs": round(2.0 * 2 * big.numel() / ms / 1e9, 2)}
+    ident = torch.arange(big.shape[0], dtype=torch.int32, device=dev)  # the remap path with the identity map
+    ms = _time(lambda: transpose(big, rows=ident), iters)
+    res["t_big_remap_id"] = {"ms": round(ms, 4), "TBs": round(2.0 * 2 * big.numel() / ms / 1e9, 2)}
+    perm = src_m.clone()
+    perm[perm >= 0] = torch.arange(int((perm >= 0).sum()), dtype=torch.int32, device=dev)  # the expert plan's
+    ms = _time(lambda: transpose(big, rows=perm[:big.shape[0]]), iters)                   # padding, one source
+    res["t_big_remap_pad"] = {"ms": round(ms, 4), "TBs": round(2.0 * 2 * big.numel() / ms / 1e9, 2)}
+    P = src_m.shape[0]
+    big2 = torch.randn(P, 2 * F, device=dev).to(torch.bfloat16)  # plain, with tmulti_dgu's padded row count
+    ms = _time(lambda: transpose(big2), iters)
+    res["t_big_P"] = {"ms": round(ms, 4), "TBs": round(2.0 * 2 * big2.numel() / ms / 1e9, 2), "P": P}
+    del big2
     del big
     w = torch.randn(2 * F, d, device=dev).to(torch.bfloat16)
     wt = torch.empty(d, 2 * F, device=dev, dtype=torch.bfloat16)
