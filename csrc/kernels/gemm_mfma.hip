@@ -232,13 +232,14 @@ __device__ __forceinline__ void vm_wait() {
 
 template <int MODE, bool AK, bool BKM, int EPI>
 __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
-  // DMA placement (tools/gemm_sched_ab.py, profiles/gemm_sched_ab_r04.jsonl, random operands, bit-identical output):
-  //   SC 0: one half-tile per phase (B1 | A1 | A0 | B0), phase reads 12 / 4 / 8 / 0 -- grouped-K (dW) modes, where it
-  //         measured 4-6 % faster than SC 1;
+  // DMA placement (tools/gemm_sched_ab.py, profiles/gemm_sched_ab_r04*.jsonl, random operands, bit-identical output):
   //   SC 1: two half-tiles in phases 2 and 4 only (B1 A1 of t+1 | B0 A0 of t+2), none beside phase 1's 12 reads --
-  //         dense and grouped-M, 2-4 % faster than SC 0. (Also reading B half 0 of the next tile a phase early
-  //         into a second register set, phase reads 8 / 4 / 8 / 4, was slower than SC 1 on every shape.)
-  constexpr int SC = (MODE == kDense || MODE == kGroupM) ? 1 : 0;
+  //         dense and grouped-M 2-4 % faster than SC 0, grouped-K (dW) 1.5 % faster once its operand rows are whole
+  //         128-B lines (profiles/transpose_row_pad_r04.jsonl; with misaligned rows SC 0 had measured 4-6 % faster);
+  //   SC 0: one half-tile per phase (B1 | A1 | A0 | B0), phase reads 12 / 4 / 8 / 0 -- kept for the segmented
+  //         grouped-K over token-major or per-segment operands. (Reading B half 0 of the next tile a phase early into
+  //         a second register set, phase reads 8 / 4 / 8 / 4, was slower than SC 1 on every shape.)
+  constexpr int SC = MODE == kGroupKSeg ? 0 : 1;
   __shared__ __attribute__((aligned(1024))) char smem[4 * TILE_BYTES];  // [buf][A | B][half][16 KiB]
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
