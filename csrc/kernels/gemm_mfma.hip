@@ -720,6 +720,8 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
   // rounds of 256 CUs, so a third round runs ~20 % full: split the long K in two (fp32 partials + one reduce)
   at::Tensor part;
   at::Tensor out_final = out;
+  // (round 4: splitting K >= 8192 in two and K >= 24576 in three measured 3-7 % slower on the Mixtral shapes than
+  // this rule: the fp32 partial traffic outweighs the fuller last round; profiles/gemm_splitk_policy_ab_r04.jsonl)
   if (mode == kGroupM && !out32 && out.is_contiguous() && ldc == N && p.tiles_n <= 16 && K >= 16384) {
     p.splitk = 2;
     part = at::empty({p.splitk, M, N}, out.options().dtype(at::kFloat));
