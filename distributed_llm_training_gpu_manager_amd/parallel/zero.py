@@ -323,6 +323,7 @@ class ZeroEngine:
                  ep_comm: Optional[Comm] = None):
         self._opt_pending: Dict[int, Any] = {}  # group -> event of its overlapped update (cfg.optimizer_overlap)
         self._opt_stream = None
+        self._opt_delay_cycles = 0  # test hook: spin the optimizer stream first (a missing wait then reads stale state)
         self.mcfg, self.cfg, self.device = model_cfg, cfg, device
         self.comm = comm or Comm()
         self.W, self.rank = self.comm.world, self.comm.rank
@@ -1221,6 +1222,8 @@ class ZeroEngine:
         side = self._opt_stream
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
+            if self._opt_delay_cycles:
+                torch.cuda._sleep(self._opt_delay_cycles)
             for gi in self._opt_order:
                 g = self.groups[gi]
                 if g.shard_numel > 0:

@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 STATE = ("master", "exp_avg", "exp_avg_sq", "grad_shard", "p16_shard")
 
 
-def _run(model, world, async_mode, steps=3, ga=2, **kw):
+def _run(model, world, async_mode, steps=3, ga=2, opt_delay=0, **kw):
     dev = torch.device("cuda", 0)
     mc = get_config(model)
     ec = EngineConfig(micro_batch_size=2, seq_len=64, grad_accum=ga, lr=1e-3, scheduler="constant", grad_clip=1.0)
@@ -29,6 +29,7 @@ def _run(model, world, async_mode, steps=3, ga=2, **kw):
         setattr(ec, k, v)
     comm = ShadowComm(world, 0, async_mode=async_mode, delay_cycles=200_000 if async_mode else 0)
     eng = ZeroEngine(mc, ec, dev, comm)
+    eng._opt_delay_cycles = opt_delay
     g = torch.Generator().manual_seed(3)
     for _ in range(steps):
         mbs = []
@@ -93,3 +94,19 @@ def test_async_shadow_is_bit_identical_mixtral_ep4(stage, mesh):
     assert n_async > 0
     for k in STATE:
         assert torch.equal(ref[k], got[k]), (stage, k, float((ref[k].float() - got[k].float()).abs().max()))
+
+
+@pytest.mark.parametrize("model,world,kw", [
+    ("llama-tiny", 1, dict(zero_stage=3)),
+    ("llama-tiny", 4, dict(zero_stage=3, local_grad_accum=True)),
+    ("llama-tiny", 4, dict(zero_stage=3, max_live_parameters=0, max_reuse_distance=0, local_grad_accum=False)),
+    ("mixtral-tiny", 4, dict(zero_stage=3, expert_parallel_size=4, local_grad_accum=False)),
+])
+def test_overlapped_optimizer_waits_per_group(model, world, kw):
+    """cfg.optimizer_overlap with the optimizer stream spun before its updates (so a gather, fetch or gradient write
+    that does not wait for its group's update reads or clobbers stale state): bit-identical to the flat update on the
+    compute stream, with asynchronous (RCCL-ordered) collectives."""
+    ref, _ = _run(model, world, True, optimizer_overlap=False, **kw)
+    got, _ = _run(model, world, True, opt_delay=2_000_000, optimizer_overlap=True, **kw)
+    for k in STATE:
+        assert torch.equal(ref[k], got[k]), (model, kw, k, float((ref[k].float() - got[k].float()).abs().max()))
