@@ -35,7 +35,7 @@ from ..ops.gemm import grad_mm, transpose_multi
 from ..ops import gemm_mfma as gm
 from ..ops.moe import moe_combine, moe_combine_bwd, moe_permute, pad_plan_multi
 from ..parallel.ep import ExpertDispatcher
-from ..utils.streams import side_stream
+from ..utils.streams import side_stream, test_delay
 from .common import ParamSpec, Params, StepContext, Unit
 from .config import ModelConfig
 from .llama import LlamaBlock, LlamaEmbedding, LlamaHead
@@ -276,6 +276,7 @@ class MixtralBlock(LlamaBlock):
             if side is not None:
                 side.wait_stream(cur)
                 with torch.cuda.stream(side):
+                    test_delay()
                     ops_g = (transpose_multi([t[2] for t in part], src), transpose_multi([t[3] for t in part], src))
                 ev = torch.cuda.Event()
                 ev.record(side)

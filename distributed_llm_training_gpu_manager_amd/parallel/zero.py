@@ -776,7 +776,7 @@ class ZeroEngine:
                      for n, shp in self._tnames[gi]}
         if ver != self._pver:
             from ..ops.gemm import transpose
-            from ..utils.streams import side_stream
+            from ..utils.streams import side_stream, test_delay
             # only the backward's input-gradient GEMMs read the copies: the rebuild (bandwidth-bound) runs on a side
             # stream beside the forward's compute and the group's next fetch (its backward visit) waits for it
             side = side_stream(self.device, "tcache") if self.is_cuda else None
@@ -784,6 +784,8 @@ class ZeroEngine:
             if side is not None:
                 side.wait_stream(cur)
             with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                if side is not None:
+                    test_delay()
                 for n, shp in self._tnames[gi]:
                     if len(shp) == 3:
                         for e in range(shp[0]):

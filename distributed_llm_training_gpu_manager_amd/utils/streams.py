@@ -11,6 +11,13 @@ from typing import Dict, Optional, Tuple
 import torch
 
 _STREAMS: Dict[Tuple[int, str], "torch.cuda.Stream"] = {}
+TEST_DELAY_CYCLES = {"cycles": 0}  # test hook: side-stream work first spins this long (a missing wait then shows)
+
+
+def test_delay() -> None:
+    """Called at the start of work queued on a side stream (inside its stream context)."""
+    if TEST_DELAY_CYCLES["cycles"]:
+        torch.cuda._sleep(TEST_DELAY_CYCLES["cycles"])
 
 
 def side_stream(device: torch.device, name: str) -> Optional["torch.cuda.Stream"]:

@@ -225,6 +225,31 @@ def test_optimizer_overlap_matches_flat_update_gpu(model):
         assert torch.equal(a, b)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("model", ["llama-tiny", "mixtral-tiny"])
+def test_side_stream_work_is_waited_for_gpu(model):
+    """The W^T cache rebuild and the MoE dW re-layout run on side streams (utils.streams): with that work spun
+    first, the trained state is bit-identical to a run without the spin -- every consumer waits for its event."""
+    from distributed_llm_training_gpu_manager_amd.utils import streams
+    mc = get_config(model)
+    res = {}
+    for delay in (0, 3_000_000):
+        streams.TEST_DELAY_CYCLES["cycles"] = delay
+        try:
+            ec = EngineConfig(zero_stage=3, micro_batch_size=2, seq_len=64, grad_accum=3, lr=1e-3,
+                              scheduler="constant", init_device="cpu")
+            eng = ZeroEngine(mc, ec, torch.device("cuda"))
+            g = torch.Generator().manual_seed(17)
+            for _ in range(3):
+                toks = [torch.randint(0, mc.vocab_size, (2, 65), generator=g) for _ in range(3)]
+                eng.train_step([(t[:, :-1].cuda(), t[:, 1:].cuda()) for t in toks])
+            res[delay] = (eng.master.cpu(), eng.exp_avg_sq.cpu())
+        finally:
+            streams.TEST_DELAY_CYCLES["cycles"] = 0
+    for a, b in zip(res[0], res[3_000_000]):
+        assert torch.equal(a, b)
+
+
 def test_gpt2_kept_graph_matches_activation_checkpointing_cpu():
     """GPT-2 blocks keep their forward autograd graph; with activation checkpointing the engine re-runs
     the block right before its backward instead. Both must train identically."""
