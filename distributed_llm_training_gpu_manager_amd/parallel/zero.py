@@ -37,7 +37,13 @@ Schedule (one micro-batch)
               and optimizer state stay partitioned
     step    : grad_stats (sum g^2, #non-finite) -> all_reduce(2 floats) ->
               fused AdamW reading clip coef / overflow flag on device ->
-              (stage 1/2) all-gather updated bf16 params
+              (stage 1/2) all-gather updated bf16 params. ZeRO-3 on the device runs the
+              AdamW as one launch per unit on a side stream (``optimizer_overlap``); the
+              next step's forward waits for each unit's update where it first uses it
+              (the gather of a partitioned unit, the fetch of an unpartitioned one).
+    side streams: the per-step W^T cache rebuild (read only by the backward's dX GEMMs)
+              and the MoE dW operand re-layout run beside the compute stream; every
+              consumer waits for their events (tests spin those streams to prove it).
 """
 from __future__ import annotations
 
