@@ -303,7 +303,7 @@ def main() -> int:
     if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
     if mesh_sweep:
-        _mesh_sweep_child(port, eng, args.comm_sweep_timeout + 60)
+        _mesh_sweep_child(port, eng, args.comm_sweep_timeout)
     return 0
 
 
