@@ -76,6 +76,7 @@ template <typename T> using vec8_t = typename vec8<T>::type;
 template <typename T> struct vec4;
 template <> struct vec4<bf16> { typedef bf16x4 type; };
 template <> struct vec4<f16> { typedef f16x4 type; };
+template <> struct vec4<float> { typedef f32x4 type; };
 template <typename T> using vec4_t = typename vec4<T>::type;
 
 template <typename T>
