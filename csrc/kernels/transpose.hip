@@ -133,7 +133,10 @@ at::Tensor dlgm_transpose(const at::Tensor& x, const c10::optional<at::Tensor>& 
   if (R == 0 || C == 0) return y;
   const int64_t tiles = ((R + 63) / 64) * ((C + 63) / 64);
   TORCH_CHECK(tiles < (int64_t(1) << 30) && R < (int64_t(1) << 30), "transpose: too many 64x64 tiles");
-  const int64_t grid = (tiles + 3) / 4;  // one 64x64 tile per wave (see transpose_grid_ab_r04.json)
+  // remapped: one 64x64 tile per wave (the MoE dW re-layout 6 % faster); plain: at most 16 workgroups per CU
+  // walking tiles (the activation transposes of the Llama step ran 13 % slower with one tile per wave;
+  // profiles/transpose_grid_ab_r04.json)
+  const int64_t grid = remap ? (tiles + 3) / 4 : std::min<int64_t>((tiles + 3) / 4, 256 * 16);
   transpose_bf16_kernel<<<grid, 256, 0, c10::hip::getCurrentHIPStream()>>>(
       reinterpret_cast<const bf16*>(x.data_ptr()), reinterpret_cast<bf16*>(y.data_ptr()), R, C, x.stride(0), ldy,
       remap ? rows_opt->data_ptr<int>() : nullptr, Sources{{}, 0});
@@ -164,7 +167,7 @@ at::Tensor dlgm_transpose_multi(const std::vector<at::Tensor>& xs, const at::Ten
   if (P == 0 || C == 0) return y;
   const int64_t tiles = ((P + 63) / 64) * ((C + 63) / 64);
   TORCH_CHECK(tiles < (int64_t(1) << 30) && P < (int64_t(1) << 30), "transpose_multi: too many 64x64 tiles");
-  const int64_t grid = (tiles + 3) / 4;  // one 64x64 tile per wave (see transpose_grid_ab_r04.json)
+  const int64_t grid = (tiles + 3) / 4;  // one 64x64 tile per wave (see dlgm_transpose)
   transpose_bf16_kernel<<<grid, 256, 0, c10::hip::getCurrentHIPStream()>>>(
       reinterpret_cast<const bf16*>(x0.data_ptr()), reinterpret_cast<bf16*>(y.data_ptr()), P, C, x0.stride(0), ldy,
       rows.data_ptr<int>(), srcs);
