@@ -32,22 +32,24 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_fwd_kernel(
   if (row >= T) return;
   const int nch = D >> 3;
   const size_t base = (size_t)row * D;
-  f32x8 v[MAXC];
+  // the row is held as raw 16-bit values (4 VGPRs per 8 elements, widened on use): half the registers of an fp32
+  // copy, so a whole T = 8192 launch is resident at once (same arithmetic, bit-identical outputs)
+  vec8_t<E> v[MAXC];
   float ss = 0.f;
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
     const int ch = lane + c * 64;
     if (ch < nch) {
-      v[c] = load8f(x + base + ch * 8);
       if constexpr (RESID) {
-        v[c] += load8f(r + base + ch * 8);
-        store8f(h + base + ch * 8, v[c]);
-        // the normalised value must be computed from the rounded residual
-        // stream so forward and backward see the same h.
-        v[c] = __builtin_convertvector(__builtin_convertvector(v[c], vec8_t<E>), f32x8);
+        // the normalised value is computed from the rounded residual stream, so forward and backward see the same h
+        v[c] = __builtin_convertvector(load8f(x + base + ch * 8) + load8f(r + base + ch * 8), vec8_t<E>);
+        *reinterpret_cast<vec8_t<E>*>(h + base + ch * 8) = v[c];
+      } else {
+        v[c] = *reinterpret_cast<const vec8_t<E>*>(x + base + ch * 8);
       }
+      const f32x8 f = __builtin_convertvector(v[c], f32x8);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) ss += v[c][j] * v[c][j];
+      for (int j = 0; j < 8; ++j) ss += f[j] * f[j];
     }
   }
   ss = wave_sum(ss);
@@ -58,7 +60,7 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_fwd_kernel(
     const int ch = lane + c * 64;
     if (ch < nch) {
       f32x8 wv = load8f(w + ch * 8);
-      store8f(y + base + ch * 8, v[c] * rs * wv);
+      store8f(y + base + ch * 8, __builtin_convertvector(v[c], f32x8) * rs * wv);
     }
   }
 }
