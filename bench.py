@@ -114,13 +114,14 @@ def main() -> int:
                     help="after the timed steps, measure RCCL busbw over xGMI (auto: when WORLD_SIZE > 1)")
     ap.add_argument("--comm-sweep-timeout", type=float, default=120.0)
     ap.add_argument("--mesh-sweep", default="auto", choices=["auto", "on", "off"],
-                    help="after the result line, measure the device-driven xGMI mesh all-gather / reduce-scatter in a "
-                         "child process per rank (auto: on the GPU when WORLD_SIZE > 1)")
+                    help="after the result line, in a child process per rank: check the mesh and RCCL against each "
+                         "other and one process ([mesh-check] on stderr), then on the GPU measure the device-driven "
+                         "xGMI mesh collectives (auto: when WORLD_SIZE > 1)")
     ap.add_argument("--xgmi-mesh", default="off", choices=["on", "off"],
                     help="run the ZeRO collectives over the device-driven xGMI mesh instead of RCCL rings")
     ap.add_argument("--defer-expert-wgrad", default="auto", choices=["auto", "on", "off"],
                     help="MoE: expert dW once per step over the concatenated micro-batches")
-    ap.add_argument("--optimizer-overlap", default="on", choices=["on", "off"],
+    ap.add_argument("--optimizer-overlap", default="off", choices=["on", "off"],
                     help="ZeRO-3: per-group AdamW on a side stream, overlapping the next step's forward")
     ap.add_argument("--telemetry-interval", type=float, default=2.0)
     ap.add_argument("--n-layers", type=int, default=0,
@@ -288,8 +289,7 @@ def main() -> int:
         dog.cancel()
         if out is not None:
             out["extra"]["comm_busbw"] = rows
-    mesh_sweep = args.mesh_sweep == "on" or (args.mesh_sweep == "auto" and env.world > 1
-                                               and env.device.type == "cuda")
+    mesh_sweep = args.mesh_sweep == "on" or (args.mesh_sweep == "auto" and env.world > 1)
     port = None
     if mesh_sweep and env.world > 1:  # agree on the child job's rendezvous port while the group still exists
         pt = torch.tensor([_free_port() if env.rank == 0 else 0], dtype=torch.int64, device=env.device)

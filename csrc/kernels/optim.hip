@@ -28,9 +28,11 @@ constexpr int kThreads = 256;
 // Streaming launches give every lane one 16-byte vector per operand (the kernels keep a grid-stride loop, so
 // the clamp only bounds the block index): AdamW 6.04 TB/s this way vs 5.51 TB/s with 8 workgroups per CU
 // looping, same arithmetic and bit-identical results (profiles/adamw_stats_grid_ab_r04.jsonl)
+// HIP on AMD needs gridDim.x * blockDim.x <= UINT32_MAX: cap the grid there (2^24 blocks of 256 lanes; the loop covers
+// the rest of a flat buffer over 2^34 elements)
 int64_t stream_grid(int64_t n_vec) {
   const int64_t b = (n_vec + kThreads - 1) / kThreads;
-  return std::max<int64_t>(1, std::min<int64_t>(b, INT32_MAX));
+  return std::max<int64_t>(1, std::min<int64_t>(b, (int64_t)(UINT32_MAX / kThreads)));
 }
 
 // grad_stats: 8 vectors in flight per lane, up to 16 workgroups per CU and per tensor (pure-read sweep of 4 GiB of

@@ -84,23 +84,27 @@ __device__ __forceinline__ uint64_t load_flag(uint64_t* f) {
   return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Poll until *f >= target (as signed: targets <= 0 pass at once); false after `timeout` wall-clock ticks.
-__device__ bool wait_ge(uint64_t* f, int64_t target, int64_t timeout) {
-  if (target <= 0) return true;
-  const uint64_t t0 = wall_clock64();
-  while ((int64_t)load_flag(f) < target) {
-    __builtin_amdgcn_s_sleep(2);
-    if ((int64_t)(wall_clock64() - t0) > timeout) return false;
-  }
-  return true;
-}
-
 __device__ __forceinline__ void set_word(int64_t* st, int idx, int64_t v) {
   __hip_atomic_store(st + idx, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ int64_t get_word(const int64_t* st, int idx) {
   return __hip_atomic_load(const_cast<int64_t*>(st) + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Poll until *f >= target (as signed: targets <= 0 pass at once); false after `timeout` wall-clock ticks, and at
+// once when this rank already recorded a timeout (the sticky error word): after one dead-peer timeout every later
+// wait of the step returns immediately and the host raises at the step boundary (XgmiMesh.check) instead of
+// spinning `timeout` once per collective.
+__device__ bool wait_ge(uint64_t* f, int64_t target, int64_t timeout, const int64_t* st) {
+  if (target <= 0) return true;
+  const uint64_t t0 = wall_clock64();
+  while ((int64_t)load_flag(f) < target) {
+    if (get_word(st, kStErr)) return false;
+    __builtin_amdgcn_s_sleep(2);
+    if ((int64_t)(wall_clock64() - t0) > timeout) return false;
+  }
+  return true;
 }
 
 // End of a multi-block producer / consumer: every wave drains its stores, the last workgroup to arrive stores
@@ -144,7 +148,7 @@ __global__ __launch_bounds__(64) void mesh_sync_kernel(int64_t* st, const int64_
   }
   if (wait_kind >= 0) {
     bool ok = true;
-    if (t < W) ok = wait_ge(flag_at(peers[me], wait_kind, ch, t), v - lag, timeout);
+    if (t < W) ok = wait_ge(flag_at(peers[me], wait_kind, ch, t), v - lag, timeout, st);
     if (!ok) set_word(st, kStErr, 1);
     __syncthreads();
     acquire_system();
@@ -367,7 +371,7 @@ __global__ __launch_bounds__(kThreads) void mesh_ep_plan_kernel(const int* __res
   __syncthreads();
   const int64_t e = e_sh;
   bool ok = true;
-  if (t < W) ok = wait_ge(flag_at(peers[me], kAck, ch, t), e - S, timeout);
+  if (t < W) ok = wait_ge(flag_at(peers[me], kAck, ch, t), e - S, timeout, st);
   if (!ok) set_word(st, kStErr, 1);
   __syncthreads();
   for (int i = t; i < W * E; i += kThreads) {
@@ -380,7 +384,7 @@ __global__ __launch_bounds__(kThreads) void mesh_ep_plan_kernel(const int* __res
   release_system();
   if (t < W) store_flag(flag_at(peers[t], kCnt, ch, shadow ? t : me), (uint64_t)e);
   ok = true;
-  if (t < W) ok = wait_ge(flag_at(peers[me], kCnt, ch, t), e, timeout);
+  if (t < W) ok = wait_ge(flag_at(peers[me], kCnt, ch, t), e, timeout, st);
   if (!ok) set_word(st, kStErr, 1);
   __syncthreads();
   acquire_system();

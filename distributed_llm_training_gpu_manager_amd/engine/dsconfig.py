@@ -92,7 +92,8 @@ def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, model_cf
         v = mi["xgmi_mesh"]
         cfg.xgmi_mesh = ("on" if v else "off") if isinstance(v, bool) else str(v)
     if "ep_capacity_factor" in mi:
-        cfg.ep_capacity_factor = float(mi["ep_capacity_factor"])
+        v = mi["ep_capacity_factor"]
+        cfg.ep_capacity_factor = None if v in (None, "dropless", "auto") else float(v)
     if mi.get("comm_dtype"):
         cfg.comm_dtype = {"fp32": torch.float32, "float32": torch.float32}.get(mi["comm_dtype"], torch.bfloat16)
     if auto_mbs:

@@ -7,7 +7,9 @@ user script is here: synthetic data, the ZeRO engine, in-proc
 loss monitoring, the NaN trap, async checkpoints, auto-resume and spot preemption.
 
 Exit codes (read by the supervisor): 0 done, 3 NaN/Inf halt, 4 preempted (emergency
-checkpoint written). Rank 0 publishes per-step progress to ``DLGM_STATUS_FILE``.
+checkpoint written), 5 transport failure (an xGMI mesh wait timed out or an EP dispatch overflowed:
+the supervisor resumes from the newest verified checkpoint). Rank 0 publishes per-step progress to
+``DLGM_STATUS_FILE``; every rank writes its heartbeat to ``DLGM_HEARTBEAT_DIR`` (hang detection).
 """
 from __future__ import annotations
 
@@ -28,7 +30,7 @@ import torch
 from ..ckpt.checkpoint import AsyncCheckpointer, export_consolidated
 from ..health.loss_monitor import json_safe, LossSpikeMonitor, MonitorConfig, TrainingMetrics
 from ..health.nan_trap import NanTrap
-from ..launcher.supervisor import EXIT_NAN_HALT, EXIT_PREEMPTED, write_status
+from ..launcher.supervisor import EXIT_NAN_HALT, EXIT_PREEMPTED, EXIT_TRANSPORT, write_heartbeat, write_status
 from ..models import get_config
 from ..parallel.comm import Comm, init_distributed
 from ..parallel.zero import EngineConfig, ZeroEngine
@@ -128,6 +130,9 @@ class Trainer:
         self.timeline: Dict[str, float] = {"process_start": _process_start(), "imported": _T_IMPORTED}
         self.env = init_distributed(args.device)
         self.timeline["dist_init"] = time.time()
+        self.mem_notes: Dict[str, float] = {}
+        if self.env.device.type == "cuda":  # HBM still held by a killed predecessor shows up here
+            self.mem_notes["gpu_free_at_start_GiB"] = round(torch.cuda.mem_get_info(self.env.device)[0] / 2 ** 30, 1)
         self.comm = Comm()
         self.shadow = int(getattr(args, "shadow_world", 0) or 0)
         if self.shadow > 1:
@@ -178,8 +183,10 @@ class Trainer:
         save_dir = args.save_dir or os.environ.get("DLGM_SAVE_DIR")
         self.engine = ZeroEngine(self.mcfg, self.ecfg, self.env.device, self.comm)
         self.timeline["engine"] = time.time()
+        if self.env.device.type == "cuda":
+            self.mem_notes["gpu_free_after_engine_GiB"] = round(torch.cuda.mem_get_info(self.env.device)[0] / 2 ** 30, 1)
         self.monitor = LossSpikeMonitor(MonitorConfig())
-        self.trap = NanTrap(self.env.device, self.monitor, width=5)
+        self.trap = NanTrap(self.env.device, self.monitor, width=6)
         shm = {"auto": "auto", "on": True, "off": False}[args.ckpt_shm]
         self.ckpt = AsyncCheckpointer(self.engine, save_dir, mode=args.ckpt_mode, keep_last=args.keep_last, shm=shm,
                                       disk=bool(args.ckpt_disk)) if save_dir else None
@@ -236,16 +243,19 @@ class Trainer:
         rank takes the same halt / preemption decision at the same loop iteration."""
         v = self.trap.get(step)
         if v is None:
-            v = [float(x) for x in torch.cat([self.engine.stats, issued["m"]["loss"].reshape(1).float(),
-                                              issued["m"]["grad_norm"].reshape(1).float()]).tolist()]
-        ss, bad, flag, loss, gnorm = v[0], v[1], v[2], v[3], v[4]
+            v = [float(x) for x in self._report_vector(issued["m"]).tolist()]
+        ss, bad, flag, loss, gnorm, transport = v[0], v[1], v[2], v[3], v[4], v[5]
         now = time.time()
         dt = now - self._t_last
         self._t_last = now
         rec = {"step": step, "loss": loss, "grad_norm": gnorm,
                "lr": issued["m"]["lr"], "step_s": dt, "tokens_per_sec": self._tokens_step / max(dt, 1e-9),
-               "nonfinite": bad, "preempt": flag > 0}
+               "nonfinite": bad, "preempt": flag > 0, "transport": int(transport)}
         self.log.append(rec)
+        self._reports += 1
+        if self._reports > 1:  # (the first report's time includes the warm-up)
+            self._last_step_s = dt
+        self._last_reported = step
         a = self.args
         if self.env.rank == 0:
             write_status(step, loss=loss, nonfinite=bad)
@@ -254,7 +264,8 @@ class Trainer:
                 t = self.timeline
                 keys = ["process_start", "imported", "dist_init", "engine", "restored", "first_step"]
                 self._say("startup: " + json.dumps({f"{b}_s": round(t[b] - t[a_], 2) for a_, b in zip(keys, keys[1:])}
-                                                    | {"total_s": round(now - t["process_start"], 2)}))
+                                                    | {"total_s": round(now - t["process_start"], 2)}
+                                                    | self.mem_notes))
             hbm = self.telemetry.aggs["hbm_used_gib"].max if self.telemetry is not None else None
             alerts = self.monitor.ingest(TrainingMetrics(step=step, loss=loss, learning_rate=rec["lr"],
                                                          gradient_norm=rec["grad_norm"],
@@ -269,10 +280,25 @@ class Trainer:
                 self._say(json.dumps(json_safe(rec)) + ("" if not alerts else f" alerts={[x.alert_type for x in alerts]}"))
         return rec
 
+    def _report_vector(self, m: Dict[str, Any]) -> torch.Tensor:
+        """[sum g^2, non-finite, flags, loss, unscaled grad norm, transport word] of the step just queued (device)."""
+        return torch.cat([self.engine.stats, m["loss"].reshape(1).float(), m["grad_norm"].reshape(1).float(),
+                          self.engine.transport_word()])
+
     def _decide(self, rec: Dict[str, Any], last_issued: int) -> Optional[int]:
         """Exit code to stop with after step rec['step'] (None: go on). `last_issued` has been queued too;
         with the NaN latch its update is skipped on the device, so a NaN halt leaves the pre-NaN state."""
         a = self.args
+        if rec.get("transport"):
+            # the mesh's sticky words (1: a device-side wait timed out, 2: an EP dispatch overflowed an explicit
+            # capacity): the step trained on data nobody can vouch for -- stop without saving it; the supervisor
+            # resumes from the newest verified checkpoint
+            self._say(f"xGMI mesh transport failure at step {rec['step']} (word {rec['transport']}); halting")
+            try:
+                self.engine.check_transport()
+            except RuntimeError as e:
+                self._say(str(e))
+            return EXIT_TRANSPORT
         if rec["nonfinite"] > 0 and a.halt_on_nan:
             self._say(f"NaN/Inf gradients at step {rec['step']} ({int(rec['nonfinite'])} elements): update skipped "
                       f"on device; halting")
@@ -309,12 +335,17 @@ class Trainer:
             self._say(f"note: {n}")
         self._tokens_step = self.ecfg.micro_batch_size * self.ecfg.seq_len * self.ecfg.grad_accum * self.env.world
         self._t_last = time.time()
+        self._reports, self._last_step_s, self._last_reported = 0, None, start
+        write_heartbeat(self.env.rank, start, phase="ready")  # restored / initialised: the first step is next
         self.engine.sync_flags = self.env.world > 1
         first_attempt = os.environ.get("DLGM_RESTART", "0") == "0"
         rc = 0
         prev: Optional[Tuple[int, Dict[str, Any]]] = None
         last = start
         for step in range(start + 1, a.steps + 1):
+            # every rank's own heartbeat, before it issues the step: a rank that stops (SIGSTOP, a hang in its own
+            # code) goes stale first, the ranks waiting for it in their next collective one step later
+            write_heartbeat(self.env.rank, self._last_reported, issuing=step, step_s=self._last_step_s)
             if a.inject_nan_step == step and first_attempt and a.inject_nan_rank in (-1, self.env.rank):
                 # one faulty rank among healthy ones (--inject-nan-rank): the non-finite count rides the all-reduced
                 # gradient statistics, so every rank skips the update and halts at the same step
@@ -325,9 +356,9 @@ class Trainer:
                 m = self.engine.train_step(self.data.batches(step))
                 for _ in range(a.profile_steps - 1 if prof else 0):  # extra traced steps reuse this step's data
                     self.engine.train_step(self.data.batches(step))
-            # [sum g^2, non-finite, flags, loss, unscaled grad norm]: the fp16 loss scale stays on the device
-            self.trap.record(step, torch.cat([self.engine.stats, m["loss"].reshape(1).float(),
-                                              m["grad_norm"].reshape(1).float()]))
+            # [sum g^2, non-finite, flags, loss, unscaled grad norm, transport]: read one step late from the pinned
+            # ring (no sync in the loop); the fp16 loss scale stays on the device
+            self.trap.record(step, self._report_vector(m))
             issued = {"m": m}
             last = step
             # step t-1's outcome, read while step t runs on the device
@@ -358,6 +389,8 @@ class Trainer:
                     if last_saved > 0:
                         self.ckpt.wait_published(last_saved)
                 os.kill(os.getpid(), signal.SIGKILL)
+            if a.stop_at_step == step and first_attempt and self.env.rank == a.stop_rank:
+                os.kill(os.getpid(), signal.SIGSTOP)  # hang drill: this rank freezes (only SIGKILL / SIGCONT move it)
             if a.preempt_at_step == step and first_attempt and a.preempt_rank in (-1, self.env.rank):
                 # a notice on one rank only (--preempt-rank): its flag rides the next step's all-reduced statistics
                 os.kill(os.getpid(), signal.SIGUSR1)
@@ -449,6 +482,9 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--kill-at-step", type=int, default=-1, help="fault drill: SIGKILL this rank after the step "
                     "(first attempt only)")
     ap.add_argument("--kill-rank", type=int, default=0, help="rank the SIGKILL drill kills")
+    ap.add_argument("--stop-at-step", type=int, default=-1, help="hang drill: SIGSTOP this rank after the step "
+                    "(first attempt only)")
+    ap.add_argument("--stop-rank", type=int, default=0, help="rank the hang drill freezes")
     ap.add_argument("--preempt-at-step", type=int, default=-1, help="spot drill: deliver SIGUSR1 after the step")
     ap.add_argument("--halt-on-nan", type=int, default=1)
     ap.add_argument("--metrics-url", default=os.environ.get("DLGM_METRICS_URL"))

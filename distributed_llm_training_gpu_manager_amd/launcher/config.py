@@ -52,6 +52,12 @@ class MI355XOptions(BaseModel):
     save_dir: Optional[str] = None
     auto_resume: bool = True
     max_restarts: int = Field(default=3, ge=0)
+    heartbeat_timeout_s: float = Field(
+        default=-1.0, description="hung-rank detection: seconds without a rank heartbeat before the job is killed and "
+        "resumed; -1 = auto (max(heartbeat_min_s, 10 x the steady step time)), 0 = off")
+    heartbeat_min_s: float = Field(default=120.0, gt=0)
+    startup_timeout_s: float = Field(default=900.0, gt=0,
+                                     description="bound for a rank's first heartbeat (start-up, restore, first step)")
     comm_dtype: Optional[str] = None
     expert_parallel_size: int = Field(default=1, ge=1)
     sequence_parallel_size: int = Field(default=1, ge=1, description="Ulysses sequence parallelism (long context)")
@@ -61,8 +67,9 @@ class MI355XOptions(BaseModel):
                              "(single rank; or every collective on the xGMI mesh)")
     xgmi_mesh: str = Field(default="off", description="on: dense ZeRO gathers / reduce-scatters and the EP token "
                            "exchange over the device-driven xGMI mesh (HIP IPC symmetric heaps); off: RCCL rings")
-    ep_capacity_factor: float = Field(default=2.0, gt=0, description="mesh EP receive capacity, x the balanced "
-                                      "share of rows (overflow rows are dropped and flagged)")
+    ep_capacity_factor: Optional[float] = Field(
+        default=None, gt=0, description="mesh EP receive capacity, x the balanced share of rows; null = dropless "
+        "(worst-case receive slot; a routing that overflows an explicit capacity stops the job)")
     auto_micro_batch: bool = Field(default=False, description="size the micro-batch (and GA, activation "
                                    "checkpointing) to the per-rank HBM plan, keeping the global batch")
 

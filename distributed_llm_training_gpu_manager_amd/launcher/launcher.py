@@ -117,9 +117,14 @@ class ZeroLauncher:
         resume = opts.auto_resume if (auto_resume is None and opts is not None) else bool(auto_resume)
         env = {"MASTER_ADDR": config.master_addr if config.master_addr != "localhost" else "127.0.0.1",
                "MASTER_PORT": str(config.master_port), "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+        # hung-rank detection is on for every launched job: every rank beats after each step, the supervisor kills
+        # and resumes the job when one goes silent past the bound (and the ranks' process-group timeout follows it)
         spec = JobSpec(job_id=job_id, argv=argv, env=env, auto_resume=resume,
                        max_restarts=opts.max_restarts if opts else 3,
-                       save_dir=(opts.save_dir if opts and opts.save_dir else None))
+                       save_dir=(opts.save_dir if opts and opts.save_dir else None),
+                       heartbeat_timeout_s=opts.heartbeat_timeout_s if opts else -1.0,
+                       heartbeat_min_s=opts.heartbeat_min_s if opts else 120.0,
+                       startup_timeout_s=opts.startup_timeout_s if opts else 900.0)
         try:
             job = self.registry.submit(spec)
             result.status = "launched"

@@ -8,8 +8,15 @@ and the README's auto-resume claim (``README.md:14``) has no implementation. Her
 * every job runs in its own process group (``start_new_session``) so the whole rank
   tree can be signalled (spot notice -> SIGUSR1, cancel -> SIGTERM/SIGKILL);
 * stdout/stderr go to ``<run_dir>/job.log`` (no pipes to fill up);
-* the training ranks publish progress to ``<run_dir>/status.json``
-  (``DLGM_STATUS_FILE``): a stale heartbeat is treated like a crash;
+* the training ranks publish progress to ``<run_dir>/status.json`` (``DLGM_STATUS_FILE``, rank 0) and EVERY
+  rank writes its own heartbeat to ``<run_dir>/heartbeat/rank{r}.json`` (``DLGM_HEARTBEAT_DIR``) after each
+  completed step. Hang detection is on by default: a rank whose heartbeat is older than
+  max(``heartbeat_min_s``, ``heartbeat_step_mult`` x the slowest rank's steady step time) -- or that never beat
+  within ``startup_timeout_s`` of the attempt's start -- marks the attempt hung (a SIGSTOPped rank, a deadlocked
+  collective: the others block in their next collective, so their beats go stale too; the stalest rank is named in
+  the event). The whole rank tree is killed and the job resumes from the newest verified checkpoint. The ranks'
+  process-group timeout (``DLGM_PG_TIMEOUT_S``) is set to the same bound, so a collective that can never complete
+  also fails inside the rank;
 * on a non-zero exit (SIGKILL'd rank, hang) the supervisor relaunches the job with
   ``--resume=auto`` (the engine rolls back to the newest checkpoint -- /dev/shm snapshot
   tier first -- that verifies on every rank) up to ``max_restarts`` times, and records
@@ -38,6 +45,7 @@ from typing import Dict, List, Optional
 
 EXIT_NAN_HALT = 3
 EXIT_PREEMPTED = 4
+EXIT_TRANSPORT = 5  # xGMI mesh wait timed out / EP capacity overflow: resumed like a crash
 
 
 @dataclass
@@ -49,7 +57,11 @@ class JobSpec:
     max_restarts: int = 3
     save_dir: Optional[str] = None
     run_dir: Optional[str] = None
-    heartbeat_timeout_s: float = 0.0  # 0 = disabled
+    # hang detection: < 0 = auto (max(heartbeat_min_s, heartbeat_step_mult x steady step time)), 0 = off, > 0 fixed
+    heartbeat_timeout_s: float = -1.0
+    heartbeat_min_s: float = 120.0
+    heartbeat_step_mult: float = 10.0
+    startup_timeout_s: float = 900.0  # no heartbeat from some rank this long after an attempt started -> hung
     resume_arg: str = "--resume=auto"
     restart_on_preempt: bool = False
     max_nan_restarts: int = 1
@@ -69,6 +81,7 @@ class Job:
         os.makedirs(self.run_dir, exist_ok=True)
         self.log_path = os.path.join(self.run_dir, "job.log")
         self.status_path = os.path.join(self.run_dir, "status.json")
+        self.heartbeat_dir = os.path.join(self.run_dir, "heartbeat")
         self.status = "pending"
         self.pid: Optional[int] = None
         self.restarts = 0
@@ -94,6 +107,23 @@ class Job:
                 return json.load(f)
         except (OSError, ValueError):
             return None
+
+    def heartbeats(self) -> Dict[int, Dict]:
+        """rank -> its last heartbeat record (every attempt's; callers filter on ``restart``)."""
+        out: Dict[int, Dict] = {}
+        try:
+            names = os.listdir(self.heartbeat_dir)
+        except OSError:
+            return out
+        for n in names:
+            if n.startswith("rank") and n.endswith(".json"):
+                try:
+                    with open(os.path.join(self.heartbeat_dir, n)) as f:
+                        rec = json.load(f)
+                    out[int(n[4:-5])] = rec
+                except (OSError, ValueError):
+                    continue
+        return out
 
     def to_dict(self) -> Dict:
         return {
@@ -154,6 +184,54 @@ class Supervisor(threading.Thread):
                 return w
         return 0
 
+    def heartbeat_timeout(self, beats: Dict[int, Dict]) -> float:
+        """Seconds without a heartbeat after which a rank is hung (0: detection off)."""
+        spec = self.job.spec
+        if spec.heartbeat_timeout_s >= 0:
+            return spec.heartbeat_timeout_s
+        step_s = max([float(b.get("step_s") or 0.0) for b in beats.values()] or [0.0])
+        return max(spec.heartbeat_min_s, spec.heartbeat_step_mult * step_s)
+
+    def hung_rank(self, attempt_t0: float, expected: Optional[int], now: Optional[float] = None) -> Optional[Dict]:
+        """The stalest rank of the current attempt if it is past its bound, else None."""
+        job, spec = self.job, self.job.spec
+        now = time.time() if now is None else now
+        beats = {r: b for r, b in job.heartbeats().items() if b.get("restart", 0) == job.restarts
+                 and b.get("time", 0) >= attempt_t0}
+        prog = job.progress()
+        if not beats and prog is not None and prog.get("restart", 0) == job.restarts and \
+                prog.get("time", 0) >= attempt_t0:
+            beats = {0: prog}  # a rank-0-only status writer (older training scripts)
+        timeout = self.heartbeat_timeout(beats)
+        if timeout <= 0:
+            return None
+        ranks = range(expected) if expected else sorted(beats)
+        worst = None
+        for r in ranks:
+            b = beats.get(r)
+            if b is None:  # never beat in this attempt: the startup bound (at least the steady-state one)
+                age, bound = now - attempt_t0, max(spec.startup_timeout_s, timeout)
+            elif not b.get("step_s") and spec.heartbeat_timeout_s < 0:
+                # ready, no step finished yet (restore, warm-up, the first step): no step time to scale by
+                age, bound = now - float(b.get("time", attempt_t0)), max(spec.startup_timeout_s, timeout)
+            else:
+                age, bound = now - float(b.get("time", attempt_t0)), timeout
+            if age > bound and (worst is None or age > worst["age_s"]):
+                worst = {"rank": r, "age_s": round(age, 2), "bound_s": round(bound, 2),
+                         "last_step": None if b is None else b.get("step")}
+        if worst is None and not expected and not beats and spec.heartbeat_timeout_s > 0 \
+                and now - attempt_t0 > max(spec.startup_timeout_s, timeout):
+            worst = {"rank": None, "age_s": round(now - attempt_t0, 2), "bound_s": spec.startup_timeout_s,
+                     "last_step": None}
+        return worst
+
+    def expected_ranks(self) -> Optional[int]:
+        argv = self.job.spec.argv
+        n = self.nproc_of(argv)
+        if self.job.world_history:
+            n = self.job.world_history[-1]
+        return n
+
     def _start(self, resume: bool) -> subprocess.Popen:
         spec = self.job.spec
         argv = list(spec.argv)
@@ -164,7 +242,14 @@ class Supervisor(threading.Thread):
         if self.job.lr_scale != 1.0:
             argv += ["--lr-scale", str(self.job.lr_scale)]
         env = {**os.environ, **spec.env, "DLGM_STATUS_FILE": self.job.status_path, "DLGM_JOB_ID": spec.job_id,
-               "DLGM_RESTART": str(self.job.restarts)}
+               "DLGM_RESTART": str(self.job.restarts), "DLGM_HEARTBEAT_DIR": self.job.heartbeat_dir}
+        if spec.heartbeat_timeout_s != 0:
+            # a collective that can never complete fails inside the ranks on the same bound (the auto bound before
+            # any step time is known: the startup one)
+            pg = spec.heartbeat_timeout_s if spec.heartbeat_timeout_s > 0 else max(spec.heartbeat_min_s,
+                                                                                  spec.startup_timeout_s)
+            env.setdefault("DLGM_PG_TIMEOUT_S", str(int(max(30.0, pg))))
+        os.makedirs(self.job.heartbeat_dir, exist_ok=True)
         if spec.save_dir:
             env["DLGM_SAVE_DIR"] = spec.save_dir
         log = open(self.job.log_path, "ab", buffering=0)
@@ -211,11 +296,9 @@ class Supervisor(threading.Thread):
                 job.event("recovered", mttr_s=job.mttr_s[-1], step=prog.get("step"))
                 failure_t = None
             # heartbeat: only records of the current attempt count, measured from the attempt start
-            last_beat = max(attempt_t0, prog.get("time", 0)) if prog and prog.get("restart", 0) == job.restarts \
-                else attempt_t0
-            if rc is None and spec.heartbeat_timeout_s > 0 and prog is not None and \
-                    time.time() - last_beat > spec.heartbeat_timeout_s:
-                job.event("heartbeat_lost", last=prog.get("time"))
+            hung = self.hung_rank(attempt_t0, self.expected_ranks()) if rc is None else None
+            if hung is not None:
+                job.event("heartbeat_lost", **hung)
                 self._kill_group(proc, grace_s=2.0)
                 rc = proc.poll() if proc.poll() is not None else -9
             if job._cancel.is_set():
@@ -322,16 +405,31 @@ def default_registry() -> JobRegistry:
     return _DEFAULT
 
 
+def _write_json(path: str, rec: Dict) -> None:
+    tmp = f"{path}.{os.getpid()}.tmp"
+    with open(tmp, "w") as f:
+        json.dump(rec, f)
+    os.replace(tmp, path)
+
+
 def write_status(step: int, **kw) -> None:
     """Called by training rank 0 after each completed step (atomic replace)."""
     path = os.environ.get("DLGM_STATUS_FILE")
     if not path:
         return
-    rec = {"step": step, "time": time.time(), "restart": int(os.environ.get("DLGM_RESTART", "0")), **kw}
-    tmp = path + ".tmp"
-    with open(tmp, "w") as f:
-        json.dump(rec, f)
-    os.replace(tmp, path)
+    _write_json(path, {"step": step, "time": time.time(), "restart": int(os.environ.get("DLGM_RESTART", "0")), **kw})
+
+
+def write_heartbeat(rank: int, step: int, **kw) -> None:
+    """Called by EVERY training rank after each completed step (and once when it is ready to train): the
+    supervisor's hang detection reads one file per rank (``DLGM_HEARTBEAT_DIR``)."""
+    d = os.environ.get("DLGM_HEARTBEAT_DIR")
+    if not d:
+        return
+    os.makedirs(d, exist_ok=True)
+    _write_json(os.path.join(d, f"rank{int(rank)}.json"),
+                {"rank": int(rank), "step": step, "time": time.time(), "pid": os.getpid(),
+                 "restart": int(os.environ.get("DLGM_RESTART", "0")), **kw})
 
 
 def main(argv: Optional[List[str]] = None) -> int:
@@ -354,7 +452,10 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--job-id", default=f"job_{int(time.time())}")
     ap.add_argument("--run-dir", default=None)
     ap.add_argument("--save-dir", default=None)
-    ap.add_argument("--heartbeat-timeout", type=float, default=0.0)
+    ap.add_argument("--heartbeat-timeout", type=float, default=-1.0,
+                    help="seconds without a rank heartbeat before the job is killed and resumed (-1: auto, 0: off)")
+    ap.add_argument("--heartbeat-min", type=float, default=120.0)
+    ap.add_argument("--startup-timeout", type=float, default=900.0)
     ap.add_argument("--restart-on-preempt", action="store_true")
     ap.add_argument("--no-auto-resume", action="store_true")
     ap.add_argument("--max-nan-restarts", type=int, default=1)
@@ -367,6 +468,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     cmd = argv[cut + 1:]
     spec = JobSpec(job_id=a.job_id, argv=cmd, auto_resume=not a.no_auto_resume, max_restarts=a.max_restarts,
                    save_dir=a.save_dir, run_dir=a.run_dir, heartbeat_timeout_s=a.heartbeat_timeout,
+                   heartbeat_min_s=a.heartbeat_min, startup_timeout_s=a.startup_timeout,
                    restart_on_preempt=a.restart_on_preempt, max_nan_restarts=a.max_nan_restarts,
                    elastic=a.elastic, min_world=a.min_world, max_world=a.max_world, global_batch=a.global_batch,
                    micro_batch=a.micro_batch)

@@ -59,8 +59,11 @@ class DistEnv:
     device: torch.device = torch.device("cpu")
 
 
-def init_distributed(device_type: str = "auto", timeout_s: int = 1800) -> DistEnv:
-    """Initialise the default process group from torchrun-style env vars (idempotent)."""
+def init_distributed(device_type: str = "auto", timeout_s: Optional[int] = None) -> DistEnv:
+    """Initialise the default process group from torchrun-style env vars (idempotent). The collective timeout is
+    ``DLGM_PG_TIMEOUT_S`` when set (the supervisor sets it to its hang bound), else 1800 s (torch's default)."""
+    if timeout_s is None:
+        timeout_s = int(float(os.environ.get("DLGM_PG_TIMEOUT_S", "1800")))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

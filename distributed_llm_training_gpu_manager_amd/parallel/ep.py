@@ -19,10 +19,15 @@ device (``_regroup_index``), never as a host list.
 :class:`MeshExpertDispatcher` is the MI355X-native transport (parallel/xgmi_mesh.py): the routing counts travel
 through the ranks' symmetric heaps, every destination offset is computed on the device, each rank writes its rows
 straight into the expert owners' receive buffers over xGMI in local-expert-major order (no regroup copy), and the
-combine is the mirror image -- no host read at all, so the EP micro-batch loop can be captured in a HIP graph. The
-receive buffer has a static capacity (``capacity_factor`` x the balanced share); rows past it are dropped, their
-expert output is zero, and a sticky overflow word is raised on every rank (:meth:`MeshExpertDispatcher.overflowed`).
-The RCCL dispatcher above stays the default and the fallback (``EngineConfig.xgmi_mesh``).
+combine is the mirror image. The exchange is DROPLESS by default: every rank's receive slot holds the worst case
+(all W x T x k rows of the EP group), so no routing can overflow it (Mixtral-8x7B EP = 8, seq 4096, top-2: 512 MiB
+per slot of a 288 GB MI355X). The rows handed to the expert GEMMs are either a static worst-case tensor (no host read
+at all: the EP micro-batch loop can be captured in a HIP graph; chosen when those activations fit the HBM plan) or,
+``sized_output``, exactly the received rows (one host read of the received count per dispatch, like the RCCL path's
+split exchange). An explicit ``capacity_factor`` gives the old static capacity (capturable with less memory); a
+routing that overflows it raises at the next step boundary (:meth:`MeshExpertDispatcher.overflowed`, read by
+``ZeroEngine.check_transport``) instead of training on dropped tokens. The RCCL dispatcher above stays the default
+transport and the fallback (``EngineConfig.xgmi_mesh``).
 """
 from __future__ import annotations
 
@@ -70,6 +75,7 @@ class DispatchCtx:
     local_offsets: Optional[torch.Tensor] = None  # int32 [El + 1] on the device: expert row ranges
     nrows: Optional[torch.Tensor] = None  # int32 [1] on the device: valid rows of a capacity-sized dispatch output
     plan: Optional[torch.Tensor] = None  # mesh transfer tables (MeshExpertDispatcher)
+    out_rows: int = 0  # rows of the mesh dispatch output (>= the valid rows)
 
     def counts(self) -> List[int]:
         """Host per-local-expert row counts (a device sync at EP = 1; the per-expert fallback path only)."""
@@ -153,21 +159,28 @@ class MeshExpertDispatcher:
 
     dispatch:   mesh_ep_plan (epoch open + count exchange + tables, one workgroup) -> mesh_push_rows (this rank's
                 expert-sorted rows into every owner's slot at device-computed rows) -> wait -> copy-out of the
-                [capacity, D] local-expert-major rows (ACKs the slot)
-    combine:    epoch open -> push each (local expert, source) block back to the source's expert-sorted rows (zeros
-                for rows dropped by the capacity) -> wait -> copy-out of the [tokens x k, D] rows
+                local-expert-major rows (ACKs the slot)
+    combine:    epoch open -> push each (local expert, source) block back to the source's expert-sorted rows -> wait
+                -> copy-out of the [tokens x k, D] rows
     redispatch: the dispatch pattern again with the forward's tables (backward: d outputs)
-    The dispatch output has `capacity` rows; ``ctx.local_offsets`` / ``ctx.nrows`` say which are valid.
+
+    capacity_factor None (dropless): the receive slot holds W x rows, so the device tables never clamp a row.
+    The dispatch output then has ``C`` rows (static: capturable) or, with ``sized_output``, the received count
+    rounded up to 64 (one host read per dispatch). ``ctx.local_offsets`` / ``ctx.nrows`` say which rows are valid;
+    every consumer (grouped GEMMs, SwiGLU, the combine push) reads only those.
     """
 
     def __init__(self, ep_comm: Comm, n_experts: int, device: torch.device, rows: int, d_model: int,
-                 dtype: torch.dtype, capacity_factor: float = 2.0, slots: int = 2, timeout_s: float = 60.0):
+                 dtype: torch.dtype, capacity_factor: Optional[float] = None, slots: int = 2, timeout_s: float = 60.0,
+                 sized_output: bool = False):
         from .._native import hip_ops
         from .xgmi_mesh import CH_COMBINE, CH_DISPATCH, XgmiMesh, capacity_rows, ep_region_bytes
         self.W, self.rank, self.E = ep_comm.world, ep_comm.rank, n_experts
         assert n_experts % self.W == 0, "n_experts must be divisible by the EP size"
         self.El = n_experts // self.W
         self.rows, self.D, self.dtype = int(rows), int(d_model), dtype
+        self.dropless = capacity_factor is None
+        self.sized = bool(sized_output) and self.dropless
         esz = torch.tensor([], dtype=dtype).element_size()
         self.C = capacity_rows(self.rows, self.W, capacity_factor)
         self.hdr, disp = ep_region_bytes(self.W, n_experts, self.C, d_model * esz)
@@ -176,6 +189,7 @@ class MeshExpertDispatcher:
         self.L = list(hip_ops().mesh_plan_layout(self.W, n_experts))
         self._A, self._B = self.mesh.regions["ep_dispatch"], self.mesh.regions["ep_combine"]
         self._cd, self._cc = CH_DISPATCH, CH_COMBINE
+        self.max_rows_seen = 0  # sized_output: the largest received count so far (host-side record)
 
     def _push(self, x: torch.Tensor, plan: torch.Tensor, combine: bool) -> None:
         from .._native import hip_ops
@@ -206,10 +220,15 @@ class MeshExpertDispatcher:
         self._push(x_sorted, plan, False)
         m.wait_data(self._cd)
         nrows = plan[self.L[0]:self.L[0] + 1]
-        out = x_sorted.new_empty((self.C, self.D))
+        out_rows = self.C
+        if self.sized:  # the received count on the host (the plan kernel has it after the count exchange)
+            n = int(nrows)
+            self.max_rows_seen = max(self.max_rows_seen, n)
+            out_rows = max(64, (n + 63) // 64 * 64)
+        out = x_sorted.new_empty((out_rows, self.D))
         self._copy(out, nrows, False)
         lo = self.L[3]
-        ctx = DispatchCtx([], [], None, None, plan[lo:lo + self.El + 1], nrows=nrows, plan=plan)
+        ctx = DispatchCtx([], [], None, None, plan[lo:lo + self.El + 1], nrows=nrows, plan=plan, out_rows=out_rows)
         return out, ctx
 
     def redispatch(self, rows_sorted: torch.Tensor, ctx: DispatchCtx) -> torch.Tensor:
@@ -217,12 +236,12 @@ class MeshExpertDispatcher:
         self.mesh.begin(self._cd, self._A.slots)
         self._push(rows_sorted, ctx.plan, False)
         self.mesh.wait_data(self._cd)
-        out = rows_sorted.new_empty((self.C, self.D))
+        out = rows_sorted.new_empty((ctx.out_rows, self.D))
         self._copy(out, ctx.nrows, False)
         return out
 
     def combine(self, y_local: torch.Tensor, ctx: DispatchCtx) -> torch.Tensor:
-        assert y_local.shape == (self.C, self.D)
+        assert y_local.shape == (ctx.out_rows, self.D)
         self.mesh.begin(self._cc, self._B.slots)
         self._push(y_local, ctx.plan, True)
         self.mesh.wait_data(self._cc)
@@ -231,8 +250,20 @@ class MeshExpertDispatcher:
         return out
 
     def overflowed(self) -> bool:
-        """Did any dispatch so far overflow a receive capacity (host read: call at a step boundary)?"""
+        """Did any dispatch so far overflow the receive capacity (host read: call at a step boundary)? Never in the
+        dropless mode (an assertion); in the capacity mode the engine raises on it."""
         return self.mesh.overflowed()
 
     def close(self) -> None:
         self.mesh.close()
+
+
+def static_dispatch_fits(rows_worst: int, d_model: int, ffn_dim: int, n_layers: int, activation_checkpointing: bool,
+                         hbm_bytes: float, fraction: float = 0.10, esz: int = 2) -> bool:
+    """Dropless mesh EP: can every MoE layer keep worst-case-sized expert activations (x, gate/up, SwiGLU output, y:
+    D + 3F + D per row) within `fraction` of HBM? Then the dispatch output is a static tensor and the EP loop stays
+    capturable; otherwise it is sized per dispatch by one host read."""
+    per_layer = rows_worst * (2 * d_model + 3 * ffn_dim) * esz
+    live_layers = 1 if activation_checkpointing else n_layers
+    # backward temporaries of one layer (dA, dGU, dX) on top of the saved ones
+    return per_layer * live_layers + rows_worst * (3 * ffn_dim + d_model) * esz <= fraction * hbm_bytes

@@ -273,9 +273,11 @@ def ep_region_bytes(world: int, n_experts: int, rows: int, row_bytes: int) -> Tu
     return hdr, hdr + rows * row_bytes
 
 
-def capacity_rows(tokens_k: int, world: int, factor: float) -> int:
-    """Static receive capacity of an EP rank: factor x the balanced share (each rank receives tokens_k rows on
-    average under balanced routing), at most every row of every source (W x tokens_k), 64-row aligned."""
-    c = int(math.ceil(factor * tokens_k))
-    c = min(c, world * tokens_k)
+def capacity_rows(tokens_k: int, world: int, factor: Optional[float]) -> int:
+    """Receive rows of an EP rank. factor None = dropless: the worst case, every row of every source (W x
+    tokens_k) -- on a 288 GB MI355X the slot costs little (Mixtral EP = 8, seq 4096, top-2: 65,536 rows x 8 KiB =
+    512 MiB). A factor gives a static capacity of factor x the balanced share (each rank receives tokens_k rows on
+    average under balanced routing), at most the worst case. 64-row aligned."""
+    worst = world * tokens_k
+    c = worst if factor is None else min(int(math.ceil(factor * tokens_k)), worst)
     return max(64, (c + 63) // 64 * 64)

@@ -123,7 +123,12 @@ class EngineConfig:
     xgmi_mesh: str = "off"
     mesh_min_bytes: int = 0  # dense collectives below this many bytes stay on RCCL
     mesh_timeout_s: float = 120.0  # a device-side wait past this records an error (XgmiMesh.check) and returns
-    ep_capacity_factor: float = 2.0  # mesh EP receive capacity: this many times the balanced share of rows
+    # mesh EP receive capacity: None = dropless (every rank's receive slot holds the worst case, W x T x k rows; the
+    # expert activations are static worst-case tensors when they fit ep_static_hbm_fraction of HBM -- capturable --
+    # else sized per dispatch by one host read); a number = a static capacity of that many times the balanced share,
+    # and a routing that overflows it raises at the step boundary (check_transport)
+    ep_capacity_factor: Optional[float] = None
+    ep_static_hbm_fraction: float = 0.10
     # expert weight gradients: keep each micro-batch's (dY, X) per expert and run one dW GEMM per expert over
     # the concatenated micro-batches at the last one (K = GA x tokens: the fp32 gradient is read and written
     # once per step instead of once per micro-batch). Only with direct fp32 gradient targets; "auto" = on
@@ -138,8 +143,9 @@ class EngineConfig:
     # ZeRO-3 on the device (no offload, no mesh): the AdamW of step s runs on a side stream as one launch per
     # parameter group in forward order, and step s+1's forward waits for each group's update where it fetches
     # the group instead of for the whole update -- the bandwidth-bound optimizer overlaps the first layers'
-    # compute (element for element the same arithmetic as the single flat launch)
-    optimizer_overlap: bool = True
+    # compute (element for element the same arithmetic as the single flat launch). Off by default: the round-4
+    # closing A/B measured it neutral for Llama-3-8B and Mixtral (profiles/optimizer_overlap_onoff_closing_r04.txt)
+    optimizer_overlap: bool = False
     nvme_path: Optional[str] = None
     param_nvme_path: Optional[str] = None  # offload_param.nvme_path (defaults to nvme_path)
     # ZeRO-2/3 gradients: True = accumulate fp32 locally and reduce-scatter once per optimizer step;
@@ -329,6 +335,9 @@ class ZeroEngine:
                  ep_comm: Optional[Comm] = None):
         self._opt_pending: Dict[int, Any] = {}  # group -> event of its overlapped update (cfg.optimizer_overlap)
         self._opt_stream = None
+        # the stream the engine computes on (captured at construction): join_optimizer orders IT after the overlapped
+        # updates, whatever stream happens to be current where the join is called from
+        self._compute_stream = torch.cuda.current_stream(device) if device.type == "cuda" else None
         self._opt_delay_cycles = 0  # test hook: spin the optimizer stream first (a missing wait then reads stale state)
         self.mcfg, self.cfg, self.device = model_cfg, cfg, device
         self.comm = comm or Comm()
@@ -397,6 +406,7 @@ class ZeroEngine:
         self.gfull_total = goff
         self.mesh = None
         self.ep_mesh = None
+        self._transport_word = None
         self._init_mesh(model_cfg)
         # compute dtype: bf16, or fp16 for the DeepSpeed "fp16" block -- every HIP kernel has an f16
         # instantiation (f16 MFMA in attention) and the dynamic loss scaler guards the fp16 range
@@ -490,9 +500,17 @@ class ZeroEngine:
         if self.ep_size > 1 and self.ep_comm is not None and self.ep_comm.world > 1:
             from .ep import MeshExpertDispatcher
             dt = torch.float16 if c.fp16 else torch.bfloat16
-            self.ep_mesh = MeshExpertDispatcher(self.ep_comm, model_cfg.n_experts, self.device,
-                                                c.tokens_per_micro * model_cfg.top_k, model_cfg.d_model, dt,
-                                                c.ep_capacity_factor, timeout_s=c.mesh_timeout_s)
+            from .ep import static_dispatch_fits
+            rows = c.tokens_per_micro * model_cfg.top_k
+            sized = False
+            if c.ep_capacity_factor is None:
+                hbm = torch.cuda.get_device_properties(self.device).total_memory
+                sized = not static_dispatch_fits(rows * self.ep_comm.world, model_cfg.d_model, model_cfg.ffn_dim,
+                                                 model_cfg.n_layers, c.activation_checkpointing, hbm,
+                                                 c.ep_static_hbm_fraction)
+            self.ep_mesh = MeshExpertDispatcher(self.ep_comm, model_cfg.n_experts, self.device, rows,
+                                                model_cfg.d_model, dt, c.ep_capacity_factor,
+                                                timeout_s=c.mesh_timeout_s, sized_output=sized)
 
     def is_cuda_dev(self) -> bool:
         return self.device.type == "cuda"
@@ -506,15 +524,34 @@ class ZeroEngine:
                 and t.numel() * t.element_size() >= self.cfg.mesh_min_bytes)
 
     def check_transport(self) -> None:
-        """Raise if a mesh wait timed out; warn once if an EP dispatch overflowed its capacity (host reads)."""
+        """Raise if a mesh wait timed out or an EP dispatch overflowed its receive capacity (host reads of two device
+        words: the trainer calls this at every step boundary where it already syncs, and train_step after the
+        optimizer when ``check_transport_every`` says so). A timed-out wait makes every later mesh kernel return at
+        once (the sticky error word), so the step that raised trained on nothing it could not trust: the caller
+        halts the job and the supervisor resumes from the last verified checkpoint."""
         for m in (self.mesh, self.ep_mesh.mesh if self.ep_mesh is not None else None):
             if m is not None:
                 m.check()
-        if self.ep_mesh is not None and self.ep_mesh.overflowed() and not getattr(self, "_ovf_warned", False):
-            import warnings
-            self._ovf_warned = True
-            warnings.warn(f"mesh EP dispatch overflowed its receive capacity ({self.ep_mesh.C} rows, "
-                          f"ep_capacity_factor {self.cfg.ep_capacity_factor}): dropped rows got zero expert output")
+        if self.ep_mesh is not None and self.ep_mesh.overflowed():
+            what = ("internal error: the dropless receive slot overflowed" if self.ep_mesh.dropless else
+                    f"a routing overflowed the mesh EP receive capacity ({self.ep_mesh.C} rows, ep_capacity_factor "
+                    f"{self.cfg.ep_capacity_factor}); set ep_capacity_factor to None (dropless)")
+            raise RuntimeError(f"xGMI mesh: {what}")
+
+    def transport_word(self) -> torch.Tensor:
+        """fp32 [1] on the device: 1 if a mesh wait timed out, + 2 if an EP dispatch overflowed its receive
+        capacity; 0 without a mesh. The trainer reads it one step late with the NaN-trap report (no sync)."""
+        if self._transport_word is None:
+            self._transport_word = torch.zeros(1, dtype=torch.float32, device=self.device)
+        meshes = [m for m in (self.mesh, self.ep_mesh.mesh if self.ep_mesh is not None else None) if m is not None]
+        if not meshes:
+            return self._transport_word
+        from .xgmi_mesh import ST_ERR, ST_OVF
+        w = self._transport_word
+        w.zero_()
+        for m in meshes:
+            w += (m.state[ST_ERR] != 0).float() + 2.0 * (m.state[ST_OVF] != 0).float()
+        return w.clamp_(max=3.0)
 
     def _split_persistent(self, groups, stages):
         """stage3_param_persistence_threshold: move each unit's small tensors (norm weights, biases) into a
@@ -1251,10 +1288,14 @@ class ZeroEngine:
             torch.cuda.current_stream(self.device).wait_event(ev)
 
     def join_optimizer(self) -> None:
-        """The current stream waits for the overlapped optimizer updates still pending: anything that reads or
-        writes master / moments / gradients / the compute copy outside the forward's fetches calls this."""
+        """The engine's compute stream AND the current stream wait for the overlapped optimizer updates still
+        pending: anything that reads or writes master / moments / gradients / the compute copy outside the forward's
+        fetches calls this (a state read under a side-stream context must not leave the compute stream unordered)."""
         if self._opt_pending:
-            torch.cuda.current_stream(self.device).wait_stream(self._opt_stream)
+            cur = torch.cuda.current_stream(self.device)
+            cur.wait_stream(self._opt_stream)
+            if self._compute_stream is not None and self._compute_stream != cur:
+                self._compute_stream.wait_stream(self._opt_stream)
             self._opt_pending.clear()
 
     def _offload_step(self, lr: float, inv_scale: float) -> None:
@@ -1306,7 +1347,7 @@ class ZeroEngine:
         per-phase timers (host-side event bookkeeping). The fp16 loss scale is a device word
         (LossScaler.state), so the fp16 path replays the same graph at every scale."""
         c = self.cfg
-        moe_ok = not self.has_experts or self.ep_size == 1 or self.ep_mesh is not None
+        moe_ok = not self.has_experts or self.ep_size == 1 or (self.ep_mesh is not None and not self.ep_mesh.sized)
         return (c.hip_graphs and self.is_cuda and (self.W == 1 or self._loop_on_mesh()) and moe_ok
                 and self.offload is None
                 and not self.param_host

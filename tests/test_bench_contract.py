@@ -74,16 +74,22 @@ def test_bench_torchrun_two_ranks():
 
 def test_bench_mesh_sweep_child_keeps_one_result_line():
     """--mesh-sweep on: after the result line each rank starts tools/mesh_sweep.py as a child process (a fresh
-    process group on an agreed port); its report goes to stderr, stdout still holds exactly one JSON line."""
+    process group on an agreed port) that first checks the transports (utils/meshcheck.py; without a GPU: the gloo
+    ranks' ZeRO-3 parity against one process) and prints one [mesh-check] line; its reports go to stderr, stdout
+    still holds exactly one JSON line."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", *TINY[:-2], "--comm-sweep", "off",
            "--mesh-sweep", "on"]
     res = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
     assert res.returncode == 0, res.stderr[-3000:]
     assert len([ln for ln in res.stdout.splitlines() if ln.startswith("{")]) == 1, res.stdout
-    sweep = [ln for ln in res.stderr.splitlines() if ln.startswith("[mesh-sweep] ")]
-    assert len(sweep) == 1, res.stderr[-3000:]
-    assert json.loads(sweep[0][len("[mesh-sweep] "):])["world"] == 2
+    chk = [ln for ln in res.stderr.splitlines() if ln.startswith("[mesh-check] ")]
+    assert len(chk) == 1, res.stderr[-3000:]
+    rec = json.loads(chk[0][len("[mesh-check] "):])
+    assert rec["world"] == 2 and rec["pass"], rec
+    assert rec["zero3_parity"]["rccl_vs_world1"]["pass"] and "skipped" in rec["mesh_ops"]
+    # the bandwidth rows need the GPU (the mesh is device memory): none on CPU
+    assert not [ln for ln in res.stderr.splitlines() if ln.startswith("[mesh-sweep] ")]
 
 
 TINY = ["--steps", "2", "--warmup", "1", "--model", "llama-tiny", "--seq", "64", "--ga", "2", "--comm-sweep", "off"]

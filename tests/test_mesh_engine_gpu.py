@@ -101,7 +101,7 @@ def test_mesh_engine_matches_single_process(tmp_path, world, stage, live, ga):
 def _moe_worker(rank, world, port, mode, out_path):
     dev = _init(rank, world, port)
     mc = get_config("mixtral-tiny")
-    kw = dict(expert_parallel_size=world, ep_capacity_factor=float(world))
+    kw = dict(expert_parallel_size=world)  # dropless (worst-case receive slot; static: capturable at this size)
     if mode == "graph":
         kw.update(xgmi_mesh="on", hip_graphs=True)
     elif mode == "mesh":
@@ -118,6 +118,7 @@ def _moe_worker(rank, world, port, mode, out_path):
            "capturable": eng.graph_capturable(), "master": eng.master.detach().cpu().clone()}
     if eng.ep_mesh is not None:
         rec["overflow"] = eng.ep_mesh.overflowed()
+        rec["dropless_static"] = eng.ep_mesh.dropless and not eng.ep_mesh.sized
     for m_ in (eng.mesh, eng.ep_mesh):
         if m_ is not None:
             m_.close()
@@ -136,7 +137,7 @@ def test_mixtral_ep4_micro_batch_loop_captures_on_the_mesh(tmp_path):
     for r in range(world):
         g, m, c = res["graph"][r], res["mesh"][r], res["rccl"][r]
         assert g["capturable"] and g["graph"] and g["state"] == "warm", (r, g["state"])
-        assert not g["overflow"] and not m["overflow"]
+        assert not g["overflow"] and not m["overflow"] and g["dropless_static"] and m["dropless_static"]
         # graph replay == the same mesh loop run eagerly, bit for bit
         assert g["losses"] == m["losses"], (r, g["losses"], m["losses"])
         assert torch.equal(g["master"], m["master"]), r

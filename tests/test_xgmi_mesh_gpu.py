@@ -7,9 +7,11 @@ the wire differs. Checks, all bit-exact:
 * all-gather (pull): == concatenation of every rank's shard, over several versions (quiesce / publish ordering);
 * reduce-scatter (push + fp32 reduce): == the fp32 rank-order sum of the bf16-rounded chunks, times the scale,
   (+ the previous value when accumulating), from fp32 and from bf16 inputs, several epochs through 2 slots;
-* EP dispatch / redispatch / combine: == the RCCL-path dispatcher (ExpertDispatcher over the same ranks), with an
-  expert that receives no rows, and with a receive capacity too small (dropped rows come back as zeros, the overflow
-  word is raised on every rank);
+* EP dispatch / redispatch / combine: == the RCCL-path dispatcher (ExpertDispatcher over the same ranks) for EVERY
+  row, with an expert that receives no rows and with a skewed routing that sends nearly every row to one owner
+  (dropless: the receive slot holds the worst case), both with a static worst-case output and with the output sized
+  by one host read; an explicit capacity that is too small raises the overflow word (an assertion: the engine stops
+  the job) and its rows past the capacity come back as zeros;
 * the MoE EP micro-batch path replays from a captured HIP graph.
 """
 import os
@@ -121,15 +123,20 @@ def _routing(rank, T, K, E, seed, skew):
     return topi
 
 
-def _ep_worker(rank, world, port, E, T, K, D, factor, skew, out_path):
+def _ep_worker(rank, world, port, E, T, K, D, factor, skew, sized, out_path):
     dev = _init(rank, world, port)
     from distributed_llm_training_gpu_manager_amd.ops.moe import moe_permute
     from distributed_llm_training_gpu_manager_amd.parallel.comm import Comm
     from distributed_llm_training_gpu_manager_amd.parallel.ep import ExpertDispatcher, MeshExpertDispatcher
     comm = Comm()
     ref = ExpertDispatcher(comm, E)
-    mesh = MeshExpertDispatcher(comm, E, dev, T * K, D, torch.bfloat16, capacity_factor=factor, timeout_s=20)
+    mesh = MeshExpertDispatcher(comm, E, dev, T * K, D, torch.bfloat16, capacity_factor=factor, timeout_s=20,
+                                sized_output=sized)
     C = mesh.C
+    if factor is None and C < world * T * K:
+        ok_geom = False
+    else:
+        ok_geom = True
     ok, msgs = True, []
     for it in range(3):
         topi = _routing(rank, T, K, E, 100 * it, skew).to(dev)
@@ -140,6 +147,12 @@ def _ep_worker(rank, world, port, E, T, K, D, factor, skew, out_path):
         xm, cm = mesh.dispatch(x, counts, offsets)
         total = xr.shape[0]
         keep = min(total, C)
+        if factor is None and (keep != total or xm.shape[0] < total):  # dropless: every row arrives
+            ok = False
+            msgs.append(f"dropless dispatch lost rows: total {total} C {C} out rows {xm.shape[0]}")
+        if sized and xm.shape[0] != max(64, (total + 63) // 64 * 64):
+            ok = False
+            msgs.append(f"sized output {xm.shape[0]} rows for {total}")
         if int(cm.nrows) != keep or not torch.equal(xm[:keep].cpu(), xr[:keep].cpu()):
             ok = False
             msgs.append(f"dispatch it{it} total {total} C {C} nrows {int(cm.nrows)}")
@@ -166,17 +179,50 @@ def _ep_worker(rank, world, port, E, T, K, D, factor, skew, out_path):
     torch.cuda.synchronize()
     mesh.mesh.check()
     ovf = mesh.overflowed()
-    if ovf != bool(skew):
+    want_ovf = bool(skew) and factor is not None
+    if ovf != want_ovf or not ok_geom:
         ok = False
-        msgs.append(f"overflow flag {ovf} (skew {skew})")
+        msgs.append(f"overflow flag {ovf} (skew {skew}, factor {factor}, C {C})")
     mesh.close()
     _finish(rank, ok, out_path, {"msgs": msgs} if rank == 0 else None)
 
 
-@pytest.mark.parametrize("world,E,factor,skew", [(2, 4, 4.0, False), (4, 8, 4.0, False), (4, 4, 4.0, False),
-                                                 (4, 8, 0.5, True)])
-def test_mesh_expert_dispatch_matches_rccl_dispatcher(tmp_path, world, E, factor, skew):
+@pytest.mark.parametrize("world,E,factor,skew,sized", [
+    (2, 4, None, False, False), (4, 8, None, False, False), (4, 4, None, False, True),
+    (4, 8, None, True, False), (4, 8, None, True, True),  # skewed routing, dropless: every row, bit-exact
+    (4, 8, 0.5, True, False)])  # explicit capacity: the overflow word is raised (the engine raises on it)
+def test_mesh_expert_dispatch_matches_rccl_dispatcher(tmp_path, world, E, factor, skew, sized):
     out = str(tmp_path / "ep.pt")
-    mp.spawn(_ep_worker, args=(world, _free_port(), E, 96, 2, 128, factor, skew, out), nprocs=world, join=True)
+    mp.spawn(_ep_worker, args=(world, _free_port(), E, 96, 2, 128, factor, skew, sized, out), nprocs=world,
+             join=True)
     res = torch.load(out, weights_only=True)
     assert res["ok"] == 1, res.get("msgs")
+
+
+def _check_worker(rank, world, port, out_path):
+    dev = _init(rank, world, port)
+    import json
+    from distributed_llm_training_gpu_manager_amd.parallel.comm import Comm
+    from distributed_llm_training_gpu_manager_amd.utils.meshcheck import run_checks
+    rec = run_checks(Comm(), dev)
+    if rank == 0:
+        with open(out_path, "w") as f:
+            json.dump(rec, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_mesh_self_check_passes_with_ranks_sharing_one_gpu(tmp_path):
+    """The checks the multi-GPU bench runs on itself before its mesh sweep (utils/meshcheck.py):
+    the same code, two ranks on one MI355X (gloo for the bootstrap and as the "RCCL" side)."""
+    import json
+    out = str(tmp_path / "check.json")
+    mp.spawn(_check_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    with open(out) as f:
+        rec = json.load(f)
+    assert rec["pass"], rec
+    assert rec["all_gather"]["pass"] and rec["reduce_scatter"]["bit_exact_vs_rank_order_fp32"], rec
+    ep = rec["ep_dispatch_combine"]
+    assert ep["pass"] and ep["max_rows_received"] > 512 * 2, ep  # the skewed routing exceeded the balanced share
+    par = rec["zero3_parity"]
+    assert par["rccl_vs_world1"]["pass"] and par["mesh_vs_world1"]["pass"] and par["mesh_collectives_issued"] > 0
