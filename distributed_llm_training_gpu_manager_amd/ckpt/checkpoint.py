@@ -51,6 +51,7 @@ import torch
 
 from .. import _host
 from .ptzip import PtWriter, Slot, read_slot
+from ..utils.streams import owned_stream
 
 STATE = ("master", "exp_avg", "exp_avg_sq")
 TAG_RE = re.compile(r"^global_step(\d+)$")
@@ -167,7 +168,7 @@ class AsyncCheckpointer:
         self._unreg = None
         self._restored_map: Optional[torch.Tensor] = None  # the shm file mapped by a restore (reused, see _load_shm)
         self._ring: List[torch.Tensor] = []
-        self._stream = torch.cuda.Stream(self.dev) if self.cuda else None
+        self._stream = owned_stream(self.dev, "ckpt") if self.cuda else None
         self._capture_ev = None
         self._pending = 0
         self._saves = 0
@@ -179,6 +180,7 @@ class AsyncCheckpointer:
         self.rollbacks: List[str] = []
         self.restored_from: Optional[str] = None
         self._prep: Optional[threading.Thread] = None
+        self.prep_stats: Dict[str, Any] = {}  # snapshot-buffer preparation: fallocate / register seconds
         # the 16-bit module state dict in mp_rank_00_model_states.pt (DeepSpeed: always for stages 0-2; stage 3
         # with stage3_gather_16bit_weights_on_model_save): rank 0 keeps a pinned host copy per save
         self.module = bool(module if module is not None else
@@ -231,6 +233,14 @@ class AsyncCheckpointer:
             torch.cuda.current_stream(self.dev).wait_event(self._capture_ev)
 
     def _alloc_snapshot(self) -> None:
+        t0 = time.time()
+        try:
+            self._alloc_snapshot_inner()
+        finally:
+            self.prep_stats["alloc_s"] = round(time.time() - t0, 2)
+            self.prep_stats["done_at"] = time.time()
+
+    def _alloc_snapshot_inner(self) -> None:
         nb = self.snap_bytes
         if self.mode == "shm":
             keep, self._restored_map = self._restored_map, None
@@ -241,8 +251,10 @@ class AsyncCheckpointer:
                 # reserve the pages now (posix_fallocate): a full tmpfs is an error here, not a SIGBUS in the middle
                 # of a snapshot copy into a sparse file
                 fd = os.open(self.shm_path, os.O_RDWR | os.O_CREAT, 0o600)
+                tf = time.time()
                 try:
                     os.posix_fallocate(fd, 0, nb)
+                    self.prep_stats["fallocate_s"] = round(time.time() - tf, 2)
                     reserved = True
                 except OSError as e:
                     reserved = False
@@ -259,7 +271,9 @@ class AsyncCheckpointer:
                     return
                 snap = torch.from_file(self.shm_path, shared=True, size=nb, dtype=torch.uint8)
             if self.cuda:
+                tr = time.time()
                 self._pinned_shm = self._register_chunked(snap.data_ptr(), nb)
+                self.prep_stats["register_s"] = round(time.time() - tr, 2)
             self._snap = snap
         elif self.mode == "device":
             self._snap = torch.empty(nb, dtype=torch.uint8, device=self.dev)
@@ -332,6 +346,7 @@ class AsyncCheckpointer:
         if not self.prepare:
             return
         if self.active and self._snap is None and self._prep is None:
+            self.prep_stats["started_at"] = time.time()
             self._prep = threading.Thread(target=self._alloc_snapshot, daemon=True, name="ckpt-prepare")
             self._prep.start()
 

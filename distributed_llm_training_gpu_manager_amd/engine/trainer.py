@@ -336,6 +336,7 @@ class Trainer:
         self._tokens_step = self.ecfg.micro_batch_size * self.ecfg.seq_len * self.ecfg.grad_accum * self.env.world
         self._t_last = time.time()
         self._reports, self._last_step_s, self._last_reported = 0, None, start
+        self._step_timing = int(os.environ.get("DLGM_STEP_TIMING", "0") or 0)
         write_heartbeat(self.env.rank, start, phase="ready")  # restored / initialised: the first step is next
         self.engine.sync_flags = self.env.world > 1
         first_attempt = os.environ.get("DLGM_RESTART", "0") == "0"
@@ -352,10 +353,16 @@ class Trainer:
                 self.engine.fault_inject_nan = True
             self.engine.host_flag = 1.0 if self.preempt else 0.0
             prof = getattr(a, "profile_steps", 0) and step - start == 2  # trace window after one warm step
+            t_iss = time.time()
             with trace_window(a.profile_dir if prof else None, self.env.rank):
                 m = self.engine.train_step(self.data.batches(step))
                 for _ in range(a.profile_steps - 1 if prof else 0):  # extra traced steps reuse this step's data
                     self.engine.train_step(self.data.batches(step))
+            if self._step_timing and step - start <= self._step_timing and self.env.device.type == "cuda":
+                # diagnostic (DLGM_STEP_TIMING=N: the first N steps of this attempt): host issue time vs device time
+                t_q = time.time()
+                torch.cuda.synchronize(self.env.device)
+                self._say(f"step-timing: step {step} issue {t_q - t_iss:.3f}s device-done {time.time() - t_iss:.3f}s")
             # [sum g^2, non-finite, flags, loss, unscaled grad norm, transport]: read one step late from the pinned
             # ring (no sync in the loop); the fp16 loss scale stays on the device
             self.trap.record(step, self._report_vector(m))
@@ -421,6 +428,13 @@ class Trainer:
             rc = EXIT_PREEMPTED
         if self.ckpt is not None:
             self.ckpt.wait()
+            if self.ckpt.prep_stats:
+                ps = dict(self.ckpt.prep_stats)
+                t0 = ps.pop("started_at", None)
+                if t0 is not None and "done_at" in ps:
+                    ps["done_after_start_s"] = round(ps.pop("done_at") - t0, 2)
+                    ps["started_after_process_s"] = round(t0 - self.timeline["process_start"], 2)
+                self._say("ckpt prepare: " + json.dumps(ps))
             if rc == 0 and a.export:
                 export_consolidated(self.engine, a.export)
             # a finished job has nothing to resume: give the host RAM of the shm snapshot tier back

@@ -23,6 +23,7 @@ from collections import deque
 from typing import Callable, Deque, Dict, List, Optional, Tuple
 
 import torch
+from ..utils.streams import owned_stream
 
 
 class NanTrap:
@@ -43,7 +44,7 @@ class NanTrap:
         self._pending: Deque = deque()
         self._lock = threading.Lock()
         self._done = threading.Condition(self._lock)
-        self._stream = torch.cuda.Stream(device) if self._cuda else None
+        self._stream = owned_stream(device, "nan-trap") if self._cuda else None
         self._stop = threading.Event()
         self._poll_s = poll_s
         self._thread = threading.Thread(target=self._watch, daemon=True, name="nan-trap")

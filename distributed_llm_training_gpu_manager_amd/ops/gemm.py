@@ -133,14 +133,59 @@ def lt_mm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, acc: bool) -> boo
 _F16_PICK: dict = {}
 
 
+def _f16_cache_path() -> Path:
+    base = os.environ.get("DLGM_TUNE_CACHE") or os.path.join(os.path.expanduser("~"), ".cache", "dlgm")
+    _lt_table()
+    return Path(base) / f"gemm_lt_f16_v{_LT['version']}.json"
+
+
+def _f16_load() -> None:
+    """Recorded fp16 picks: the committed table (tuned/gemm_lt_f16_v<ver>.json) first, then this host's cache."""
+    if _F16_PICK:
+        return
+    _lt_table()
+    for path in (TUNED_DIR / f"gemm_lt_f16_v{_LT['version']}.json", _f16_cache_path()):
+        try:
+            with open(path) as f:
+                for k, v in json.load(f).get("solutions", {}).items():
+                    _F16_PICK.setdefault(k, int(v))
+        except (OSError, ValueError):
+            pass
+    _F16_PICK.setdefault("", -1)  # loaded marker
+
+
+def _f16_persist(key: str, idx: int) -> None:
+    """Merge one timed pick into the host cache (atomic replace): every later process reuses it."""
+    path = _f16_cache_path()
+    try:
+        path.parent.mkdir(parents=True, exist_ok=True)
+        cur = {}
+        if path.exists():
+            with open(path) as f:
+                cur = json.load(f).get("solutions", {})
+        cur.setdefault(key, idx)
+        tmp = path.with_suffix(f".{os.getpid()}.tmp")
+        with open(tmp, "w") as f:
+            json.dump({"solutions": cur}, f, indent=1, sort_keys=True)
+        os.replace(tmp, path)
+    except (OSError, ValueError):
+        pass
+
+
 def _f16_solution(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, beta: float) -> int:
-    """Fastest of hipBLASLt's top heuristic candidates for this fp16 problem, timed once per process."""
+    """hipBLASLt solution for this fp16 -> fp32 problem. Timing picks the fastest of the heuristic's top
+    candidates, but two candidates within timing noise of each other would make the pick -- and with it the
+    summation order, i.e. the bits -- differ from process to process. So a pick is taken from the committed
+    table or this host's cache when one is recorded; only a problem seen nowhere is timed, and its pick is
+    written to the cache at once, so every later process computes the same bits."""
+    _f16_load()
     key = _lt_key(out, a, b, beta)
     idx = _F16_PICK.get(key)
     if idx is None:
         res = hip_ops().gemm_lt_tune(out, a, b, beta, 24, False, 2)
         idx = int(res[0, 0]) if res.shape[0] else -1
         _F16_PICK[key] = idx
+        _f16_persist(key, idx)
     return idx
 
 

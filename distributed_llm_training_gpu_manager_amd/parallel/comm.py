@@ -24,6 +24,7 @@ from typing import Callable, List, Optional
 
 import torch
 import torch.distributed as dist
+from ..utils.streams import owned_stream
 
 
 class Handle:
@@ -257,7 +258,7 @@ class ShadowComm(Comm):
         dev = tensors[0].device
         cur = torch.cuda.current_stream(dev)
         if self._stream is None:
-            self._stream = torch.cuda.Stream(dev)
+            self._stream = owned_stream(dev, "shadow-comm")
         s = self._stream
         s.wait_stream(cur)
         with torch.cuda.stream(s):

@@ -44,6 +44,7 @@ import torch.distributed as dist
 
 from .._native import hip_ops
 from .comm import Comm, Handle
+from ..utils.streams import owned_stream
 
 CNT, DATA, ACK, VER, RDONE = 0, 1, 2, 3, 4
 ST_EPOCH, ST_VER, ST_ERR, ST_OVF, ST_SHADOW = 0, 16, 17, 18, 19
@@ -122,7 +123,7 @@ class XgmiMesh:
         self.timeout_ticks = int(timeout_s * 100e6)  # s_memrealtime runs at 100 MHz on MI355X
         # one stream per traffic class (parameter gathers / gradient reductions), like the engine's two RCCL
         # communicators: a prefetch gather and a reduce-scatter run concurrently
-        self._streams: Dict[str, torch.cuda.Stream] = {k: torch.cuda.Stream(device) for k in ("ag", "rs")}
+        self._streams: Dict[str, torch.cuda.Stream] = {k: owned_stream(device, f"mesh-{k}") for k in ("ag", "rs")}
         self.closed = False
         self.issued = 0
         if self.W > 1 and not self.shadow:  # nobody may write into a heap before every rank mapped every heap

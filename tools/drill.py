@@ -77,6 +77,8 @@ def drill_sigkill(a, work):
             "mttr_s": [round(x, 2) for x in job.mttr_s], "resume_load_s": [float(s) for _, s in resumed],
             "resumed_from_step": [int(s) for s, _ in resumed], "restored_from": via, "restore_breakdown": stats,
             "startup_timeline": startup,  # per launch: imports / process group / engine / restore / first step
+            "step_timing": re.findall(r"step-timing: (.*)", log),  # DLGM_STEP_TIMING: issue vs device-done per step
+            "ckpt_prepare": [json.loads(x) for x in re.findall(r"ckpt prepare: (\{.*?\})", log)],
             "events": job.events,
             "ckpt_after_resume": hist,
             "step_s_after_resume": steps_after,

@@ -29,7 +29,7 @@ def main() -> int:
     ap.add_argument("--n-layers", type=int, default=0)
     ap.add_argument("--warm", default="none", help="none | engine (ZeroEngine.warm_up before step 1)")
     ap.add_argument("--per-unit", type=int, default=1, help="sync + time every unit (changes overlap)")
-    ap.add_argument("--ckpt", dest="ckpt_tier", default="none", help="none | shm: an AsyncCheckpointer with the "
+    ap.add_argument("--ckpt-tier", dest="ckpt_tier", default="none", help="none | shm: an AsyncCheckpointer with the "
                     "/dev/shm tier whose snapshot buffer is prepared in the background from before step 1 (the "
                     "trainer's first launch)")
     ap.add_argument("--save-after", type=int, default=-1, help="save after this step (0-based)")
