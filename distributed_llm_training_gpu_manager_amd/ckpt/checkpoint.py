@@ -60,6 +60,9 @@ MODEL0 = "mp_rank_00_model_states.pt"
 # 1 GiB pieces with 5 ms pauses kept the first step after a restore at 0.9 s (one whole-file registration: 6.4 s)
 REG_CHUNK = 1 << 30
 REG_PAUSE_S = 0.005
+# pinned slots of the capture into a not-yet-page-locked part of the shm snapshot (_ring_capture)
+RING_SLOT = 256 << 20
+RING_SLOTS = 4
 DS_VERSION = "0.13.1+dlgm-mi355x"  # the DeepSpeed release the reference pins (requirements.txt:6)
 
 
@@ -163,12 +166,17 @@ class AsyncCheckpointer:
         self._snap: Optional[torch.Tensor] = None  # uint8 [14 n]: fp32 master | exp_avg | exp_avg_sq | bf16 params
         self._pinned_shm = False
         self._reg: List[Tuple[int, int]] = []  # page-locked pieces of the shm snapshot (address, bytes)
-        self._reg_hurry = threading.Event()
+        self._falloc_done = 0  # shm snapshot bytes [0, _falloc_done) reserved
+        self._reg_done = 0  # ... and [0, _reg_done) page-locked (the DMA part of a save)
+        self._reg_failed = False
+        self._slots: List[torch.Tensor] = []  # pinned slots of _ring_capture
+        self._prep_yield = threading.Event()  # a save needs the buffer now: stop preparing after this piece
         self._reg_stop = threading.Event()
         self._unreg = None
         self._restored_map: Optional[torch.Tensor] = None  # the shm file mapped by a restore (reused, see _load_shm)
         self._ring: List[torch.Tensor] = []
         self._stream = owned_stream(self.dev, "ckpt") if self.cuda else None
+        self.last_ring: Dict[str, Any] = {}
         self._capture_ev = None
         self._pending = 0
         self._saves = 0
@@ -237,44 +245,33 @@ class AsyncCheckpointer:
         try:
             self._alloc_snapshot_inner()
         finally:
-            self.prep_stats["alloc_s"] = round(time.time() - t0, 2)
-            self.prep_stats["done_at"] = time.time()
+            self.prep_stats["alloc_s"] = round(self.prep_stats.get("alloc_s", 0.0) + time.time() - t0, 2)
+            if self.mode != "shm" or self._falloc_done >= self.snap_bytes:
+                self.prep_stats["done_at"] = time.time()
 
     def _alloc_snapshot_inner(self) -> None:
         nb = self.snap_bytes
         if self.mode == "shm":
-            keep, self._restored_map = self._restored_map, None
-            if keep is not None and self.shm_path == self.shm_src_path and keep.numel() == nb:
-                snap = keep  # the file this rank just restored from, already mapped (and its pages touched)
-            else:
-                del keep
-                # reserve the pages now (posix_fallocate): a full tmpfs is an error here, not a SIGBUS in the middle
-                # of a snapshot copy into a sparse file
-                fd = os.open(self.shm_path, os.O_RDWR | os.O_CREAT, 0o600)
-                tf = time.time()
-                try:
-                    os.posix_fallocate(fd, 0, nb)
-                    self.prep_stats["fallocate_s"] = round(time.time() - tf, 2)
-                    reserved = True
-                except OSError as e:
-                    reserved = False
-                    self.tier_notes.append(f"shm reservation of {nb} B failed ({e}); snapshot tier -> host memory")
-                finally:
-                    os.close(fd)
-                if not reserved:
+            if self._snap is None:
+                keep, self._restored_map = self._restored_map, None
+                if keep is not None and self.shm_path == self.shm_src_path and keep.numel() == nb:
+                    self._snap = keep  # the file this rank just restored from, already mapped (pages touched)
+                    self._falloc_done = nb
+                else:
+                    del keep
+                    fd = os.open(self.shm_path, os.O_RDWR | os.O_CREAT, 0o600)
                     try:
-                        os.unlink(self.shm_path)
-                    except OSError:
-                        pass
-                    self.mode = "host"
-                    self._snap = torch.empty(nb, dtype=torch.uint8, pin_memory=self.cuda)
-                    return
-                snap = torch.from_file(self.shm_path, shared=True, size=nb, dtype=torch.uint8)
-            if self.cuda:
-                tr = time.time()
-                self._pinned_shm = self._register_chunked(snap.data_ptr(), nb)
-                self.prep_stats["register_s"] = round(time.time() - tr, 2)
-            self._snap = snap
+                        os.ftruncate(fd, nb)
+                    finally:
+                        os.close(fd)
+                    self._snap = torch.from_file(self.shm_path, shared=True, size=nb, dtype=torch.uint8)
+            if not self._prepare_shm(nb):
+                try:
+                    os.unlink(self.shm_path)
+                except OSError:
+                    pass
+                self.mode = "host"
+                self._snap = torch.empty(nb, dtype=torch.uint8, pin_memory=self.cuda)
         elif self.mode == "device":
             self._snap = torch.empty(nb, dtype=torch.uint8, device=self.dev)
             self._ring = [torch.empty(self.ring_elems, dtype=torch.float32, pin_memory=True) for _ in range(2)]
@@ -296,34 +293,63 @@ class AsyncCheckpointer:
         unreg.restype, unreg.argtypes = ctypes.c_int, [ctypes.c_void_p]
         return (lambda p_, n_: int(reg(p_, n_, 0))), (lambda p_: int(unreg(p_)))
 
-    def _register_chunked(self, ptr: int, nb: int) -> bool:
-        """Page-lock the mapped snapshot file in REG_CHUNK pieces with a pause between them. One
-        hipHostRegister of the whole ~112 GB file holds the HIP runtime for ~6 s and every kernel launch of
-        the training thread waits meanwhile (measured on MI355X: the first step after a restore took 6.4 s
-        instead of 0.9 s); pieces with a short pause let the training thread launch between them, and a
-        save that needs the buffer sets _reg_hurry to finish without pauses. Device copies into the snapshot
-        are split at the piece boundaries (_copy_to_snap)."""
-        fns = self._hip_register_fns()
-        if fns is None:
+    def _prepare_shm(self, nb: int) -> bool:
+        """Reserve (posix_fallocate: a full tmpfs is an error here, not a SIGBUS in the middle of a snapshot copy)
+        and page-lock the mapped snapshot file piece by piece, REG_CHUNK bytes at a time, front to back, with a
+        short pause between pieces. One hipHostRegister of a whole ~112 GB file holds the HIP runtime for ~6 s
+        and every kernel launch of the training thread waits meanwhile (MI355X: the first step after a restore
+        took 6.4 s instead of 0.9 s); pieces with a pause let the training thread launch between them.
+
+        The prepared prefix [0, _reg_done) is what a save copies by DMA at ~57 GB/s; a save that arrives first
+        (an early spot notice) sets _prep_yield, this loop stops after its current piece, the save streams the
+        rest through pinned slots (_ring_capture) and restarts the preparation afterwards. Returns False when
+        the reservation failed (the caller falls back to the host tier)."""
+        fd = os.open(self.shm_path, os.O_RDWR)
+        ptr = self._snap.data_ptr()
+        fns = self._hip_register_fns() if self.cuda else None
+        if self.cuda and fns is None:
             cr = torch.cuda.cudart()
             fns = (lambda p_, n_: int(cr.cudaHostRegister(p_, n_, 0))), (lambda p_: int(cr.cudaHostUnregister(p_)))
-        self._unreg = fns[1]
-        self._reg = []
-        off = 0
-        while off < nb:
-            if self._reg_stop.is_set():  # close() while page-locking: it unregisters what is in self._reg
-                return False
-            ln = min(REG_CHUNK, nb - off)
-            if fns[0](ptr + off, ln) != 0:
-                for p_, _ in self._reg:
-                    fns[1](p_)
-                self._reg = []
-                return False
-            self._reg.append((ptr + off, ln))
-            off += ln
-            if REG_PAUSE_S > 0 and off < nb and not self._reg_hurry.is_set():
-                time.sleep(REG_PAUSE_S)
-        return True
+        if fns is not None:
+            self._unreg = fns[1]
+        try:
+            off = min(self._falloc_done, self._reg_done if (self.cuda and not self._reg_failed) else nb)
+            while off < nb:
+                if self._prep_yield.is_set() or self._reg_stop.is_set():
+                    return True
+                ln = min(REG_CHUNK, nb - off)
+                if self._falloc_done <= off:
+                    tf = time.time()
+                    try:
+                        os.posix_fallocate(fd, off, ln)
+                    except OSError as e:
+                        self.tier_notes.append(f"shm reservation of {nb} B failed ({e}); snapshot tier -> host memory")
+                        self._unregister_all()
+                        return False
+                    self._falloc_done = off + ln
+                    self.prep_stats["fallocate_s"] = round(self.prep_stats.get("fallocate_s", 0.0) + time.time() - tf, 3)
+                if fns is not None and not self._reg_failed and self._reg_done <= off:
+                    tr = time.time()
+                    if fns[0](ptr + off, ln) != 0:
+                        self._reg_failed = True  # the rest goes through the pinned slots; never a correctness issue
+                        self.tier_notes.append("hipHostRegister of the shm snapshot failed; pinned-slot capture")
+                    else:
+                        self._reg.append((ptr + off, ln))
+                        self._reg_done = off + ln
+                    self.prep_stats["register_s"] = round(self.prep_stats.get("register_s", 0.0) + time.time() - tr, 3)
+                off += ln
+                if REG_PAUSE_S > 0 and off < nb:
+                    time.sleep(REG_PAUSE_S)
+            self._pinned_shm = self.cuda and self._reg_done >= nb
+            return True
+        finally:
+            os.close(fd)
+
+    def _unregister_all(self) -> None:
+        if self._unreg is not None:
+            for p_, _ in self._reg:
+                self._unreg(p_)
+        self._reg, self._reg_done, self._pinned_shm = [], 0, False
 
     def _copy_to_snap(self, dst: torch.Tensor, src: torch.Tensor) -> None:
         """dst (a flat view of the snapshot) <- src, asynchronously, never crossing a page-locked piece."""
@@ -339,14 +365,48 @@ class AsyncCheckpointer:
             dst[i:i + m].copy_(src[i:i + m], non_blocking=True)
             i += m
 
+    def _ring_capture(self, segs: List[Tuple[int, torch.Tensor]], lo: int, hi: int) -> List[int]:
+        """Snapshot bytes [lo, hi) <- the device state, through RING_SLOTS pinned slots: the D2H of piece k+1..
+        runs on the checkpoint stream while _host's 16 threads copy piece k into the mapping (faulting its pages
+        in parallel) with the per-CHUNK CRC32C of the copied bytes. Blocks the calling thread; ~31 GB/s on
+        MI355X against ~9 GB/s for a plain copy into an unregistered mapping (tools/diag/r05/shm_bench.py).
+        `segs`: (snapshot byte offset, flat uint8 view of the device source). lo is CHUNK-aligned."""
+        if not self._slots:
+            self._slots = [torch.empty(RING_SLOT, dtype=torch.uint8, pin_memory=True) for _ in range(RING_SLOTS)]
+        crcs: List[int] = []
+        pend: List[Tuple[int, int, int, Any]] = []
+
+        def drain():
+            k, off, ln, ev = pend.pop(0)
+            ev.synchronize()
+            crcs.extend(_host.copy_crc32c_chunks(self._slots[k % RING_SLOTS][:ln], self._snap[off:off + ln]))
+        for k, off in enumerate(range(lo, hi, RING_SLOT)):
+            if len(pend) == RING_SLOTS:
+                drain()
+            ln = min(RING_SLOT, hi - off)
+            slot = self._slots[k % RING_SLOTS]
+            with torch.cuda.stream(self._stream):
+                for base, src in segs:
+                    a, b = max(off, base), min(off + ln, base + src.numel())
+                    if a < b:
+                        slot[a - off:b - off].copy_(src[a - base:b - base], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self._stream)
+            pend.append((k, off, ln, ev))
+        while pend:
+            drain()
+        return crcs
+
     def prepare_async(self) -> None:
-        """Allocate (and page-lock) the snapshot buffer on a background thread while training runs, so the
+        """Reserve (and page-lock) the snapshot buffer on a background thread while training runs, so the
         first save -- often an emergency one on a spot notice -- does not pay for 14 B/param of fresh host
-        pages. Call it after any restore: the shm tier's file is the one a restore reads."""
+        pages. Called when the job starts (and again after a save that interrupted it)."""
         if not self.prepare:
             return
-        if self.active and self._snap is None and self._prep is None:
-            self.prep_stats["started_at"] = time.time()
+        if self.active and self._prep is None and (self._snap is None or (
+                self.mode == "shm" and (self._falloc_done < self.snap_bytes or
+                                        (self.cuda and not self._reg_failed and self._reg_done < self.snap_bytes)))):
+            self.prep_stats.setdefault("started_at", time.time())
             self._prep = threading.Thread(target=self._alloc_snapshot, daemon=True, name="ckpt-prepare")
             self._prep.start()
 
@@ -368,11 +428,14 @@ class AsyncCheckpointer:
         if self.busy:  # previous write-out still streaming from the snapshot buffer
             self.wait()
         save_id = f"{step}.{self._restart}.{self._saves}"
+        interrupted = False
         if self._prep is not None:
-            self._reg_hurry.set()  # a save is waiting: page-lock the rest without yielding to training
-            self._prep.join()  # background allocation / page-locking of the snapshot buffer
+            self._prep_yield.set()  # a save is waiting: stop preparing after the current piece
+            self._prep.join()
             self._prep = None
-        if self._snap is None:
+            self._prep_yield.clear()
+            interrupted = True
+        if self._snap is None or (not self.prepare and self.mode == "shm" and self._falloc_done < self.snap_bytes):
             self._alloc_snapshot()
         if self.mode == "shm" and os.path.exists(self.shm_meta):
             os.unlink(self.shm_meta)  # the snapshot is about to change: never restore a torn one
@@ -380,12 +443,25 @@ class AsyncCheckpointer:
         v = self._views(self._snap)
         srcs = [(v["master"], eng.master), (v["exp_avg"], eng.exp_avg), (v["exp_avg_sq"], eng.exp_avg_sq),
                 (v["bf16"], eng.p16_shard)]
+        ring_crcs: Optional[Tuple[int, List[int]]] = None
         if self.cuda:
             cur = torch.cuda.current_stream(self.dev)
             self._stream.wait_stream(cur)
+            # shm tier: the page-locked prefix by DMA, the rest (a save that came before the preparation
+            # finished) through the pinned slots -- first, so the training thread returns while the DMA runs
+            dma_end = self._reg_done if (self.mode == "shm" and not self._pinned_shm) else self.snap_bytes
+            if dma_end < self.snap_bytes:
+                tr = time.time()
+                segs = [(dst.data_ptr() - self._snap.data_ptr(), s.reshape(-1).view(torch.uint8)) for dst, s in srcs]
+                ring_crcs = (dma_end, self._ring_capture(segs, dma_end, self.snap_bytes))
+                self._falloc_done = max(self._falloc_done, self.snap_bytes)  # every page now exists
+                self.last_ring = {"bytes": self.snap_bytes - dma_end, "s": round(time.time() - tr, 3)}
             with torch.cuda.stream(self._stream):
                 for dst, s in srcs:
-                    self._copy_to_snap(dst, s)
+                    a = dst.data_ptr() - self._snap.data_ptr()
+                    n_dma = max(0, min(dst.numel() * dst.element_size(), dma_end - a)) // dst.element_size()
+                    if n_dma:
+                        self._copy_to_snap(dst[:n_dma], s[:n_dma])
                 ev = torch.cuda.Event()
                 ev.record(self._stream)
             self._capture_ev = ev
@@ -393,9 +469,12 @@ class AsyncCheckpointer:
             for dst, s in srcs:
                 dst.copy_(s)
             ev = None
+        if interrupted:
+            self.prepare_async()  # page-lock the rest in the background for the next save
         mod_ev = self._capture_module() if (self.module and self.disk) else None
         meta = self._meta(step, client_state or {})
         meta["_module_ev"] = mod_ev
+        meta["_ring_crcs"] = ring_crcs
         with self._plock:
             self._pending += 1
         self._q.put((tag, step, save_id, ev, meta, t0))
@@ -534,10 +613,17 @@ class AsyncCheckpointer:
                 time.sleep(0.0005)
         t_cap = time.time()
         v = self._views(self._snap)
+        ring_crcs = meta.pop("_ring_crcs", None)
         rec: Dict[str, Any] = {"tag": tag, "step": step, "capture_s": t_cap - t0, "mode": self.mode,
                                "bytes": self.snap_bytes}
+        if ring_crcs is not None:
+            rec["ring"] = dict(self.last_ring)
         if self.mode == "shm":
-            crcs = _host.crc32c_chunks(self._snap)
+            if ring_crcs is not None:  # the pinned-slot part was checksummed while it was copied
+                lo, tail = ring_crcs
+                crcs = (_host.crc32c_chunks(self._snap[:lo]) if lo else []) + list(tail)
+            else:
+                crcs = _host.crc32c_chunks(self._snap)
             tmpm = self.shm_meta + ".tmp"
             with open(tmpm, "w") as f:
                 json.dump({"save_dir": self.save_dir, "step": step, "save_id": save_id, "sig": self.sig,
@@ -868,11 +954,11 @@ class AsyncCheckpointer:
             self._prep.join()
             self._prep = None
         if self.cuda and self._reg:
-            for p_, _ in self._reg:
-                self._unreg(p_)
-        self._reg = []
+            self._unregister_all()
+        self._reg, self._reg_done, self._falloc_done = [], 0, 0
         self._pinned_shm = False
         self._snap = None
+        self._slots = []
         self._restored_map = None
         if discard_shm:
             self.discard_shm()

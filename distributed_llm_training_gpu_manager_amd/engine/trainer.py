@@ -380,13 +380,20 @@ class Trainer:
                     rc = stop
                     break
             save_due = self.ckpt is not None and a.save_interval > 0 and step % a.save_interval == 0
-            if save_due:  # never persist a step before knowing it is clean
+            # the first step of a resumed attempt is read at once: recovery (the supervisor's MTTR) is confirmed when
+            # that step is done, not one step later
+            confirm = start > 0 and step == start + 1
+            if save_due or confirm:  # never persist a step before knowing it is clean
                 rec = self._report(step, issued)
                 stop = self._decide(rec, step)
                 if stop is not None:
                     rc = stop
                     break
-                self.ckpt.save(step, client_state={"step": step, "global_batch": self.global_batch})
+                if self._prep_after_first:
+                    self._prep_after_first = False
+                    self.ckpt.prepare_async()
+                if save_due:
+                    self.ckpt.save(step, client_state={"step": step, "global_batch": self.global_batch})
             else:
                 prev = (step, issued)
             if a.kill_at_step == step and first_attempt and self.env.rank == a.kill_rank:
@@ -426,6 +433,13 @@ class Trainer:
                 self.ckpt.save(last, client_state={"step": last, "preempted": True,
                                                       "global_batch": self.global_batch}, blocking=True)
             rc = EXIT_PREEMPTED
+        if self.env.device.type == "cuda":
+            dv = self.env.device
+            self._say("memory: " + json.dumps({
+                "peak_allocated_GiB": round(torch.cuda.max_memory_allocated(dv) / 2 ** 30, 1),
+                "peak_reserved_GiB": round(torch.cuda.max_memory_reserved(dv) / 2 ** 30, 1),
+                "alloc_retries": int(torch.cuda.memory_stats(dv).get("num_alloc_retries", 0)),
+                "hbm_GiB": round(torch.cuda.get_device_properties(dv).total_memory / 2 ** 30, 1)}))
         if self.ckpt is not None:
             self.ckpt.wait()
             if self.ckpt.prep_stats:

@@ -283,6 +283,10 @@ class MixtralBlock(LlamaBlock):
                 for t in part:  # stashed operands freed after the flush: keep them until the side copies ran
                     t[2].record_stream(side)
                     t[3].record_stream(side)
+                # the row plan too: allocated on this stream and freed when the flush returns, its block would go to
+                # the next allocation here (the router backward's dlogits) while a lagging side stream still reads
+                # it as row indices
+                src.record_stream(side)
             else:
                 ops_g = (transpose_multi([t[2] for t in part], src), transpose_multi([t[3] for t in part], src))
             gm.grouped_wgrad(g["w_down"], ops_d[0], ops_d[1], poff, acc or i > 0, kmajor=True, stats=xs)

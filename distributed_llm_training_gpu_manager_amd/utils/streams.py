@@ -18,6 +18,7 @@ owners that manage their own capture rules: communicators, the optimizer stream,
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 from typing import Dict, Optional, Tuple
 
@@ -27,6 +28,7 @@ _STREAMS: Dict[Tuple[int, str], "torch.cuda.Stream"] = {}
 _KIND_NEXT: Dict[str, int] = {}
 _LOCK = threading.Lock()
 _HIP = {"lib": None}
+_POOL = os.environ.get("DLGM_STREAM_POOL", "0") == "1"  # diagnostic: draw from torch's pool as round 4 did
 TEST_DELAY_CYCLES = {"cycles": 0}  # test hook: side-stream work first spins this long (a missing wait then shows)
 
 
@@ -49,6 +51,8 @@ def _hip():
 
 
 def _new_stream(idx: int) -> "torch.cuda.Stream":
+    if _POOL:
+        return torch.cuda.Stream(torch.device("cuda", idx))
     lib = _hip()
     if lib:
         s = ctypes.c_void_p()
@@ -77,6 +81,8 @@ def owned_stream(device: torch.device, kind: str, slots: int = 16) -> "torch.cud
     """A dedicated stream for an object that owns one for its lifetime (a communicator, a mesh, the optimizer /
     checkpoint / NaN-trap copy streams): the next of `slots` streams of this kind, so the live objects of one
     engine never share a HIP stream while a process that builds thousands of them (the test suite) reuses a few."""
+    if _POOL:  # diagnostic A/B only: the round-4 behaviour (a fresh stream from torch's round-robin pool)
+        return torch.cuda.Stream(device)
     with _LOCK:
         k = _KIND_NEXT.get(kind, 0)
         _KIND_NEXT[kind] = k + 1

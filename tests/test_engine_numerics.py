@@ -250,6 +250,49 @@ def test_side_stream_work_is_waited_for_gpu(model):
         assert torch.equal(a, b)
 
 
+@pytest.mark.gpu
+def test_side_stream_inputs_survive_block_reuse_gpu(monkeypatch):
+    """A tensor read on a side stream must be record_stream-ed to it: otherwise, freed on the host, its block goes to
+    the next allocation of the issuing stream while the (lagging) side stream still reads it. Here the MoE dW
+    re-layout's side stream lags by ~15 ms and, right after every flush, the issuing stream grabs and scribbles over
+    every small block it can get; the trained state must stay bit-identical to an undisturbed run. (Round 5: the
+    re-layout's row plan was not recorded -- it was freed when the flush returned, and the router backward's next
+    allocations could land in it.)"""
+    from distributed_llm_training_gpu_manager_amd.models import mixtral as mx
+    from distributed_llm_training_gpu_manager_amd.utils import streams
+    mc = get_config("mixtral-tiny")
+    orig = mx.MixtralBlock._flush_wgrad_grouped
+    held = []
+
+    def scribbled(self, g, ctx=None):
+        orig(self, g, ctx)
+        for n in (64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384):
+            for _ in range(8):
+                # (segment 1, row 5): an in-range row of the re-layout's plan, so a read of a reused block gives a
+                # wrong result instead of a wild address
+                held.append(torch.full((n,), (1 << 24) | 5, dtype=torch.int32, device="cuda"))
+
+    res = {}
+    for disturb in (False, True):
+        streams.TEST_DELAY_CYCLES["cycles"] = 30_000_000 if disturb else 0
+        if disturb:
+            monkeypatch.setattr(mx.MixtralBlock, "_flush_wgrad_grouped", scribbled)
+        try:
+            ec = EngineConfig(zero_stage=3, micro_batch_size=2, seq_len=64, grad_accum=3, lr=1e-3,
+                              scheduler="constant", init_device="cpu")
+            eng = ZeroEngine(mc, ec, torch.device("cuda"))
+            g = torch.Generator().manual_seed(17)
+            for _ in range(3):
+                toks = [torch.randint(0, mc.vocab_size, (2, 65), generator=g) for _ in range(3)]
+                eng.train_step([(t[:, :-1].cuda(), t[:, 1:].cuda()) for t in toks])
+                held.clear()
+            res[disturb] = (eng.master.cpu(), eng.exp_avg_sq.cpu())
+        finally:
+            streams.TEST_DELAY_CYCLES["cycles"] = 0
+    for a, b in zip(res[False], res[True]):
+        assert torch.equal(a, b)
+
+
 def test_gpt2_kept_graph_matches_activation_checkpointing_cpu():
     """GPT-2 blocks keep their forward autograd graph; with activation checkpointing the engine re-runs
     the block right before its backward instead. Both must train identically."""

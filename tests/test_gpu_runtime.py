@@ -75,6 +75,49 @@ def test_shm_tier_checkpoint_roundtrip(tmp_path):
     assert torch.equal(d["optimizer_state_dict"]["fp32_flat_groups"][0], want.cpu())
 
 
+def test_shm_save_before_preparation_finishes_uses_pinned_slots(tmp_path, monkeypatch):
+    """An early save (a spot notice in the first steps) interrupts the background reservation / page-locking:
+    the page-locked prefix goes by DMA, the rest through the pinned slots with on-the-fly CRCs; the preparation
+    resumes afterwards, the snapshot restores bit-exactly and a later save is all-DMA."""
+    from distributed_llm_training_gpu_manager_amd.ckpt import checkpoint as C
+
+    monkeypatch.setattr(C, "REG_CHUNK", 64 << 20)
+    monkeypatch.setattr(C, "REG_PAUSE_S", 0.05)
+    e = _engine()
+    t = torch.randint(0, 32768, (1, 257), device="cuda")
+    e.train_step([(t[:, :-1], t[:, 1:])])
+    ck = C.AsyncCheckpointer(e, str(tmp_path), shm=True, disk=False)
+    assert ck.mode == "shm" and ck.snap_bytes > 4 * (64 << 20)
+    ck.prepare_async()
+    time.sleep(0.12)  # a few pieces prepared, most not
+    ck.save(1, {"step": 1}, blocking=True)
+    rec = ck.history[-1]
+    assert "ring" in rec and 0 < rec["ring"]["bytes"] < ck.snap_bytes, rec
+    want = e.master.clone()
+    import json
+
+    from distributed_llm_training_gpu_manager_amd import _host
+    with open(ck.shm_meta) as f:
+        meta = json.load(f)
+    snap = torch.from_file(ck.shm_path, shared=False, size=ck.snap_bytes, dtype=torch.uint8)
+    assert _host.crc32c_chunks(snap) == meta["crc"]  # slot-copied CRCs agree with a full recomputation
+    assert torch.equal(snap[:4 * ck.n].view(torch.float32), want.cpu())
+    del snap
+    if ck._prep is not None:
+        ck._prep.join()
+    assert ck._pinned_shm
+    e.train_step([(t[:, :-1], t[:, 1:])])
+    ck.save(2, {"step": 2}, blocking=True)
+    assert "ring" not in ck.history[-1]
+    want2 = e.master.clone()
+    ck.close()
+    e2 = _engine(seed=3)
+    ck2 = C.AsyncCheckpointer(e2, str(tmp_path), shm=True, disk=False)
+    assert ck2.load("auto")["step"] == 2
+    assert torch.equal(e2.master, want2) and not torch.equal(want, want2)
+    ck2.close(discard_shm=True)
+
+
 def _trainer(tmp, *extra):
     from distributed_llm_training_gpu_manager_amd.engine.trainer import Trainer, parse_args
 

@@ -106,12 +106,6 @@ def test_overlapped_optimizer_waits_per_group(model, world, kw):
     """cfg.optimizer_overlap with the optimizer stream spun before its updates (so a gather, fetch or gradient write
     that does not wait for its group's update reads or clobbers stale state): bit-identical to the flat update on the
     compute stream, with asynchronous (RCCL-ordered) collectives."""
-    # Warm-up run, discarded. After one particular earlier test selection, the first engine of this test
-    # computed step-1 gradients that differed in the last bits, by a different amount each time. The runs after
-    # it agreed with each other and with the synchronous shadow run. Any engine run before the reference removes
-    # the effect (a Llama one does too); a device sync and sleep does not (tools/diag/r04_flake_warm.sh). That
-    # points at process-level GEMM state, not at the optimizer stream this test checks.
-    _run(model, world, True, optimizer_overlap=False, **kw)
     ref, _ = _run(model, world, True, optimizer_overlap=False, **kw)
     got, _ = _run(model, world, True, opt_delay=2_000_000, optimizer_overlap=True, **kw)
     bad = [k for k in STATE if not torch.equal(ref[k], got[k])]

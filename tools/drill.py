@@ -79,6 +79,7 @@ def drill_sigkill(a, work):
             "startup_timeline": startup,  # per launch: imports / process group / engine / restore / first step
             "step_timing": re.findall(r"step-timing: (.*)", log),  # DLGM_STEP_TIMING: issue vs device-done per step
             "ckpt_prepare": [json.loads(x) for x in re.findall(r"ckpt prepare: (\{.*?\})", log)],
+            "memory": [json.loads(x) for x in re.findall(r"memory: (\{.*?\})", log)],
             "events": job.events,
             "ckpt_after_resume": hist,
             "step_s_after_resume": steps_after,
@@ -94,7 +95,10 @@ def drill_spot(a, work):
     res = re.findall(r"resumed from step (\d+) in ([0-9.]+)s", out2)
     via = re.findall(r"resumed from step \d+ in [0-9.]+s via (\S+)", out2)
     stats = re.findall(r"restore (\{.*?\})\)", out2)
-    return {"drill": "spot", "restore_breakdown": [json.loads(x) for x in stats], "exit_code_preempted": rc, "emergency_ckpt": em, "restore_exit": rc2,
+    return {"drill": "spot", "restore_breakdown": [json.loads(x) for x in stats], "exit_code_preempted": rc,
+            "emergency_ckpt": em, "restore_exit": rc2,
+            "memory": [json.loads(x) for x in re.findall(r"memory: (\{.*?\})", out + out2)],
+            "ckpt_prepare": [json.loads(x) for x in re.findall(r"ckpt prepare: (\{.*?\})", out + out2)],
             "restore": res, "restored_from": via, "restore_process_wall_s": round(dt2, 2),
             "tail": (out[-300:], out2[-300:])}
 

@@ -33,6 +33,12 @@ def main() -> int:
                     "/dev/shm tier whose snapshot buffer is prepared in the background from before step 1 (the "
                     "trainer's first launch)")
     ap.add_argument("--save-after", type=int, default=-1, help="save after this step (0-based)")
+    ap.add_argument("--save-dir", default=None, help="checkpoint dir (shared by a --kill-after-save run and a "
+                    "--resume run: the /dev/shm snapshot outlives the killed process, as in the SIGKILL drill)")
+    ap.add_argument("--kill-after-save", action="store_true", help="SIGKILL this process right after the save")
+    ap.add_argument("--resume", action="store_true", help="restore from --save-dir before step 1 (the snapshot "
+                    "buffer is then prepared after the first step, as the trainer does after a restore)")
+    ap.add_argument("--headroom", type=float, default=None, help="EngineConfig.hbm_headroom")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     t_imp0 = time.time()
@@ -48,7 +54,8 @@ def main() -> int:
            "import_s": round(time.time() - t_imp0, 2)}
     mc = get_config(a.model, **({"n_layers": a.n_layers} if a.n_layers else {}))
     ec = EngineConfig(zero_stage=3, micro_batch_size=1, seq_len=a.seq, grad_accum=1, lr=3e-5,
-                      activation_checkpointing=bool(a.ckpt))
+                      activation_checkpointing=bool(a.ckpt),
+                      **({"hbm_headroom": a.headroom} if a.headroom is not None else {}))
     t0 = time.time()
     eng = ZeroEngine(mc, ec, dev, ShadowComm(a.shadow_world, 0, async_mode=True))
     torch.cuda.synchronize()
@@ -63,11 +70,21 @@ def main() -> int:
     if a.ckpt_tier == "shm":
         import tempfile
         from distributed_llm_training_gpu_manager_amd.ckpt.checkpoint import AsyncCheckpointer
-        ck = AsyncCheckpointer(eng, tempfile.mkdtemp(prefix="probe_ck_"), shm=True, disk=False, keep_last=1)
+        ck = AsyncCheckpointer(eng, a.save_dir or tempfile.mkdtemp(prefix="probe_ck_"), shm=True, disk=False,
+                               keep_last=1)
         rec["ckpt_mode"] = ck.mode
-        t0 = time.time()
-        ck.prepare_async()
-        rec["prepare_started_s"] = round(time.time() - t0, 3)
+        if a.resume:
+            t0 = time.time()
+            cs = ck.load("auto")
+            torch.cuda.synchronize()
+            rec["restore_s"] = round(time.time() - t0, 2)
+            rec["restored_from"] = ck.restored_from
+            rec["restore_stats"] = getattr(ck, "restore_stats", {})
+            rec["resumed"] = cs is not None
+        else:
+            t0 = time.time()
+            ck.prepare_async()
+            rec["prepare_started_s"] = round(time.time() - t0, 3)
     unit_t = {}
     cur = {"step": 0}
     if a.per_unit:
@@ -104,13 +121,24 @@ def main() -> int:
         steps.append({"step_s": round(time.time() - t0, 3),
                       "reserved_GiB": round(torch.cuda.memory_reserved(dev) / 2 ** 30, 1),
                       "segments": int(st.get("segment.all.current", 0)),
-                      "alloc_calls": int(st.get("num_alloc_retries", 0)),
+                      "alloc_retries": int(st.get("num_alloc_retries", 0)),
+                      "peak_alloc_GiB": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1),
                       "hip_mallocs": int(st.get("segment.all.allocated", 0)),
                       "prep_alive": bool(ck is not None and ck._prep is not None and ck._prep.is_alive())})
+        if ck is not None and a.resume and s == 0:
+            ck.prepare_async()  # after the first recovered step, as the trainer does
         if ck is not None and s == a.save_after:
             t0 = time.time()
             ck.save(s + 1, blocking=True)
             steps[-1]["save_s"] = round(time.time() - t0, 2)
+            if a.kill_after_save:
+                rec["steps"] = steps
+                print(json.dumps(rec), flush=True)
+                if a.out:
+                    with open(a.out, "w") as f:
+                        json.dump(rec, f, indent=1)
+                import signal
+                os.kill(os.getpid(), signal.SIGKILL)
     rec["steps"] = steps
     if ck is not None:
         t0 = time.time()
