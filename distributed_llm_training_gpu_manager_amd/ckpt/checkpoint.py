@@ -177,6 +177,10 @@ class AsyncCheckpointer:
         self._ring: List[torch.Tensor] = []
         self._stream = owned_stream(self.dev, "ckpt") if self.cuda else None
         self.last_ring: Dict[str, Any] = {}
+        self.defer_moments = True  # shm restore: Adam moments restored beside the first step (_load_shm)
+        self._moments: Optional[threading.Thread] = None
+        self._moments_err: Optional[BaseException] = None
+        self._moments_ev = None
         self._capture_ev = None
         self._pending = 0
         self._saves = 0
@@ -294,16 +298,21 @@ class AsyncCheckpointer:
         return (lambda p_, n_: int(reg(p_, n_, 0))), (lambda p_: int(unreg(p_)))
 
     def _prepare_shm(self, nb: int) -> bool:
-        """Reserve (posix_fallocate: a full tmpfs is an error here, not a SIGBUS in the middle of a snapshot copy)
-        and page-lock the mapped snapshot file piece by piece, REG_CHUNK bytes at a time, front to back, with a
-        short pause between pieces. One hipHostRegister of a whole ~112 GB file holds the HIP runtime for ~6 s
-        and every kernel launch of the training thread waits meanwhile (MI355X: the first step after a restore
-        took 6.4 s instead of 0.9 s); pieces with a pause let the training thread launch between them.
+        """Make the mapped snapshot file ready for a DMA capture, in two passes of REG_CHUNK pieces, front to back:
 
-        The prepared prefix [0, _reg_done) is what a save copies by DMA at ~57 GB/s; a save that arrives first
+        1. reserve every page (posix_fallocate: a full tmpfs is an error here, not a SIGBUS in the middle of a
+           snapshot copy). ~19 GB/s on the MI355X host, pure kernel work that touches no HIP state; faulting the
+           pages in instead (first-touch writes or MADV_POPULATE_WRITE, 16 threads) ran at 3.8 GB/s
+           (tools/diag/r05/prefault_bench.py). Done first, so an early save finds the file allocated.
+        2. page-lock it (hipHostRegister) with a short pause between pieces: one registration of a whole ~112 GB
+           file holds the HIP runtime for ~6 s and every kernel launch of the training thread waits meanwhile
+           (MI355X: the first step after a restore took 6.4 s instead of 0.9 s).
+
+        The page-locked prefix [0, _reg_done) is what a save copies by DMA at ~57 GB/s; a save that arrives first
         (an early spot notice) sets _prep_yield, this loop stops after its current piece, the save streams the
-        rest through pinned slots (_ring_capture) and restarts the preparation afterwards. Returns False when
-        the reservation failed (the caller falls back to the host tier)."""
+        rest through pinned slots (_ring_capture, reserving what pass 1 has not reached yet just ahead of the
+        copy) and restarts the preparation afterwards. Returns False when the reservation failed (the caller falls
+        back to the host tier)."""
         fd = os.open(self.shm_path, os.O_RDWR)
         ptr = self._snap.data_ptr()
         fns = self._hip_register_fns() if self.cuda else None
@@ -312,38 +321,49 @@ class AsyncCheckpointer:
             fns = (lambda p_, n_: int(cr.cudaHostRegister(p_, n_, 0))), (lambda p_: int(cr.cudaHostUnregister(p_)))
         if fns is not None:
             self._unreg = fns[1]
+
+        def stopped() -> bool:
+            return self._prep_yield.is_set() or self._reg_stop.is_set()
         try:
-            off = min(self._falloc_done, self._reg_done if (self.cuda and not self._reg_failed) else nb)
-            while off < nb:
-                if self._prep_yield.is_set() or self._reg_stop.is_set():
+            while self._falloc_done < nb:
+                if stopped():
                     return True
+                off = self._falloc_done
+                tf = time.time()
+                if not self._reserve(fd, off, min(REG_CHUNK, nb - off)):
+                    self._unregister_all()
+                    return False
+                self.prep_stats["fallocate_s"] = round(self.prep_stats.get("fallocate_s", 0.0) + time.time() - tf, 3)
+            self.prep_stats.setdefault("reserved_at", time.time())
+            while fns is not None and not self._reg_failed and self._reg_done < nb:
+                if stopped():
+                    return True
+                off = self._reg_done
                 ln = min(REG_CHUNK, nb - off)
-                if self._falloc_done <= off:
-                    tf = time.time()
-                    try:
-                        os.posix_fallocate(fd, off, ln)
-                    except OSError as e:
-                        self.tier_notes.append(f"shm reservation of {nb} B failed ({e}); snapshot tier -> host memory")
-                        self._unregister_all()
-                        return False
-                    self._falloc_done = off + ln
-                    self.prep_stats["fallocate_s"] = round(self.prep_stats.get("fallocate_s", 0.0) + time.time() - tf, 3)
-                if fns is not None and not self._reg_failed and self._reg_done <= off:
-                    tr = time.time()
-                    if fns[0](ptr + off, ln) != 0:
-                        self._reg_failed = True  # the rest goes through the pinned slots; never a correctness issue
-                        self.tier_notes.append("hipHostRegister of the shm snapshot failed; pinned-slot capture")
-                    else:
-                        self._reg.append((ptr + off, ln))
-                        self._reg_done = off + ln
-                    self.prep_stats["register_s"] = round(self.prep_stats.get("register_s", 0.0) + time.time() - tr, 3)
-                off += ln
-                if REG_PAUSE_S > 0 and off < nb:
+                tr = time.time()
+                if fns[0](ptr + off, ln) != 0:
+                    self._reg_failed = True  # the rest goes through the pinned slots; never a correctness issue
+                    self.tier_notes.append("hipHostRegister of the shm snapshot failed; pinned-slot capture")
+                else:
+                    self._reg.append((ptr + off, ln))
+                    self._reg_done = off + ln
+                self.prep_stats["register_s"] = round(self.prep_stats.get("register_s", 0.0) + time.time() - tr, 3)
+                if REG_PAUSE_S > 0 and self._reg_done < nb:
                     time.sleep(REG_PAUSE_S)
             self._pinned_shm = self.cuda and self._reg_done >= nb
             return True
         finally:
             os.close(fd)
+
+    def _reserve(self, fd: int, off: int, ln: int) -> bool:
+        """posix_fallocate one piece of the snapshot file (the next unreserved one)."""
+        try:
+            os.posix_fallocate(fd, off, ln)
+        except OSError as e:
+            self.tier_notes.append(f"shm reservation of {self.snap_bytes} B failed ({e}); snapshot tier -> host memory")
+            return False
+        self._falloc_done = off + ln
+        return True
 
     def _unregister_all(self) -> None:
         if self._unreg is not None:
@@ -367,34 +387,58 @@ class AsyncCheckpointer:
 
     def _ring_capture(self, segs: List[Tuple[int, torch.Tensor]], lo: int, hi: int) -> List[int]:
         """Snapshot bytes [lo, hi) <- the device state, through RING_SLOTS pinned slots: the D2H of piece k+1..
-        runs on the checkpoint stream while _host's 16 threads copy piece k into the mapping (faulting its pages
-        in parallel) with the per-CHUNK CRC32C of the copied bytes. Blocks the calling thread; ~31 GB/s on
-        MI355X against ~9 GB/s for a plain copy into an unregistered mapping (tools/diag/r05/shm_bench.py).
-        `segs`: (snapshot byte offset, flat uint8 view of the device source). lo is CHUNK-aligned."""
+        runs on the checkpoint stream while _host's 16 threads copy piece k into the mapping with the per-CHUNK
+        CRC32C of the copied bytes. Blocks the calling thread; ~31 GB/s on MI355X into reserved pages against
+        ~9 GB/s for a plain copy into an unregistered mapping (tools/diag/r05/shm_bench.py). Pages the preparation
+        has not reserved yet are reserved by a helper thread running ahead of the copy (posix_fallocate ~19 GB/s;
+        letting the copy fault them in ran at 3.8 GB/s). `segs`: (snapshot byte offset, flat uint8 view of the
+        device source). lo is CHUNK-aligned."""
         if not self._slots:
             self._slots = [torch.empty(RING_SLOT, dtype=torch.uint8, pin_memory=True) for _ in range(RING_SLOTS)]
         crcs: List[int] = []
         pend: List[Tuple[int, int, int, Any]] = []
+        res_err: List[str] = []
+        resv = None
+        if self.mode == "shm" and self._falloc_done < hi:
+            def reserve_ahead():
+                fd = os.open(self.shm_path, os.O_RDWR)
+                try:
+                    while self._falloc_done < hi:
+                        if not self._reserve(fd, self._falloc_done, min(REG_CHUNK, hi - self._falloc_done)):
+                            res_err.append(self.tier_notes[-1])
+                            return
+                finally:
+                    os.close(fd)
+            resv = threading.Thread(target=reserve_ahead, daemon=True, name="ckpt-reserve")
+            resv.start()
 
         def drain():
             k, off, ln, ev = pend.pop(0)
+            while self._falloc_done < off + ln and not res_err:
+                time.sleep(0.0005)
+            if res_err:
+                raise RuntimeError(f"shm snapshot: {res_err[0]}")
             ev.synchronize()
             crcs.extend(_host.copy_crc32c_chunks(self._slots[k % RING_SLOTS][:ln], self._snap[off:off + ln]))
-        for k, off in enumerate(range(lo, hi, RING_SLOT)):
-            if len(pend) == RING_SLOTS:
+        try:
+            for k, off in enumerate(range(lo, hi, RING_SLOT)):
+                if len(pend) == RING_SLOTS:
+                    drain()
+                ln = min(RING_SLOT, hi - off)
+                slot = self._slots[k % RING_SLOTS]
+                with torch.cuda.stream(self._stream):
+                    for base, src in segs:
+                        a, b = max(off, base), min(off + ln, base + src.numel())
+                        if a < b:
+                            slot[a - off:b - off].copy_(src[a - base:b - base], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(self._stream)
+                pend.append((k, off, ln, ev))
+            while pend:
                 drain()
-            ln = min(RING_SLOT, hi - off)
-            slot = self._slots[k % RING_SLOTS]
-            with torch.cuda.stream(self._stream):
-                for base, src in segs:
-                    a, b = max(off, base), min(off + ln, base + src.numel())
-                    if a < b:
-                        slot[a - off:b - off].copy_(src[a - base:b - base], non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record(self._stream)
-            pend.append((k, off, ln, ev))
-        while pend:
-            drain()
+        finally:
+            if resv is not None:
+                resv.join()
         return crcs
 
     def prepare_async(self) -> None:
@@ -425,16 +469,19 @@ class AsyncCheckpointer:
         if not self.active:
             return tag
         self.engine.join_optimizer()  # an overlapped optimizer update may still be writing the state
+        self._await_moments()  # a deferred restore still reading the snapshot file this save overwrites
         if self.busy:  # previous write-out still streaming from the snapshot buffer
             self.wait()
         save_id = f"{step}.{self._restart}.{self._saves}"
         interrupted = False
         if self._prep is not None:
+            tj = time.time()
             self._prep_yield.set()  # a save is waiting: stop preparing after the current piece
             self._prep.join()
             self._prep = None
             self._prep_yield.clear()
             interrupted = True
+            self.last_ring = {"prep_join_s": round(time.time() - tj, 3)}
         if self._snap is None or (not self.prepare and self.mode == "shm" and self._falloc_done < self.snap_bytes):
             self._alloc_snapshot()
         if self.mode == "shm" and os.path.exists(self.shm_meta):
@@ -454,8 +501,7 @@ class AsyncCheckpointer:
                 tr = time.time()
                 segs = [(dst.data_ptr() - self._snap.data_ptr(), s.reshape(-1).view(torch.uint8)) for dst, s in srcs]
                 ring_crcs = (dma_end, self._ring_capture(segs, dma_end, self.snap_bytes))
-                self._falloc_done = max(self._falloc_done, self.snap_bytes)  # every page now exists
-                self.last_ring = {"bytes": self.snap_bytes - dma_end, "s": round(time.time() - tr, 3)}
+                self.last_ring.update(bytes=self.snap_bytes - dma_end, s=round(time.time() - tr, 3))
             with torch.cuda.stream(self._stream):
                 for dst, s in srcs:
                     a = dst.data_ptr() - self._snap.data_ptr()
@@ -630,6 +676,8 @@ class AsyncCheckpointer:
                            "bytes": self.snap_bytes, "crc": crcs, "algo": _host.algo(),
                            "meta": {k: v for k, v in meta.items() if k != "_module_ev"}}, f)
             os.replace(tmpm, self.shm_meta)
+            if os.path.exists(self.shm_meta + ".bad"):  # a fresh snapshot replaces one a restore found bad
+                os.unlink(self.shm_meta + ".bad")
             rec["shm_s"] = time.time() - t_cap
         if not self.disk:
             self.history.append(rec)
@@ -710,6 +758,8 @@ class AsyncCheckpointer:
 
     # ------------------------------------------------------------------ restore
     def _shm_step(self) -> int:
+        if os.path.exists(self.shm_src_meta + ".bad"):
+            return -1
         try:
             with open(self.shm_src_meta) as f:
                 m = json.load(f)
@@ -728,6 +778,7 @@ class AsyncCheckpointer:
         on any rank is rolled back on all of them (recorded in ``self.rollbacks``)."""
         self.rollbacks = []
         self.engine.join_optimizer()
+        self._await_moments()
         self.restore_stats: Dict[str, Any] = {}
         agree = _Agree(self.engine)
         auto = tag in ("auto", "latest")
@@ -831,27 +882,85 @@ class AsyncCheckpointer:
         th = threading.Thread(target=reader, daemon=True)
         tl = time.time()
         th.start()
+        # the Adam moments are needed only by the first optimizer step: with the state on the device, restore the
+        # master (and whatever shares its last piece) now, hand the moments to a background thread on a stream of
+        # its own, and let the first step's forward / backward run meanwhile (the optimizer waits: _await_moments)
+        defer = self.cuda and self.defer_moments and all(getattr(eng, s_).is_cuda for s_ in STATE)
+        split = next((i for i, (_, off, _) in enumerate(jobs) if off >= 4 * n), len(jobs)) if defer else len(jobs)
         try:
-            self._restore_pieces(jobs, q, free, slots, dsts, m, check, waited)
-        finally:
+            self._restore_pieces(jobs[:split], q, free, slots, dsts, m, check, waited)
+        except BaseException:
             stop.set()
             th.join()
+            raise
         self.restore_stats["loop_s"] = round(time.time() - tl, 2)
-        tt = time.time()
-        self.restore_stats.update(wait_read_s=round(waited[0], 2), wait_h2d_s=round(waited[1], 2),
-                                  pieces=len(jobs), piece_MiB=piece >> 20, GiB=round(end / 2 ** 30, 1))
-        if check and end % _host.CHUNK:  # the chunk straddling the fp32/bf16 boundary: verify it whole
-            tail = torch.empty(min(_host.CHUNK, m["bytes"] - (end // _host.CHUNK) * _host.CHUNK), dtype=torch.uint8)
-            c = read_slot(self.shm_src_path, tail, (end // _host.CHUNK) * _host.CHUNK)
-            if c[0] != m["crc"][end // _host.CHUNK]:
-                raise CorruptCheckpoint("shm snapshot: checksum mismatch")
-        self.restore_stats["tail_s"] = round(time.time() - tt, 2)
+
+        def finish():
+            self._restore_pieces(jobs[split:], q, free, slots, dsts, m, check, waited)
+            if check and end % _host.CHUNK:  # the chunk straddling the fp32/bf16 boundary: verify it whole
+                tail = torch.empty(min(_host.CHUNK, m["bytes"] - (end // _host.CHUNK) * _host.CHUNK),
+                                   dtype=torch.uint8)
+                c = read_slot(self.shm_src_path, tail, (end // _host.CHUNK) * _host.CHUNK)
+                if c[0] != m["crc"][end // _host.CHUNK]:
+                    raise CorruptCheckpoint("shm snapshot: checksum mismatch")
+            self.restore_stats.update(wait_read_s=round(waited[0], 2), wait_h2d_s=round(waited[1], 2),
+                                      pieces=len(jobs), piece_MiB=piece >> 20, GiB=round(end / 2 ** 30, 1))
+
+        if split < len(jobs):
+            self.restore_stats["deferred_GiB"] = round(sum(j[2] for j in jobs[split:]) / 2 ** 30, 1)
+            td = time.time()
+            stream = owned_stream(self.dev, "ckpt-restore")
+
+            def background():
+                try:
+                    with torch.cuda.stream(stream):
+                        finish()
+                        ev = torch.cuda.Event()
+                        ev.record(stream)
+                    self._moments_ev = ev
+                except BaseException as e:  # noqa: BLE001 -- re-raised by _await_moments
+                    self._moments_err = e
+                finally:
+                    stop.set()
+                    th.join()
+                    self.restore_stats["deferred_s"] = round(time.time() - td, 2)
+            self._moments_err, self._moments_ev = None, None
+            self._moments = threading.Thread(target=background, daemon=True, name="ckpt-restore-moments")
+            self._moments.start()
+            self.engine.pre_step_hooks.insert(0, self._await_moments)
+        else:
+            try:
+                finish()
+            finally:
+                stop.set()
+                th.join()
         # keep the mapping: unmapping ~90 GiB of populated page tables took ~3 s on the restore's critical
         # path, and the snapshot buffer the next save needs is this same file (_alloc_snapshot reuses it)
         self._restored_map = fmap
         eng.step_count = int(m["meta"]["global_steps"])
         self._loaded_meta = m["meta"]
         return m["meta"].get("client_state", {})
+
+    def _await_moments(self, engine=None) -> None:
+        """Join a deferred restore of the Adam moments (_load_shm): the host waits for the background thread to
+        have queued its copies, the current stream for the copies. A checksum failure there ends the run loudly
+        and marks the snapshot bad, so the relaunch falls back to an older candidate instead of this one."""
+        th = self._moments
+        if th is None:
+            return
+        th.join()
+        self._moments = None
+        if self._await_moments in self.engine.pre_step_hooks:
+            self.engine.pre_step_hooks.remove(self._await_moments)
+        if self._moments_err is not None:
+            try:
+                with open(self.shm_src_meta + ".bad", "w") as f:
+                    f.write(str(self._moments_err))
+            except OSError:
+                pass
+            raise CorruptCheckpoint(f"shm snapshot: Adam moments failed to restore: {self._moments_err}")
+        if self._moments_ev is not None:
+            torch.cuda.current_stream(self.dev).wait_event(self._moments_ev)
 
     def _restore_pieces(self, jobs, q, free, slots, dsts, m, check, waited) -> None:
         """Main-thread half of the shm restore: verify each piece the reader copied and send it to the device."""
@@ -939,13 +1048,14 @@ class AsyncCheckpointer:
 
     def discard_shm(self) -> None:
         """Drop the host-RAM snapshot tier (after a clean finish: nothing to resume)."""
-        for p in (self.shm_meta, self.shm_path):
+        for p in (self.shm_meta, self.shm_path, self.shm_meta + ".bad"):
             try:
                 os.unlink(p)
             except OSError:
                 pass
 
     def close(self, discard_shm: bool = False) -> None:
+        self._await_moments()
         self.wait()
         if self._before_optimizer_step in self.engine.pre_step_hooks:
             self.engine.pre_step_hooks.remove(self._before_optimizer_step)

@@ -283,9 +283,9 @@ class MixtralBlock(LlamaBlock):
                 for t in part:  # stashed operands freed after the flush: keep them until the side copies ran
                     t[2].record_stream(side)
                     t[3].record_stream(side)
-                # the row plan too: allocated on this stream and freed when the flush returns, its block would go to
-                # the next allocation here (the router backward's dlogits) while a lagging side stream still reads
-                # it as row indices
+                # the row plan too: allocated on this stream and freed when the flush returns, its block goes straight
+                # back to this stream's next allocation. That is ordered today only because this stream waits for
+                # the side stream's event below before returning (tests/test_engine_numerics.py scribbles over it)
                 src.record_stream(side)
             else:
                 ops_g = (transpose_multi([t[2] for t in part], src), transpose_multi([t[3] for t in part], src))

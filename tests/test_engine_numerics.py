@@ -252,31 +252,45 @@ def test_side_stream_work_is_waited_for_gpu(model):
 
 @pytest.mark.gpu
 def test_side_stream_inputs_survive_block_reuse_gpu(monkeypatch):
-    """A tensor read on a side stream must be record_stream-ed to it: otherwise, freed on the host, its block goes to
-    the next allocation of the issuing stream while the (lagging) side stream still reads it. Here the MoE dW
-    re-layout's side stream lags by ~15 ms and, right after every flush, the issuing stream grabs and scribbles over
-    every small block it can get; the trained state must stay bit-identical to an undisturbed run. (Round 5: the
-    re-layout's row plan was not recorded -- it was freed when the flush returned, and the router backward's next
-    allocations could land in it.)"""
+    """Side-stream ordering under allocator pressure: the MoE dW re-layout's side stream lags by ~15 ms and, right
+    after every flush, the issuing stream grabs the re-layout row plan's block whenever the allocator hands it out
+    again and scribbles over it; the trained state must stay bit-identical to an undisturbed run. (Round 5: with
+    the plan not record_stream-ed the block did come back at once -- 6 times in this test -- and the state still
+    matched, because the issuing stream waits for the side stream's event before the flush returns; the plan is
+    recorded now, so that ordering no longer rests on where the join sits.)"""
     from distributed_llm_training_gpu_manager_amd.models import mixtral as mx
     from distributed_llm_training_gpu_manager_amd.utils import streams
     mc = get_config("mixtral-tiny")
-    orig = mx.MixtralBlock._flush_wgrad_grouped
-    held = []
+    orig, orig_plan = mx.MixtralBlock._flush_wgrad_grouped, mx.pad_plan_multi
+    plans, held = [], []
+
+    def plan(offs, rows, *a, **k):
+        src, poff = orig_plan(offs, rows, *a, **k)
+        plans.append((src.data_ptr(), src.numel()))
+        return src, poff
 
     def scribbled(self, g, ctx=None):
+        plans.clear()
         orig(self, g, ctx)
-        for n in (64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384):
-            for _ in range(8):
-                # (segment 1, row 5): an in-range row of the re-layout's plan, so a read of a reused block gives a
-                # wrong result instead of a wild address
-                held.append(torch.full((n,), (1 << 24) | 5, dtype=torch.int32, device="cuda"))
+        # take the row plan's block if the allocator hands it out again right away (it must not while the side
+        # stream still reads it) and fill it with (segment 1, row 5): an in-range row, so a read of the reused
+        # block gives a wrong result instead of a wild address
+        for ptr, n in plans:
+            for _ in range(64):
+                t = torch.empty(n, dtype=torch.int32, device="cuda")
+                held.append(t)
+                if t.data_ptr() == ptr:
+                    t.fill_((1 << 24) | 5)
+                    reused.append(ptr)
+                    break
+    reused = []
 
     res = {}
     for disturb in (False, True):
         streams.TEST_DELAY_CYCLES["cycles"] = 30_000_000 if disturb else 0
         if disturb:
             monkeypatch.setattr(mx.MixtralBlock, "_flush_wgrad_grouped", scribbled)
+            monkeypatch.setattr(mx, "pad_plan_multi", plan)
         try:
             ec = EngineConfig(zero_stage=3, micro_batch_size=2, seq_len=64, grad_accum=3, lr=1e-3,
                               scheduler="constant", init_device="cpu")
@@ -289,8 +303,9 @@ def test_side_stream_inputs_survive_block_reuse_gpu(monkeypatch):
             res[disturb] = (eng.master.cpu(), eng.exp_avg_sq.cpu())
         finally:
             streams.TEST_DELAY_CYCLES["cycles"] = 0
+    assert plans, "the deferred expert dW re-layout did not run"
     for a, b in zip(res[False], res[True]):
-        assert torch.equal(a, b)
+        assert torch.equal(a, b), f"state differs (row-plan blocks reused: {len(reused)})"
 
 
 def test_gpt2_kept_graph_matches_activation_checkpointing_cpu():

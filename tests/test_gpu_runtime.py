@@ -75,6 +75,36 @@ def test_shm_tier_checkpoint_roundtrip(tmp_path):
     assert torch.equal(d["optimizer_state_dict"]["fp32_flat_groups"][0], want.cpu())
 
 
+def test_shm_restore_defers_moments_behind_the_first_step(tmp_path):
+    """The shm restore returns once the master is on the device; the Adam moments follow on a background
+    thread while the next step's forward / backward runs, and that step's optimizer waits for them. The
+    trained state must equal a restore that copied everything before returning."""
+    from distributed_llm_training_gpu_manager_amd.ckpt.checkpoint import AsyncCheckpointer
+
+    e = _engine()
+    t = torch.randint(0, 32768, (1, 257), device="cuda")
+    for _ in range(2):
+        e.train_step([(t[:, :-1], t[:, 1:])])
+    ck = AsyncCheckpointer(e, str(tmp_path), shm=True, disk=False)
+    ck.save(2, {"step": 2}, blocking=True)
+    ck.close()
+    out = {}
+    for defer in (False, True):
+        e2 = _engine(seed=5)
+        ck2 = AsyncCheckpointer(e2, str(tmp_path), shm=True, disk=False)
+        ck2.defer_moments = defer
+        assert ck2.load("auto")["step"] == 2 and ck2.restored_from == "shm:global_step2"
+        assert ("deferred_GiB" in ck2.restore_stats) == defer, ck2.restore_stats
+        e2.train_step([(t[:, :-1], t[:, 1:])])  # the optimizer joins the deferred copies
+        assert ck2._moments is None
+        out[defer] = [x.clone() for x in (e2.master, e2.exp_avg, e2.exp_avg_sq)]
+        ck2.close()
+        del e2, ck2
+    for a, b in zip(out[False], out[True]):
+        assert torch.equal(a, b)
+    AsyncCheckpointer(_engine(), str(tmp_path), shm=True, disk=False).close(discard_shm=True)
+
+
 def test_shm_save_before_preparation_finishes_uses_pinned_slots(tmp_path, monkeypatch):
     """An early save (a spot notice in the first steps) interrupts the background reservation / page-locking:
     the page-locked prefix goes by DMA, the rest through the pinned slots with on-the-fly CRCs; the preparation

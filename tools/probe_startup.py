@@ -131,6 +131,8 @@ def main() -> int:
             t0 = time.time()
             ck.save(s + 1, blocking=True)
             steps[-1]["save_s"] = round(time.time() - t0, 2)
+            steps[-1]["save_rec"] = {k: v for k, v in (ck.history[-1] if ck.history else {}).items()}
+            steps[-1]["prep_stats"] = dict(ck.prep_stats)
             if a.kill_after_save:
                 rec["steps"] = steps
                 print(json.dumps(rec), flush=True)
