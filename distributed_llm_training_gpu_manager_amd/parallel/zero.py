@@ -47,6 +47,7 @@ Schedule (one micro-batch)
 """
 from __future__ import annotations
 
+import collections
 import contextlib
 import math
 import time
@@ -100,6 +101,13 @@ class EngineConfig:
     max_live_parameters: Any = 1e9
     max_reuse_distance: Any = 1e9
     prefetch_bucket_size: float = 5e8
+    # host run-ahead bound for ZeRO-3 gathers: a new gathered buffer is allocated only once the compute stream has
+    # finished with the one released this many releases ago (host wait on its event). Without it the host queues
+    # gathers for dozens of layers ahead of the GPU, and the released buffers -- record_stream-ed to the collective's
+    # stream, so not reusable until that stream drains -- pile up in the caching allocator: at Llama-3-70B rank scale
+    # 283-287 GiB reserved for 187.5 GiB allocated and an OOM-retry (free everything, sync, re-malloc) every step;
+    # the first step took 10.7 s instead of 4.3 s (tools/diag/r05/resume_probe.py). 0 = unbounded.
+    gather_inflight_limit: int = 4
     live_hbm_fraction: float = 0.12
     # 'hbm' residency / W^T-cache sizing leaves at least this fraction of the device free (planner.zero3_budgets)
     hbm_headroom: float = 0.10
@@ -464,6 +472,7 @@ class ZeroEngine:
             for gi in gis:
                 self._bwd_last_visit[gi] = min(si, self._bwd_last_visit.get(gi, si))
         self._live: Dict[int, Tuple[torch.Tensor, Handle]] = {}
+        self._free_events: "collections.deque" = collections.deque()  # gathered-buffer releases (run-ahead bound)
         first_use: List[int] = []
         for _, gis in self.stages:
             first_use += [gi for gi in gis if gi not in first_use]
@@ -789,8 +798,28 @@ class ZeroEngine:
         elif g.P == 1:
             self._live[gi] = (self._shard16(g), DONE)
         else:
+            self._bound_run_ahead()
             buf = torch.empty(g.numel, dtype=self.dtype, device=self.device)
             self._live[gi] = (buf, self._all_gather(g, buf, self._shard16(g)))
+
+    def _bound_run_ahead(self) -> None:
+        """Host-wait until the compute stream is done with the gathered buffer released gather_inflight_limit
+        releases ago (cfg.gather_inflight_limit; PyTorch FSDP's all-gather rate limiter works the same way)."""
+        lim = self.cfg.gather_inflight_limit
+        if lim <= 0 or not self.is_cuda or torch.cuda.is_current_stream_capturing():
+            return
+        while len(self._free_events) >= lim:
+            self._free_events.popleft().synchronize()
+
+    def _released(self, gi: int) -> None:
+        """A gathered (all-gather-allocated) buffer left the live set: note when the compute stream is done with it."""
+        if self.stage == 3 and self.is_cuda and self.groups[gi].P > 1 and not self.param_host \
+                and self.cfg.gather_inflight_limit > 0 and not torch.cuda.is_current_stream_capturing():
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            self._free_events.append(ev)
+            while len(self._free_events) > 4 * self.cfg.gather_inflight_limit:
+                self._free_events.popleft()  # releases without new gathers (resident groups): keep the newest
 
     def _issue_gathers(self, gis) -> None:
         for gi in gis:
@@ -852,7 +881,8 @@ class ZeroEngine:
     def release(self, gis) -> None:
         if self.stage == 3:
             for gi in (gis if isinstance(gis, tuple) else (gis,)):
-                self._live.pop(gi, None)
+                if self._live.pop(gi, None) is not None:
+                    self._released(gi)
 
     # ------------------------------------------------------------------ ZeRO-3 residency
     def _build_live_plan(self) -> None:
@@ -912,7 +942,8 @@ class ZeroEngine:
         if self.stage == 3:
             for gi in gis:
                 if not self.live_plan.keep(v, gi, last_micro):
-                    self._live.pop(gi, None)
+                    if self._live.pop(gi, None) is not None:
+                        self._released(gi)
 
     def _prefetch(self, si: int, step: int) -> None:
         """Issue the all-gathers of the stages after `si` (direction `step`): at least one stage, then
