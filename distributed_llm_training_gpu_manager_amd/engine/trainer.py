@@ -131,11 +131,6 @@ class Trainer:
         self.env = init_distributed(args.device)
         self.timeline["dist_init"] = time.time()
         self.mem_notes: Dict[str, float] = {}
-        pre = getattr(sys.modules[__name__.rsplit(".", 2)[0]], "_VRAM_PREWARM", None)  # train.py's restart warm-up
-        if pre is not None:
-            tw = time.time()
-            pre.join()  # before anything measures or claims HBM
-            self.mem_notes["vram_prewarm_wait_s"] = round(time.time() - tw, 2)
         if self.env.device.type == "cuda":  # HBM still held by a killed predecessor shows up here
             self.mem_notes["gpu_free_at_start_GiB"] = round(torch.cuda.mem_get_info(self.env.device)[0] / 2 ** 30, 1)
         self.comm = Comm()
@@ -190,14 +185,7 @@ class Trainer:
         self.timeline["engine"] = time.time()
         if self.env.device.type == "cuda":
             self.mem_notes["gpu_free_after_engine_GiB"] = round(torch.cuda.mem_get_info(self.env.device)[0] / 2 ** 30, 1)
-            if save_dir:  # what a relaunch of this rank pre-allocates while it imports (train.py)
-                try:
-                    os.makedirs(save_dir, exist_ok=True)
-                    with open(os.path.join(save_dir, f".engine_vram_gib.r{self.env.rank}"), "w") as f:
-                        f.write(str(round(max(0.0, self.mem_notes["gpu_free_at_start_GiB"]
-                                              - self.mem_notes["gpu_free_after_engine_GiB"]), 1)))
-                except OSError:
-                    pass
+
         self.monitor = LossSpikeMonitor(MonitorConfig())
         self.trap = NanTrap(self.env.device, self.monitor, width=6)
         shm = {"auto": "auto", "on": True, "off": False}[args.ckpt_shm]
