@@ -28,10 +28,6 @@ std::tuple<at::Tensor, at::Tensor> dlgm_cross_entropy_(at::Tensor logits, const 
                                                        const c10::optional<at::Tensor>& scale);
 // optim.hip
 void dlgm_grad_stats(at::TensorList grads, at::Tensor out, bool accumulate);
-void dlgm_adamw_step_t_(at::Tensor p, at::Tensor m, at::Tensor v, const at::Tensor& g, at::Tensor p16,
-                        at::Tensor p16t, const c10::optional<at::Tensor>& stats, double lr, double beta1, double beta2,
-                        double eps, double weight_decay, double bc1, double bc2, double grad_scale, double max_norm,
-                        const c10::optional<at::Tensor>& scale_state, int64_t R, int64_t C);
 void dlgm_adamw_step_(at::Tensor p, at::Tensor m, at::Tensor v, const at::Tensor& g,
                       const c10::optional<at::Tensor>& p16, const c10::optional<at::Tensor>& stats, double lr,
                       double beta1, double beta2, double eps, double weight_decay, double bc1, double bc2,
@@ -113,7 +109,6 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("cross_entropy_(Tensor(a!) logits, Tensor labels, int ignore_index, float grad_scale, bool compute_grad, Tensor? scale=None) -> (Tensor, Tensor)");
   m.def("grad_stats(Tensor[] grads, Tensor(a!) out, bool accumulate) -> ()");
   m.def("adamw_step_(Tensor(a!) p, Tensor(b!) m, Tensor(c!) v, Tensor g, Tensor(d!)? p16, Tensor? stats, float lr, float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2, float grad_scale, float max_norm, Tensor? scale_state=None) -> ()");
-  m.def("adamw_step_t_(Tensor(a!) p, Tensor(b!) m, Tensor(c!) v, Tensor g, Tensor(d!) p16, Tensor(e!) p16t, Tensor? stats, float lr, float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2, float grad_scale, float max_norm, Tensor? scale_state, int R, int C) -> ()");
   m.def("loss_scale_update_(Tensor(a!) state, Tensor stats, int window, int hysteresis, float min_scale) -> ()");
   m.def("accumulate_(Tensor(a!) dst, Tensor src, float alpha, float beta) -> ()");
   m.def("cast_f32_bf16_(Tensor(a!) dst, Tensor src) -> ()");
@@ -159,7 +154,6 @@ TORCH_LIBRARY_IMPL(dlgm, CUDA, m) {
   m.impl("cross_entropy_", &dlgm_cross_entropy_);
   m.impl("grad_stats", &dlgm_grad_stats);
   m.impl("adamw_step_", &dlgm_adamw_step_);
-  m.impl("adamw_step_t_", &dlgm_adamw_step_t_);
   m.impl("loss_scale_update_", &dlgm_loss_scale_update_);
   m.impl("accumulate_", &dlgm_accumulate_);
   m.impl("cast_f32_bf16_", &dlgm_cast_f32_bf16_);

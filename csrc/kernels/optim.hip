@@ -197,59 +197,6 @@ __global__ __launch_bounds__(kThreads) void adamw_kernel(float* __restrict__ p, 
     }
 }
 
-// AdamW over a stack of E row-major [R, C] weights (fp32 master / moments / gradient) that ALSO writes the
-// transposed 16-bit copy [E, C, R] the input-gradient GEMMs read (the engine's W^T cache, ZeroEngine._transposed):
-// the separate transpose pass after the step re-read the whole 16-bit copy (2 B/param) and, for the Mixtral experts,
-// ran as 32 launches beside the next forward. One 64 x 64 tile per workgroup: the update streams row-major exactly
-// as adamw_kernel does (adam4), the 16-bit tile goes through LDS, and the transposed tile leaves as whole 128-B rows.
-template <typename PT>
-__global__ __launch_bounds__(kThreads) void adamw_t_kernel(float* __restrict__ p, float* __restrict__ m,
-                                                           float* __restrict__ v, const float* __restrict__ g,
-                                                           PT* __restrict__ p16, PT* __restrict__ p16t,
-                                                           const float* __restrict__ stats,
-                                                           const float* __restrict__ inv_scale, int R, int C,
-                                                           AdamHyper h) {
-  __shared__ PT tile[64][64 + 8];  // +8: the column reads of the transposed store spread over the banks
-  bool skip;
-  const float gc = clip_coef(stats, inv_scale, h, skip);
-  if (skip) return;
-  const float decay = 1.f - h.lr * h.wd;
-  const float step_size = h.lr / h.bc1;
-  const float inv_sqrt_bc2 = rsqrtf(h.bc2);
-  const int c0 = blockIdx.x * 64, r0 = blockIdx.y * 64;
-  const int64_t eoff = (int64_t)blockIdx.z * R * C;
-  const int t = threadIdx.x, tc = (t & 15) * 4, tr = t >> 4;  // 16 threads x 4 columns per row, 16 rows per pass
-#pragma unroll
-  for (int pass = 0; pass < 4; ++pass) {
-    const int r = pass * 16 + tr;
-    const int64_t i = eoff + (int64_t)(r0 + r) * C + c0 + tc;
-    f32x4 pp = ld_vec<true>(reinterpret_cast<const f32x4*>(p + i));
-    f32x4 mm = ld_vec<true>(reinterpret_cast<const f32x4*>(m + i));
-    f32x4 vv = ld_vec<true>(reinterpret_cast<const f32x4*>(v + i));
-    float gg[4];
-    load4<float, true>(g + i, gg);
-    adam4(pp, mm, vv, gg, gc, decay, step_size, inv_sqrt_bc2, h);
-    st_stream<true>(reinterpret_cast<f32x4*>(p + i), pp);
-    st_stream<true>(reinterpret_cast<f32x4*>(m + i), mm);
-    st_stream<true>(reinterpret_cast<f32x4*>(v + i), vv);
-    const vec4_t<PT> q = __builtin_convertvector(pp, vec4_t<PT>);
-    st_stream<true>(reinterpret_cast<vec4_t<PT>*>(p16 + i), q);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) tile[r][tc + j] = q[j];
-  }
-  __syncthreads();
-  // transposed tile: output row c (= input column) holds the tile's 64 rows; 8 threads x 8 elements per row
-  const int oc = t >> 3, orr = (t & 7) * 8;
-#pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    const int c = pass * 32 + oc;
-    vec8_t<PT> o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = tile[orr + j][c];
-    *reinterpret_cast<vec8_t<PT>*>(p16t + eoff + (int64_t)(c0 + c) * R + r0 + orr) = o;
-  }
-}
-
 template <typename ST>
 __global__ __launch_bounds__(kThreads) void accumulate_kernel(float* __restrict__ dst, const ST* __restrict__ src,
                                                               int64_t n, float alpha, float beta) {
@@ -386,45 +333,6 @@ void dlgm_adamw_step_(at::Tensor p, at::Tensor m, at::Tensor v, const at::Tensor
                                                 reinterpret_cast<const GT*>(g.data_ptr()), p16p, sp, inv, n, h));
     }
   });
-  DLGM_CHECK_HIP(hipGetLastError());
-}
-
-// p, m, v, g: E*R*C fp32 (flat row-major [E, R, C] slices of the optimizer partition); p16: the 16-bit copy of
-// the same elements; p16t: [E, C, R] (the W^T cache). R and C multiples of 64.
-void dlgm_adamw_step_t_(at::Tensor p, at::Tensor m, at::Tensor v, const at::Tensor& g, at::Tensor p16,
-                        at::Tensor p16t, const c10::optional<at::Tensor>& stats, double lr, double beta1, double beta2,
-                        double eps, double weight_decay, double bc1, double bc2, double grad_scale, double max_norm,
-                        const c10::optional<at::Tensor>& scale_state, int64_t R, int64_t C) {
-  check_flat(p, "param");
-  check_flat(m, "exp_avg");
-  check_flat(v, "exp_avg_sq");
-  check_flat(g, "grad");
-  check_flat(p16, "param_16");
-  check_flat(p16t, "param_16_t");
-  TORCH_CHECK(p.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat &&
-                  g.scalar_type() == at::kFloat, "adamw_t: master / state / gradient must be fp32");
-  TORCH_CHECK(DLGM_IS16(p16) && p16t.scalar_type() == p16.scalar_type(), "adamw_t: bad 16-bit copies");
-  const int64_t n = p.numel();
-  TORCH_CHECK(R > 0 && C > 0 && R % 64 == 0 && C % 64 == 0 && n % (R * C) == 0, "adamw_t: shape must tile by 64");
-  TORCH_CHECK(m.numel() == n && v.numel() == n && g.numel() == n && p16.numel() == n && p16t.numel() == n,
-              "adamw_t: size mismatch");
-  const int64_t E = n / (R * C);
-  TORCH_CHECK(C / 64 <= INT32_MAX && R / 64 <= 65535 && E <= 65535, "adamw_t: grid too large");
-  const float* sp = nullptr;
-  if (stats.has_value() && stats->defined()) {
-    TORCH_CHECK(stats->scalar_type() == at::kFloat && stats->numel() >= 2 && stats->is_cuda(), "adamw_t: bad stats");
-    sp = stats->data_ptr<float>();
-  }
-  const float* inv = nullptr;
-  if (scale_state.has_value() && scale_state->defined()) inv = scale_state->data_ptr<float>() + 1;
-  AdamHyper h{(float)lr, (float)beta1, (float)beta2, (float)eps, (float)weight_decay, (float)bc1, (float)bc2,
-              (float)grad_scale, (float)max_norm};
-  auto stream = c10::hip::getCurrentHIPStream();
-  const dim3 grid((unsigned)(C / 64), (unsigned)(R / 64), (unsigned)E);
-  DLGM_DISPATCH_16(p16.scalar_type(), PT, adamw_t_kernel<PT><<<grid, kThreads, 0, stream>>>(
-                                            p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
-                                            g.data_ptr<float>(), reinterpret_cast<PT*>(p16.data_ptr()),
-                                            reinterpret_cast<PT*>(p16t.data_ptr()), sp, inv, (int)R, (int)C, h));
   DLGM_CHECK_HIP(hipGetLastError());
 }
 

@@ -65,24 +65,6 @@ def adamw_step_(p: torch.Tensor, m: torch.Tensor, v: torch.Tensor, g: torch.Tens
         p16.copy_(p.to(p16.dtype))
 
 
-def adamw_step_t_(p: torch.Tensor, m: torch.Tensor, v: torch.Tensor, g: torch.Tensor, p16: torch.Tensor,
-                  p16t: torch.Tensor, stats: Optional[torch.Tensor], R: int, C: int, *, lr: float, beta1: float,
-                  beta2: float, eps: float, weight_decay: float, step: int, grad_scale: float = 1.0,
-                  max_norm: float = 0.0, scale_state: Optional[torch.Tensor] = None) -> None:
-    """:func:`adamw_step_` over E stacked row-major [R, C] weights that also writes their transposed 16-bit copy
-    p16t = [E, C, R] (csrc/kernels/optim.hip adamw_t_kernel; R, C multiples of 64). Same bits as adamw_step_
-    followed by a transpose."""
-    bc1 = 1.0 - beta1 ** step
-    bc2 = 1.0 - beta2 ** step
-    if use_native(p):
-        hip_ops().adamw_step_t_(p, m, v, g, p16, p16t, stats, lr, beta1, beta2, eps, weight_decay, bc1, bc2,
-                                grad_scale, max_norm, scale_state, R, C)
-        return
-    adamw_step_(p, m, v, g, p16, stats, lr=lr, beta1=beta1, beta2=beta2, eps=eps, weight_decay=weight_decay,
-                step=step, grad_scale=grad_scale, max_norm=max_norm, scale_state=scale_state)
-    p16t.view(-1, C, R).copy_(p16.view(-1, R, C).transpose(1, 2))
-
-
 def accumulate_(dst: torch.Tensor, src: torch.Tensor, alpha: float = 1.0, beta: float = 1.0) -> None:
     """dst(fp32) = beta * dst + alpha * src."""
     if use_native(dst):

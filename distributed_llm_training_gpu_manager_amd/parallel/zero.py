@@ -183,10 +183,6 @@ class EngineConfig:
     # W^T cache also for expert-stacked [E, out, in] weights of never-gathered groups (expert dX GEMMs read
     # K-contiguous weights), within tcache_hbm_fraction of the device
     expert_weight_cache: bool = True
-    # the optimizer writes the W^T cache of unpartitioned (P == 1) groups itself (ops.adamw_step_t_: the same bits
-    # as AdamW + a transpose pass, without re-reading the 16-bit copy or the 32 per-expert transposes that ran
-    # beside the next forward)
-    fused_optimizer_transpose: bool = True
     init_device: str = "auto"  # "cpu" gives bit-identical init on any device (tests); auto: cpu below 1e9 params
     # replay the GA micro-batches of a step (forward + backward + gradient accumulation) as ONE captured
     # HIP graph: one launch instead of ~30 kernel launches per layer per micro-batch, for models whose
@@ -1242,7 +1238,6 @@ class ZeroEngine:
         return out
 
     def _optimizer_step(self) -> Dict[str, Any]:
-        self._fused_groups = ()  # set by _fused_transposes on the path that writes the caches
         for hk in self.pre_step_hooks:
             hk(self)
         if self.param_nvme is not None:  # the partition file changes below: read-aheads in flight are stale
@@ -1262,33 +1257,15 @@ class ZeroEngine:
             if self._opt_overlap_ok():
                 self._adamw_overlapped(lr, sst)
             else:
-                kw = dict(lr=lr, beta1=cfg.betas[0], beta2=cfg.betas[1], eps=cfg.eps, weight_decay=cfg.weight_decay,
-                          step=self.step_count, grad_scale=1.0, max_norm=cfg.grad_clip, scale_state=sst)
-                fused = self._fused_transposes()
-                if not fused:
-                    ops.adamw_step_(self.master, self.exp_avg, self.exp_avg_sq, self.grad_shard,
-                                    None if self.param_host else self.p16_shard, self.stats, **kw)
-                else:
-                    st = lambda t, a, n: t.narrow(0, a, n)  # noqa: E731
-                    pos = 0
-                    for off, numel, R, C, dst in fused + [(self.shard_total, 0, 0, 0, None)]:
-                        if off > pos:  # the elements between fused weights: the flat kernel
-                            ops.adamw_step_(st(self.master, pos, off - pos), st(self.exp_avg, pos, off - pos),
-                                            st(self.exp_avg_sq, pos, off - pos), st(self.grad_shard, pos, off - pos),
-                                            st(self.p16_shard, pos, off - pos), self.stats, **kw)
-                        if dst is not None:
-                            ops.adamw_step_t_(st(self.master, off, numel), st(self.exp_avg, off, numel),
-                                              st(self.exp_avg_sq, off, numel), st(self.grad_shard, off, numel),
-                                              st(self.p16_shard, off, numel), dst.view(-1), self.stats, R, C, **kw)
-                        pos = max(pos, off + numel)
+                ops.adamw_step_(self.master, self.exp_avg, self.exp_avg_sq, self.grad_shard,
+                                None if self.param_host else self.p16_shard,
+                                self.stats, lr=lr,
+                                beta1=cfg.betas[0], beta2=cfg.betas[1], eps=cfg.eps, weight_decay=cfg.weight_decay,
+                                step=self.step_count, grad_scale=1.0, max_norm=cfg.grad_clip, scale_state=sst)
             if self.param_host:
                 self._p16_to_host()
             self._mesh_publish()
         self._pver += 1  # the compute copy changes below: transposed caches are stale
-        for gi in getattr(self, "_fused_groups", ()):  # ... except those the optimizer just rewrote itself
-            ver, cache = self._tcache[gi]
-            self._tcache[gi] = (self._pver, cache)
-        self._fused_groups = ()
         if self.stage == 3:
             self._live.clear()  # (micro_step(last=True) already dropped them; direct callers may not have)
         if self.stage in (1, 2):
@@ -1300,35 +1277,6 @@ class ZeroEngine:
         if self.scaler is not None:
             self.scaler.update_(self.stats)
         return {"lr": lr, "stats": self.stats}
-
-    def _fused_transposes(self) -> List[Tuple[int, int, int, int, torch.Tensor]]:
-        """(shard offset, numel, R, C, cache tensor) of every W^T-cached weight whose transposed copy the optimizer
-        can write itself (cfg.fused_optimizer_transpose): groups of P == 1 (the shard IS the group), caches already
-        built and current, shapes that tile by 64 -- in shard order. Also remembers the groups for _optimizer_step."""
-        self._fused_groups = ()
-        c = self.cfg
-        if not (c.fused_optimizer_transpose and self.is_cuda and self.stage == 3 and not self.param_host
-                and self.mesh is None and self.offload is None):
-            return []
-        out, groups = [], []
-        for gi, names in self._tnames.items():
-            g = self.groups[gi]
-            ver, cache = self._tcache.get(gi, (-1, None))
-            if g.P != 1 or cache is None or ver != self._pver or gi in self._tcache_ev:
-                continue
-            items = []
-            for n, shp in names:
-                R, C = shp[-2], shp[-1]
-                if R % 64 or C % 64 or n not in cache:
-                    items = []
-                    break
-                items.append((g.shard_off + g.layout[n][0], math.prod(shp), R, C, cache[n]))
-            if items:
-                out += items
-                groups.append(gi)
-        out.sort(key=lambda x: x[0])
-        self._fused_groups = tuple(groups)
-        return out
 
     def _opt_overlap_ok(self) -> bool:
         return (self.cfg.optimizer_overlap and self.is_cuda and self.stage == 3 and self.offload is None

@@ -308,29 +308,6 @@ def test_side_stream_inputs_survive_block_reuse_gpu(monkeypatch):
         assert torch.equal(a, b), f"state differs (row-plan blocks reused: {len(reused)})"
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("model", ["llama-tiny", "mixtral-tiny"])
-def test_fused_optimizer_transpose_is_bit_identical_gpu(model):
-    """cfg.fused_optimizer_transpose: AdamW writes the W^T cache of the unpartitioned groups itself (dense 2-D
-    weights and the Mixtral expert stacks); training is bit-identical to AdamW + the separate transpose pass."""
-    mc = get_config(model)
-    res = {}
-    for fused in (False, True):
-        ec = EngineConfig(zero_stage=3, micro_batch_size=2, seq_len=64, grad_accum=2, lr=1e-3,
-                          scheduler="constant", init_device="cpu", fused_optimizer_transpose=fused)
-        eng = ZeroEngine(mc, ec, torch.device("cuda"))
-        g = torch.Generator().manual_seed(23)
-        n_fused = 0
-        for _ in range(4):
-            toks = [torch.randint(0, mc.vocab_size, (2, 65), generator=g) for _ in range(2)]
-            eng.train_step([(t[:, :-1].cuda(), t[:, 1:].cuda()) for t in toks])
-            n_fused = max(n_fused, len(eng._fused_transposes()))
-        assert (n_fused > 0) == fused, n_fused
-        res[fused] = [getattr(eng, k).cpu() for k in ("master", "exp_avg", "exp_avg_sq", "p16_shard")]
-    for a, b in zip(res[False], res[True]):
-        assert torch.equal(a, b)
-
-
 def test_gpt2_kept_graph_matches_activation_checkpointing_cpu():
     """GPT-2 blocks keep their forward autograd graph; with activation checkpointing the engine re-runs
     the block right before its backward instead. Both must train identically."""

@@ -133,42 +133,6 @@ def test_grad_stats_and_adamw():
     assert torch.equal(pg, before)
 
 
-@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
-def test_adamw_with_transposed_copy_is_flat_adamw_plus_transpose(dt):
-    """ops.adamw_step_t_ (one tiled launch that also writes the [E, C, R] W^T copy) == the flat AdamW kernel followed
-    by a transpose, bit for bit, for a stack of experts; the fp32 reference within rounding; an overflow skips it."""
-    torch.manual_seed(1)
-    E, R, C = 3, 192, 320
-    n = E * R * C
-    p = torch.randn(n, device=DEV)
-    m = torch.randn(n, device=DEV).abs() * 0.01
-    v = torch.rand(n, device=DEV) * 0.01
-    gr = torch.randn(n, device=DEV)
-    st = torch.zeros(2, device=DEV)
-    ops.grad_stats([gr], st)
-    kw = dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.01, step=5, max_norm=1.0)
-    a = [t.clone() for t in (p, m, v)]
-    a16 = torch.empty(n, dtype=dt, device=DEV)
-    ops.adamw_step_(a[0], a[1], a[2], gr, a16, st, **kw)
-    b = [t.clone() for t in (p, m, v)]
-    b16 = torch.empty(n, dtype=dt, device=DEV)
-    b16t = torch.empty(n, dtype=dt, device=DEV)
-    ops.adamw_step_t_(b[0], b[1], b[2], gr, b16, b16t, st, R, C, **kw)
-    for x, y in zip(a + [a16], b + [b16]):
-        assert torch.equal(x, y)
-    assert torch.equal(b16t.view(E, C, R), a16.view(E, R, C).transpose(1, 2))
-    pr = p.cpu().clone()
-    ops.adamw_step_(pr, m.cpu().clone(), v.cpu().clone(), gr.cpu(), None, st.cpu(), **kw)
-    assert rel_err(b[0], pr) < 1e-5
-    gbad = gr.clone()
-    gbad[77] = float("nan")
-    st2 = torch.zeros(2, device=DEV)
-    ops.grad_stats([gbad], st2)
-    before = b[0].clone()
-    ops.adamw_step_t_(b[0], b[1], b[2], gbad, b16, b16t, st2, R, C, **kw)
-    assert torch.equal(b[0], before)
-
-
 def test_accumulate_and_cast():
     src = torch.randn(4099, dtype=torch.bfloat16, device=DEV)
     dst = torch.ones(4099, device=DEV)
