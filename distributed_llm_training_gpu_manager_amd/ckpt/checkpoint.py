@@ -298,18 +298,23 @@ class AsyncCheckpointer:
         return (lambda p_, n_: int(reg(p_, n_, 0))), (lambda p_: int(unreg(p_)))
 
     def _prepare_shm(self, nb: int) -> bool:
-        """Reserve (posix_fallocate: a full tmpfs is an error here, not a SIGBUS in the middle of a snapshot copy)
-        and page-lock the mapped snapshot file piece by piece, REG_CHUNK bytes at a time, front to back, with a
-        short pause between pieces. One hipHostRegister of a whole ~112 GB file holds the HIP runtime for ~6 s
-        and every kernel launch of the training thread waits meanwhile (MI355X: the first step after a restore
-        took 6.4 s instead of 0.9 s); pieces with a pause let the training thread launch between them.
+        """Make the mapped snapshot file ready for a DMA capture, in two passes of REG_CHUNK pieces, front to back:
 
-        The prepared prefix [0, _reg_done) is what a save copies by DMA at ~57 GB/s; a save that arrives first
+        1. reserve every page (posix_fallocate: a full tmpfs is an error here, not a SIGBUS in the middle of a
+           snapshot copy). ~19 GB/s on the MI355X host, pure kernel work that touches no HIP state; faulting the
+           pages in instead (first-touch writes or MADV_POPULATE_WRITE, 16 threads) ran at 3.8 GB/s
+           (tools/diag/r05/prefault_bench.py). Done first, so an early save finds the file allocated.
+        2. page-lock it (hipHostRegister) with a short pause between pieces: one registration of a whole ~112 GB
+           file holds the HIP runtime for ~6 s and every kernel launch of the training thread waits meanwhile
+           (MI355X: the first step after a restore took 6.4 s instead of 0.9 s).
+
+        The page-locked prefix [0, _reg_done) is what a save copies by DMA at ~57 GB/s; a save that arrives first
         (an early spot notice) sets _prep_yield, this loop stops after its current piece, the save streams the
-        rest through pinned slots (_ring_capture) and restarts the preparation afterwards. Returns False when
-        the reservation failed (the caller falls back to the host tier). Measured on MI355X (Mixtral EP = 8 rank, 81.7
-        GB, a spot notice at step 3): this interleaved order gave a 3.4 s emergency checkpoint; reserving the whole
-        file first and page-locking after, with the slot copy reserving ahead of itself, gave 6.5 s."""
+        rest through pinned slots (_ring_capture, reserving what pass 1 has not reached yet just ahead of the
+        copy) and restarts the preparation afterwards. Returns False when the reservation failed (the caller falls
+        back to the host tier). Measured on MI355X (Mixtral EP = 8 rank, 81.7 GB, spot notice at step 3, before the
+        preparation finished): emergency checkpoints of 3.4 s and 6.5 s in two runs with this order; 15.6 s with
+        reserve + page-lock interleaved per piece and the slot copy faulting the unreserved pages itself."""
         fd = os.open(self.shm_path, os.O_RDWR)
         ptr = self._snap.data_ptr()
         fns = self._hip_register_fns() if self.cuda else None
@@ -318,38 +323,49 @@ class AsyncCheckpointer:
             fns = (lambda p_, n_: int(cr.cudaHostRegister(p_, n_, 0))), (lambda p_: int(cr.cudaHostUnregister(p_)))
         if fns is not None:
             self._unreg = fns[1]
+
+        def stopped() -> bool:
+            return self._prep_yield.is_set() or self._reg_stop.is_set()
         try:
-            off = min(self._falloc_done, self._reg_done if (self.cuda and not self._reg_failed) else nb)
-            while off < nb:
-                if self._prep_yield.is_set() or self._reg_stop.is_set():
+            while self._falloc_done < nb:
+                if stopped():
                     return True
+                off = self._falloc_done
+                tf = time.time()
+                if not self._reserve(fd, off, min(REG_CHUNK, nb - off)):
+                    self._unregister_all()
+                    return False
+                self.prep_stats["fallocate_s"] = round(self.prep_stats.get("fallocate_s", 0.0) + time.time() - tf, 3)
+            self.prep_stats.setdefault("reserved_at", time.time())
+            while fns is not None and not self._reg_failed and self._reg_done < nb:
+                if stopped():
+                    return True
+                off = self._reg_done
                 ln = min(REG_CHUNK, nb - off)
-                if self._falloc_done <= off:
-                    tf = time.time()
-                    try:
-                        os.posix_fallocate(fd, off, ln)
-                    except OSError as e:
-                        self.tier_notes.append(f"shm reservation of {nb} B failed ({e}); snapshot tier -> host memory")
-                        self._unregister_all()
-                        return False
-                    self._falloc_done = off + ln
-                    self.prep_stats["fallocate_s"] = round(self.prep_stats.get("fallocate_s", 0.0) + time.time() - tf, 3)
-                if fns is not None and not self._reg_failed and self._reg_done <= off:
-                    tr = time.time()
-                    if fns[0](ptr + off, ln) != 0:
-                        self._reg_failed = True  # the rest goes through the pinned slots; never a correctness issue
-                        self.tier_notes.append("hipHostRegister of the shm snapshot failed; pinned-slot capture")
-                    else:
-                        self._reg.append((ptr + off, ln))
-                        self._reg_done = off + ln
-                    self.prep_stats["register_s"] = round(self.prep_stats.get("register_s", 0.0) + time.time() - tr, 3)
-                off += ln
-                if REG_PAUSE_S > 0 and off < nb:
+                tr = time.time()
+                if fns[0](ptr + off, ln) != 0:
+                    self._reg_failed = True  # the rest goes through the pinned slots; never a correctness issue
+                    self.tier_notes.append("hipHostRegister of the shm snapshot failed; pinned-slot capture")
+                else:
+                    self._reg.append((ptr + off, ln))
+                    self._reg_done = off + ln
+                self.prep_stats["register_s"] = round(self.prep_stats.get("register_s", 0.0) + time.time() - tr, 3)
+                if REG_PAUSE_S > 0 and self._reg_done < nb:
                     time.sleep(REG_PAUSE_S)
             self._pinned_shm = self.cuda and self._reg_done >= nb
             return True
         finally:
             os.close(fd)
+
+    def _reserve(self, fd: int, off: int, ln: int) -> bool:
+        """posix_fallocate one piece of the snapshot file (the next unreserved one)."""
+        try:
+            os.posix_fallocate(fd, off, ln)
+        except OSError as e:
+            self.tier_notes.append(f"shm reservation of {self.snap_bytes} B failed ({e}); snapshot tier -> host memory")
+            return False
+        self._falloc_done = off + ln
+        return True
 
     def _unregister_all(self) -> None:
         if self._unreg is not None:
@@ -373,34 +389,58 @@ class AsyncCheckpointer:
 
     def _ring_capture(self, segs: List[Tuple[int, torch.Tensor]], lo: int, hi: int) -> List[int]:
         """Snapshot bytes [lo, hi) <- the device state, through RING_SLOTS pinned slots: the D2H of piece k+1..
-        runs on the checkpoint stream while _host's 16 threads copy piece k into the mapping (faulting its pages
-        in parallel) with the per-CHUNK CRC32C of the copied bytes. Blocks the calling thread; ~31 GB/s on
-        MI355X against ~9 GB/s for a plain copy into an unregistered mapping (tools/diag/r05/shm_bench.py).
-        `segs`: (snapshot byte offset, flat uint8 view of the device source). lo is CHUNK-aligned."""
+        runs on the checkpoint stream while _host's 16 threads copy piece k into the mapping with the per-CHUNK
+        CRC32C of the copied bytes. Blocks the calling thread; ~31 GB/s on MI355X into reserved pages against
+        ~9 GB/s for a plain copy into an unregistered mapping (tools/diag/r05/shm_bench.py). Pages the preparation
+        has not reserved yet are reserved by a helper thread running ahead of the copy (posix_fallocate ~19 GB/s;
+        letting the copy fault them in ran at 3.8 GB/s). `segs`: (snapshot byte offset, flat uint8 view of the
+        device source). lo is CHUNK-aligned."""
         if not self._slots:
             self._slots = [torch.empty(RING_SLOT, dtype=torch.uint8, pin_memory=True) for _ in range(RING_SLOTS)]
         crcs: List[int] = []
         pend: List[Tuple[int, int, int, Any]] = []
+        res_err: List[str] = []
+        resv = None
+        if self.mode == "shm" and self._falloc_done < hi:
+            def reserve_ahead():
+                fd = os.open(self.shm_path, os.O_RDWR)
+                try:
+                    while self._falloc_done < hi:
+                        if not self._reserve(fd, self._falloc_done, min(REG_CHUNK, hi - self._falloc_done)):
+                            res_err.append(self.tier_notes[-1])
+                            return
+                finally:
+                    os.close(fd)
+            resv = threading.Thread(target=reserve_ahead, daemon=True, name="ckpt-reserve")
+            resv.start()
 
         def drain():
             k, off, ln, ev = pend.pop(0)
+            while self._falloc_done < off + ln and not res_err:
+                time.sleep(0.0005)
+            if res_err:
+                raise RuntimeError(f"shm snapshot: {res_err[0]}")
             ev.synchronize()
             crcs.extend(_host.copy_crc32c_chunks(self._slots[k % RING_SLOTS][:ln], self._snap[off:off + ln]))
-        for k, off in enumerate(range(lo, hi, RING_SLOT)):
-            if len(pend) == RING_SLOTS:
+        try:
+            for k, off in enumerate(range(lo, hi, RING_SLOT)):
+                if len(pend) == RING_SLOTS:
+                    drain()
+                ln = min(RING_SLOT, hi - off)
+                slot = self._slots[k % RING_SLOTS]
+                with torch.cuda.stream(self._stream):
+                    for base, src in segs:
+                        a, b = max(off, base), min(off + ln, base + src.numel())
+                        if a < b:
+                            slot[a - off:b - off].copy_(src[a - base:b - base], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(self._stream)
+                pend.append((k, off, ln, ev))
+            while pend:
                 drain()
-            ln = min(RING_SLOT, hi - off)
-            slot = self._slots[k % RING_SLOTS]
-            with torch.cuda.stream(self._stream):
-                for base, src in segs:
-                    a, b = max(off, base), min(off + ln, base + src.numel())
-                    if a < b:
-                        slot[a - off:b - off].copy_(src[a - base:b - base], non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record(self._stream)
-            pend.append((k, off, ln, ev))
-        while pend:
-            drain()
+        finally:
+            if resv is not None:
+                resv.join()
         return crcs
 
     def prepare_async(self) -> None:
@@ -463,7 +503,6 @@ class AsyncCheckpointer:
                 tr = time.time()
                 segs = [(dst.data_ptr() - self._snap.data_ptr(), s.reshape(-1).view(torch.uint8)) for dst, s in srcs]
                 ring_crcs = (dma_end, self._ring_capture(segs, dma_end, self.snap_bytes))
-                self._falloc_done = max(self._falloc_done, self.snap_bytes)  # the copy allocated every page
                 self.last_ring.update(bytes=self.snap_bytes - dma_end, s=round(time.time() - tr, 3))
             with torch.cuda.stream(self._stream):
                 for dst, s in srcs:
