@@ -310,6 +310,8 @@ class Trainer:
                 self.ckpt.save(last_issued, client_state={"step": last_issued, "preempted": True,
                                                                  "global_batch": self.global_batch}, blocking=True)
             self._say(f"preemption: emergency checkpoint at step {last_issued} in {time.time() - t0:.2f}s; exiting")
+            if self.ckpt is not None and self.ckpt.history:
+                self._say("emergency checkpoint record: " + json.dumps(json_safe(self.ckpt.history[-1])))
             return EXIT_PREEMPTED
         return None
 
@@ -423,6 +425,8 @@ class Trainer:
                     self.ckpt.save(step, client_state={"step": step, "preempted": True,
                                                           "global_batch": self.global_batch}, blocking=True)
                 self._say(f"preemption: emergency checkpoint at step {step} in {time.time() - t0:.2f}s; exiting")
+                if self.ckpt is not None and self.ckpt.history:
+                    self._say("emergency checkpoint record: " + json.dumps(json_safe(self.ckpt.history[-1])))
                 rc = EXIT_PREEMPTED
                 break
         if prev is not None and rc == 0:

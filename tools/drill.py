@@ -97,6 +97,7 @@ def drill_spot(a, work):
     stats = re.findall(r"restore (\{.*?\})\)", out2)
     return {"drill": "spot", "restore_breakdown": [json.loads(x) for x in stats], "exit_code_preempted": rc,
             "emergency_ckpt": em, "restore_exit": rc2,
+            "emergency_record": [json.loads(x) for x in re.findall(r"emergency checkpoint record: (\{.*?\})\n", out)],
             "memory": [json.loads(x) for x in re.findall(r"memory: (\{.*?\})", out + out2)],
             "ckpt_prepare": [json.loads(x) for x in re.findall(r"ckpt prepare: (\{.*?\})", out + out2)],
             "restore": res, "restored_from": via, "restore_process_wall_s": round(dt2, 2),

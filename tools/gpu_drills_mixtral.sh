@@ -8,7 +8,7 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 rm -f /dev/shm/dlgm-ckpt-* 2>/dev/null
 timeout -k 10 1050 python -u tools/drill.py --model mixtral-8x7b --seq ${SEQ:-4096} --ga 1 --k 3 --save-interval 2 \
-    --steps-after 1 --drills spot,sigkill --timeout 480 --keep-last 1 --ckpt-shm on --ckpt-disk 0 \
+    --steps-after 1 --drills ${DRILLS:-spot,sigkill} --timeout 480 --keep-last 1 --ckpt-shm on --ckpt-disk 0 \
     --extra "--expert-parallel 8 --shadow-world 8 --shadow-rank 0 --xgmi-mesh on --telemetry-interval 0" \
     --out gpurun_out/drills_mixtral_8x7b_ep8_shadow_${TAG:-r05}.json > gpurun_out/drills_mixtral.log 2>&1
 rc=$?
