@@ -105,10 +105,12 @@ def test_shm_restore_defers_moments_behind_the_first_step(tmp_path):
     AsyncCheckpointer(_engine(), str(tmp_path), shm=True, disk=False).close(discard_shm=True)
 
 
-def test_shm_save_before_preparation_finishes_uses_pinned_slots(tmp_path, monkeypatch):
-    """An early save (a spot notice in the first steps) interrupts the background reservation / page-locking:
-    the page-locked prefix goes by DMA, the rest through the pinned slots with on-the-fly CRCs; the preparation
-    resumes afterwards, the snapshot restores bit-exactly and a later save is all-DMA."""
+@pytest.mark.parametrize("register_fails", [False, True])
+def test_shm_save_before_preparation_finishes(tmp_path, monkeypatch, register_fails):
+    """An early save (a spot notice in the first steps) interrupts the background reservation / page-locking: the
+    page-locked prefix goes by DMA and the save page-locks the rest itself, piece by piece, each piece's DMA queued
+    as soon as it is locked; when page-locking fails, the rest goes through the pinned slots with on-the-fly CRCs.
+    The snapshot holds the state (CRCs agree with a full recomputation), a later save works, and it restores."""
     from distributed_llm_training_gpu_manager_amd.ckpt import checkpoint as C
 
     monkeypatch.setattr(C, "REG_CHUNK", 64 << 20)
@@ -120,9 +122,16 @@ def test_shm_save_before_preparation_finishes_uses_pinned_slots(tmp_path, monkey
     assert ck.mode == "shm" and ck.snap_bytes > 4 * (64 << 20)
     ck.prepare_async()
     time.sleep(0.12)  # a few pieces prepared, most not
+    if register_fails:  # what is not page-locked yet can no longer be
+        fns = ck._hip_register_fns()
+        monkeypatch.setattr(ck, "_hip_register_fns", lambda: ((lambda p_, n_: 1), fns[1]))
     ck.save(1, {"step": 1}, blocking=True)
     rec = ck.history[-1]
-    assert "ring" in rec and 0 < rec["ring"]["bytes"] < ck.snap_bytes, rec
+    assert "ring" in rec, rec
+    if register_fails:
+        assert 0 < rec["ring"]["bytes"] < ck.snap_bytes and rec["ring"]["locked_bytes"] == 0, rec
+    else:
+        assert rec["ring"]["locked_bytes"] > 0 and "bytes" not in rec["ring"] and ck._pinned_shm, rec
     want = e.master.clone()
     import json
 
@@ -130,15 +139,13 @@ def test_shm_save_before_preparation_finishes_uses_pinned_slots(tmp_path, monkey
     with open(ck.shm_meta) as f:
         meta = json.load(f)
     snap = torch.from_file(ck.shm_path, shared=False, size=ck.snap_bytes, dtype=torch.uint8)
-    assert _host.crc32c_chunks(snap) == meta["crc"]  # slot-copied CRCs agree with a full recomputation
+    assert _host.crc32c_chunks(snap) == meta["crc"]
     assert torch.equal(snap[:4 * ck.n].view(torch.float32), want.cpu())
     del snap
     if ck._prep is not None:
         ck._prep.join()
-    assert ck._pinned_shm
     e.train_step([(t[:, :-1], t[:, 1:])])
     ck.save(2, {"step": 2}, blocking=True)
-    assert "ring" not in ck.history[-1]
     want2 = e.master.clone()
     ck.close()
     e2 = _engine(seed=3)
