@@ -458,10 +458,13 @@ class AsyncCheckpointer:
         """Finish the preparation inside a save that came first: page-lock snapshot bytes [lo, hi) REG_CHUNK by
         REG_CHUNK (a helper thread reserves the pages ahead, as in _ring_capture) and queue each piece's D2H on the
         checkpoint stream as soon as it is locked, so the DMA of piece k runs while piece k+1 is being locked.
-        Registration maps and pins the pages in one kernel pass (~27 GB/s on MI355X); writing them from the host
-        instead faults every 4 KiB page on its own: the pinned-slot copy into a fresh mapping ran at 5 GB/s inside
-        the trainer (Mixtral EP = 8 spot drill: 81.7 GB in 17.1 s). Returns the end of the locked range (< hi when
-        a registration fails; the rest then goes through the slots). `segs`: (snapshot offset, uint8 device view)."""
+        What bounds it is making fresh tmpfs pages DMA-ready at all (profiles/shm_map_bench_r05.json, 24 GiB, one
+        thread on the MI355X host): fallocate 18-19.5 GB/s, page-locking reserved but unmapped pages 12.6 GB/s (41
+        GB/s once a read pass has mapped them, itself 15.6 GB/s), a sparse file 8 GB/s -- ~7-8 GB/s end to end
+        whichever way; the pinned-slot copy into a fresh mapping ran at 5 GB/s inside the trainer, and so did this
+        (Mixtral EP = 8 spot drill: 81.7 GB in 17.1 s / 15.4 s). The background preparation hides that cost for
+        every save after the first ~10 s of a job. Returns the end of the locked range (< hi when a registration
+        fails; the rest then goes through the slots). `segs`: (snapshot offset, uint8 device view)."""
         fns = self._hip_register_fns()
         if fns is None:
             return lo
