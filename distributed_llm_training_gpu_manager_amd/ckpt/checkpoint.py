@@ -70,6 +70,10 @@ class CorruptCheckpoint(RuntimeError):
     pass
 
 
+class _ReserveFailed(RuntimeError):
+    """posix_fallocate of the shm snapshot failed (tmpfs full): the snapshot moves to the host tier."""
+
+
 def _tag(step: int) -> str:
     return f"global_step{step}"
 
@@ -167,6 +171,7 @@ class AsyncCheckpointer:
         self._pinned_shm = False
         self._reg: List[Tuple[int, int]] = []  # page-locked pieces of the shm snapshot (address, bytes)
         self._falloc_done = 0  # shm snapshot bytes [0, _falloc_done) reserved
+        self._mapped_done = 0  # ... [0, _mapped_done) mapped into this process (page tables filled)
         self._reg_done = 0  # ... and [0, _reg_done) page-locked (the DMA part of a save)
         self._reg_failed = False
         self._slots: List[torch.Tensor] = []  # pinned slots of _ring_capture
@@ -260,7 +265,7 @@ class AsyncCheckpointer:
                 keep, self._restored_map = self._restored_map, None
                 if keep is not None and self.shm_path == self.shm_src_path and keep.numel() == nb:
                     self._snap = keep  # the file this rank just restored from, already mapped (pages touched)
-                    self._falloc_done = nb
+                    self._falloc_done = self._mapped_done = nb  # the restore read every page through it
                 else:
                     del keep
                     fd = os.open(self.shm_path, os.O_RDWR | os.O_CREAT, 0o600)
@@ -298,64 +303,107 @@ class AsyncCheckpointer:
         return (lambda p_, n_: int(reg(p_, n_, 0))), (lambda p_: int(unreg(p_)))
 
     def _prepare_shm(self, nb: int) -> bool:
-        """Make the mapped snapshot file ready for a DMA capture, in two passes of REG_CHUNK pieces, front to back:
+        """Make the mapped snapshot file ready for a DMA capture in the background: _ready_pipeline with a short
+        pause between page-locked pieces (one hipHostRegister of a whole ~112 GB file holds the HIP runtime for ~6 s
+        and every kernel launch of the training thread waits meanwhile; MI355X: the first step after a restore took
+        6.4 s instead of 0.9 s). The page-locked prefix [0, _reg_done) is what a save copies by DMA at ~57 GB/s; a
+        save that arrives first (an early spot notice) sets _prep_yield, the pipeline stops after its current
+        pieces, and the save runs the same pipeline for the rest itself (_lock_and_dma). Returns False when the
+        reservation failed (the caller falls back to the host tier)."""
+        def stopped() -> bool:
+            return self._prep_yield.is_set() or self._reg_stop.is_set()
+        t0 = time.time()
+        try:
+            self._ready_pipeline(nb, stop=stopped, pause=REG_PAUSE_S)
+        except _ReserveFailed:
+            self._unregister_all()
+            return False
+        finally:
+            self.prep_stats["pipeline_s"] = round(self.prep_stats.get("pipeline_s", 0.0) + time.time() - t0, 3)
+        return True
 
-        1. reserve every page (posix_fallocate: a full tmpfs is an error here, not a SIGBUS in the middle of a
-           snapshot copy). ~19 GB/s on the MI355X host, pure kernel work that touches no HIP state; faulting the
-           pages in instead (first-touch writes or MADV_POPULATE_WRITE, 16 threads) ran at 3.8 GB/s
-           (tools/diag/r05/prefault_bench.py). Done first, so an early save finds the file allocated.
-        2. page-lock it (hipHostRegister) with a short pause between pieces: one registration of a whole ~112 GB
-           file holds the HIP runtime for ~6 s and every kernel launch of the training thread waits meanwhile
-           (MI355X: the first step after a restore took 6.4 s instead of 0.9 s).
-
-        The page-locked prefix [0, _reg_done) is what a save copies by DMA at ~57 GB/s; a save that arrives first
-        (an early spot notice) sets _prep_yield, this loop stops after its current piece, the save streams the
-        rest through pinned slots (_ring_capture, reserving what pass 1 has not reached yet just ahead of the
-        copy) and restarts the preparation afterwards. Returns False when the reservation failed (the caller falls
-        back to the host tier). Measured on MI355X (Mixtral EP = 8 rank, 81.7 GB, spot notice at step 3, before the
-        preparation finished): emergency checkpoints of 3.4 s and 6.5 s in two runs with this order; 15.6 s with
-        reserve + page-lock interleaved per piece and the slot copy faulting the unreserved pages itself."""
-        fd = os.open(self.shm_path, os.O_RDWR)
-        ptr = self._snap.data_ptr()
+    def _ready_pipeline(self, hi: int, stop=None, pause: float = 0.0, on_locked=None) -> int:
+        """Snapshot pieces [_reg_done, hi) of REG_CHUNK bytes through three stages that run concurrently, one piece
+        apart: a thread reserves (posix_fallocate: a full tmpfs is an error here, not a SIGBUS in a later copy),
+        a thread maps (reads one byte per 4 KiB page through the mapping: read faults map 16 pages at a time), and
+        the calling thread page-locks (hipHostRegister), then calls on_locked(off, ln). On the MI355X host, one
+        24 GiB pass each: reserve 17-19.5 GB/s, map 15-19 GB/s (16 threads were no faster), page-lock mapped pages
+        55-58 GB/s against 12.6 GB/s for reserved-but-unmapped ones and 8 GB/s for a sparse file
+        (profiles/shm_map_bench_r05.json) -- so the pipeline runs at about the reserve rate. Without a GPU it only
+        reserves. Returns the end of the page-locked range (< hi after a stop or a failed registration: the rest
+        then goes through the pinned slots)."""
         fns = self._hip_register_fns() if self.cuda else None
         if self.cuda and fns is None:
             cr = torch.cuda.cudart()
             fns = (lambda p_, n_: int(cr.cudaHostRegister(p_, n_, 0))), (lambda p_: int(cr.cudaHostUnregister(p_)))
         if fns is not None:
             self._unreg = fns[1]
+        halt = threading.Event()
+        err: List[str] = []
 
-        def stopped() -> bool:
-            return self._prep_yield.is_set() or self._reg_stop.is_set()
+        def reserve():
+            fd = os.open(self.shm_path, os.O_RDWR)
+            try:
+                while self._falloc_done < hi and not halt.is_set():
+                    tf = time.time()
+                    if not self._reserve(fd, self._falloc_done, min(REG_CHUNK, hi - self._falloc_done)):
+                        err.append(self.tier_notes[-1])
+                        return
+                    self.prep_stats["fallocate_s"] = round(self.prep_stats.get("fallocate_s", 0.0) + time.time() - tf, 3)
+            finally:
+                os.close(fd)
+
+        def map_pages():
+            while self._mapped_done < hi and not halt.is_set() and not err:
+                off = self._mapped_done
+                ln = min(REG_CHUNK, hi - off)
+                if self._falloc_done < off + ln:
+                    time.sleep(0.0005)
+                    continue
+                int(self._snap[off:off + ln][::4096].sum())  # one byte per page: map it
+                self._mapped_done = off + ln
+
+        ths = [threading.Thread(target=reserve, daemon=True, name="ckpt-reserve")]
+        if fns is not None and not self._reg_failed:
+            ths.append(threading.Thread(target=map_pages, daemon=True, name="ckpt-map"))
+        for t in ths:
+            t.start()
+        ptr, off = self._snap.data_ptr(), self._reg_done
         try:
-            while self._falloc_done < nb:
-                if stopped():
-                    return True
-                off = self._falloc_done
-                tf = time.time()
-                if not self._reserve(fd, off, min(REG_CHUNK, nb - off)):
-                    self._unregister_all()
-                    return False
-                self.prep_stats["fallocate_s"] = round(self.prep_stats.get("fallocate_s", 0.0) + time.time() - tf, 3)
-            self.prep_stats.setdefault("reserved_at", time.time())
-            while fns is not None and not self._reg_failed and self._reg_done < nb:
-                if stopped():
-                    return True
-                off = self._reg_done
-                ln = min(REG_CHUNK, nb - off)
-                tr = time.time()
-                if fns[0](ptr + off, ln) != 0:
-                    self._reg_failed = True  # the rest goes through the pinned slots; never a correctness issue
-                    self.tier_notes.append("hipHostRegister of the shm snapshot failed; pinned-slot capture")
-                else:
+            if fns is None or self._reg_failed:
+                while self._falloc_done < hi and not err and not (stop and stop()):
+                    time.sleep(0.001)
+            else:
+                while off < hi:
+                    if stop is not None and stop():
+                        break
+                    ln = min(REG_CHUNK, hi - off)
+                    if self._mapped_done < off + ln and not err:
+                        time.sleep(0.0005)
+                        continue
+                    if err:
+                        break
+                    tr = time.time()
+                    if fns[0](ptr + off, ln) != 0:
+                        self._reg_failed = True  # the rest goes through the pinned slots; never a correctness issue
+                        self.tier_notes.append("hipHostRegister of the shm snapshot failed; pinned-slot capture")
+                        break
                     self._reg.append((ptr + off, ln))
                     self._reg_done = off + ln
-                self.prep_stats["register_s"] = round(self.prep_stats.get("register_s", 0.0) + time.time() - tr, 3)
-                if REG_PAUSE_S > 0 and self._reg_done < nb:
-                    time.sleep(REG_PAUSE_S)
-            self._pinned_shm = self.cuda and self._reg_done >= nb
-            return True
+                    self.prep_stats["register_s"] = round(self.prep_stats.get("register_s", 0.0) + time.time() - tr, 3)
+                    if on_locked is not None:
+                        on_locked(off, ln)
+                    off += ln
+                    if pause > 0 and off < hi:
+                        time.sleep(pause)
         finally:
-            os.close(fd)
+            halt.set()
+            for t in ths:
+                t.join()
+        if err:
+            raise _ReserveFailed(err[0])
+        self._pinned_shm = self.cuda and self._reg_done >= self.snap_bytes
+        return off
 
     def _reserve(self, fd: int, off: int, ln: int) -> bool:
         """posix_fallocate one piece of the snapshot file (the next unreserved one)."""
@@ -455,59 +503,22 @@ class AsyncCheckpointer:
         return crcs
 
     def _lock_and_dma(self, segs: List[Tuple[int, torch.Tensor]], lo: int, hi: int) -> int:
-        """Finish the preparation inside a save that came first: page-lock snapshot bytes [lo, hi) REG_CHUNK by
-        REG_CHUNK (a helper thread reserves the pages ahead, as in _ring_capture) and queue each piece's D2H on the
-        checkpoint stream as soon as it is locked, so the DMA of piece k runs while piece k+1 is being locked.
-        What bounds it is making fresh tmpfs pages DMA-ready at all (profiles/shm_map_bench_r05.json, 24 GiB, one
-        thread on the MI355X host): fallocate 18-19.5 GB/s, page-locking reserved but unmapped pages 12.6 GB/s (41
-        GB/s once a read pass has mapped them, itself 15.6 GB/s), a sparse file 8 GB/s -- ~7-8 GB/s end to end
-        whichever way; the pinned-slot copy into a fresh mapping ran at 5 GB/s inside the trainer, and so did this
-        (Mixtral EP = 8 spot drill: 81.7 GB in 17.1 s / 15.4 s). The background preparation hides that cost for
-        every save after the first ~10 s of a job. Returns the end of the locked range (< hi when a registration
-        fails; the rest then goes through the slots). `segs`: (snapshot offset, uint8 device view)."""
-        fns = self._hip_register_fns()
-        if fns is None:
-            return lo
-        self._unreg = fns[1]
-        res_err: List[str] = []
-        resv = None
-        if self._falloc_done < hi:
-            def reserve_ahead():
-                fd = os.open(self.shm_path, os.O_RDWR)
-                try:
-                    while self._falloc_done < hi:
-                        if not self._reserve(fd, self._falloc_done, min(REG_CHUNK, hi - self._falloc_done)):
-                            res_err.append(self.tier_notes[-1])
-                            return
-                finally:
-                    os.close(fd)
-            resv = threading.Thread(target=reserve_ahead, daemon=True, name="ckpt-reserve")
-            resv.start()
-        ptr, off = self._snap.data_ptr(), lo
-        try:
+        """Finish the preparation inside a save that came first: _ready_pipeline over [lo, hi) without pauses, each
+        piece's D2H queued on the checkpoint stream as soon as it is page-locked (the DMA of piece k runs while
+        piece k+1 is being reserved / mapped / locked). The first versions measured what this avoids: a pinned-slot
+        copy into a fresh mapping, or page-locking unmapped pages, both ran at ~5 GB/s inside the trainer (Mixtral
+        EP = 8 spot drill, 81.7 GB: 17.1 s / 15.4 s). Returns the end of the locked range. `segs`: (snapshot offset,
+        uint8 device view)."""
+        def dma(off: int, ln: int) -> None:
             with torch.cuda.stream(self._stream):
-                while off < hi:
-                    ln = min(REG_CHUNK, hi - off)
-                    while self._falloc_done < off + ln and not res_err:
-                        time.sleep(0.0005)
-                    if res_err:
-                        raise RuntimeError(f"shm snapshot: {res_err[0]}")
-                    if fns[0](ptr + off, ln) != 0:
-                        self._reg_failed = True
-                        self.tier_notes.append("hipHostRegister of the shm snapshot failed; pinned-slot capture")
-                        break
-                    self._reg.append((ptr + off, ln))
-                    self._reg_done = off + ln
-                    for base, src in segs:
-                        a, b = max(off, base), min(off + ln, base + src.numel())
-                        if a < b:
-                            self._snap[a:b].copy_(src[a - base:b - base], non_blocking=True)
-                    off += ln
-        finally:
-            if resv is not None:
-                resv.join()
-        self._pinned_shm = self._reg_done >= self.snap_bytes
-        return off
+                for base, src in segs:
+                    a, b = max(off, base), min(off + ln, base + src.numel())
+                    if a < b:
+                        self._snap[a:b].copy_(src[a - base:b - base], non_blocking=True)
+        try:
+            return self._ready_pipeline(hi, on_locked=dma)
+        except _ReserveFailed as e:
+            raise RuntimeError(f"shm snapshot: {e}") from e
 
     def prepare_async(self) -> None:
         """Reserve (and page-lock) the snapshot buffer on a background thread while training runs, so the
@@ -1142,7 +1153,7 @@ class AsyncCheckpointer:
             self._prep = None
         if self.cuda and self._reg:
             self._unregister_all()
-        self._reg, self._reg_done, self._falloc_done = [], 0, 0
+        self._reg, self._reg_done, self._falloc_done, self._mapped_done = [], 0, 0, 0
         self._pinned_shm = False
         self._snap = None
         self._slots = []

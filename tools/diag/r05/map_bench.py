@@ -31,7 +31,7 @@ def gbps(dt):
     return round(SIZE / dt / 1e9, 1) if dt > 0 else None
 
 
-def case(name, falloc, read, popr):
+def case(name, falloc, read, popr, mt_read=False):
     path = f"/dev/shm/dlgm-mapbench-{name}"
     fd = os.open(path, os.O_RDWR | os.O_CREAT, 0o600)
     os.ftruncate(fd, SIZE)
@@ -49,6 +49,14 @@ def case(name, falloc, read, popr):
         s = int(a[::4096].sum())  # one byte per page
         res[name + "_read_GBps"] = gbps(time.time() - t)
         del a
+    if mt_read:  # read pass on the C++ host runtime's threads (the CRC of every 64 MiB chunk)
+        import sys
+        sys.path.insert(0, ".")
+        from distributed_llm_training_gpu_manager_amd import _host
+        t = time.time()
+        _host.crc32c_chunks(torch.frombuffer(m, dtype=torch.uint8))
+        res[name + "_mt_read_GBps"] = gbps(time.time() - t)
+        res[name + "_threads"] = _host.THREADS
     if popr:
         t = time.time()
         rc = libc.madvise(addr, SIZE, MADV_POPULATE_READ)
@@ -70,10 +78,8 @@ def case(name, falloc, read, popr):
     print(name, json.dumps({k: v for k, v in res.items() if k.startswith(name)}), flush=True)
 
 
-case("reg_fresh", False, False, False)
-case("reg_falloc", True, False, False)
-case("read_falloc", True, True, False)
-case("popr_falloc", True, False, True)
+for c in os.environ.get("CASES", "reg_fresh,reg_falloc,read_falloc,popr_falloc,mtread_falloc").split(","):
+    case(c, c != "reg_fresh", c == "read_falloc", c == "popr_falloc", c == "mtread_falloc")
 os.makedirs("gpurun_out/digest", exist_ok=True)
 with open("gpurun_out/digest/map_bench.json", "w") as f:
     json.dump(res, f, indent=1)
