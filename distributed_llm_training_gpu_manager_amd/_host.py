@@ -50,6 +50,8 @@ def lib():
         L.dlgm_copy_crc32c_chunks.restype = None
         L.dlgm_copy_crc32c_chunks.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
                                               ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)]
+        L.dlgm_touch_pages.restype = ctypes.c_uint64
+        L.dlgm_touch_pages.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
         L.dlgm_close_file.restype = ctypes.c_int
         L.dlgm_close_file.argtypes = [ctypes.c_int, ctypes.c_int]
         L.dlgm_aio_create.restype = ctypes.c_void_p
@@ -154,6 +156,16 @@ def copy_crc32c_chunks(src: torch.Tensor, dst: torch.Tensor) -> List[int]:
     L.dlgm_copy_crc32c_chunks(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()), n, CHUNK, THREADS,
                               crcs)
     return list(crcs)[:nch]
+
+
+def touch_pages(t: torch.Tensor, threads: int = THREADS) -> int:
+    """Read one byte per 4 KiB page of a contiguous CPU tensor (a mapped /dev/shm file) on `threads` threads:
+    maps the pages into this process, zeroing reserved-but-untouched tmpfs pages on the way. Returns the byte sum."""
+    n = t.numel() * t.element_size()
+    L = lib()
+    if L is None:
+        return int(t.view(torch.uint8)[::4096].sum()) if n else 0
+    return int(L.dlgm_touch_pages(ctypes.c_void_p(t.data_ptr()), n, int(threads)))
 
 
 def cpu_adamw_(p, m, v, g, p16, lr, b1, b2, eps, wd, bc1, bc2, gscale=1.0) -> None:

@@ -691,6 +691,20 @@ class AsyncCheckpointer:
                 "loss_scaler": (eng.scaler.state_dict() if eng.scaler is not None else None)}
 
     @property
+    def prepared(self) -> bool:
+        """The snapshot buffer is ready for a capture at DMA rate: nothing is left for the background preparation
+        (reserved and, with a GPU, page-locked -- or the page-locking failed and the pinned slots carry it)."""
+        if not self.active:
+            return True
+        if self._snap is None:
+            return False
+        if self.mode != "shm":
+            return True
+        if self._falloc_done < self.snap_bytes:
+            return False
+        return not self.cuda or self._reg_failed or self._reg_done >= self.snap_bytes
+
+    @property
     def busy(self) -> bool:
         with self._plock:
             return self._pending > 0

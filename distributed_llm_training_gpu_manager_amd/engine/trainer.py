@@ -234,6 +234,17 @@ class Trainer:
             e.grad_accum = ga
         return ga * e.micro_batch_size * dp
 
+    def _notice_due(self, step: int, first_attempt: bool) -> bool:
+        """Spot drill: deliver the preemption notice after step --preempt-at-step; with --preempt-when-ready, after
+        the first step from there on at which the snapshot buffer is prepared (a notice that lands on a warm job,
+        the usual case hours into a run, rather than seconds after its start)."""
+        a = self.args
+        if a.preempt_at_step < 0 or self._notice_sent or not first_attempt or a.preempt_rank not in (-1, self.env.rank):
+            return False
+        if not a.preempt_when_ready:
+            return step == a.preempt_at_step
+        return step >= a.preempt_at_step and (self.ckpt is None or self.ckpt.prepared)
+
     def _say(self, msg: str) -> None:
         if self.env.rank == 0:
             print(f"[train] {msg}", flush=True)
@@ -343,6 +354,7 @@ class Trainer:
         write_heartbeat(self.env.rank, start, phase="ready")  # restored / initialised: the first step is next
         self.engine.sync_flags = self.env.world > 1
         first_attempt = os.environ.get("DLGM_RESTART", "0") == "0"
+        self._notice_sent = False
         rc = 0
         prev: Optional[Tuple[int, Dict[str, Any]]] = None
         last = start
@@ -408,8 +420,9 @@ class Trainer:
                 os.kill(os.getpid(), signal.SIGKILL)
             if a.stop_at_step == step and first_attempt and self.env.rank == a.stop_rank:
                 os.kill(os.getpid(), signal.SIGSTOP)  # hang drill: this rank freezes (only SIGKILL / SIGCONT move it)
-            if a.preempt_at_step == step and first_attempt and a.preempt_rank in (-1, self.env.rank):
+            if self._notice_due(step, first_attempt):
                 # a notice on one rank only (--preempt-rank): its flag rides the next step's all-reduced statistics
+                self._notice_sent = True
                 os.kill(os.getpid(), signal.SIGUSR1)
             if self.preempt and self.env.world == 1:
                 # one rank needs no agreement: checkpoint the step just queued, now (W > 1 ranks agree through
@@ -519,6 +532,9 @@ def parse_args(argv=None) -> argparse.Namespace:
                     "(first attempt only)")
     ap.add_argument("--stop-rank", type=int, default=0, help="rank the hang drill freezes")
     ap.add_argument("--preempt-at-step", type=int, default=-1, help="spot drill: deliver SIGUSR1 after the step")
+    ap.add_argument("--preempt-when-ready", action="store_true",
+                    help="spot drill: deliver the notice at the first step >= --preempt-at-step at which the "
+                         "checkpoint snapshot buffer is prepared")
     ap.add_argument("--halt-on-nan", type=int, default=1)
     ap.add_argument("--metrics-url", default=os.environ.get("DLGM_METRICS_URL"))
     ap.add_argument("--job-id", default=os.environ.get("DLGM_JOB_ID", "local"))

@@ -165,3 +165,15 @@ def test_nvme_param_store_read_ahead(tmp_path):
     # step 0 learns the order; steps 1 and 2 hit on every access after the first
     assert st.stats["read_ahead_hits"] == 2 * (len(order) - 1), st.stats
     st.close()
+
+
+def test_touch_pages_maps_a_shared_file_and_sums_one_byte_per_page(tmp_path):
+    """_host.touch_pages (csrc/host/ckpt_io.cpp): one byte read per 4 KiB page on several threads."""
+    n = 40 << 20
+    path = tmp_path / "snap"
+    with open(path, "wb") as f:
+        f.truncate(n)
+    t = torch.from_file(str(path), shared=True, size=n, dtype=torch.uint8)
+    t[0], t[4096 * 7], t[4096 * 7 + 1], t[n - 4096] = 3, 5, 100, 11  # the +1 byte is not on a page start
+    assert _host.touch_pages(t, 4) == 3 + 5 + 11
+    assert _host.touch_pages(t[:8192], 16) == 3

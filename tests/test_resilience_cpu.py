@@ -178,6 +178,16 @@ def test_spot_preemption_drill_emergency_checkpoint_and_restore(tmp_path):
     assert r.run() == 0 and r.log[0]["step"] == 5
 
 
+def test_spot_notice_when_ready_waits_for_the_prepared_snapshot(tmp_path, monkeypatch):
+    """--preempt-when-ready (the warm spot drill): the notice goes out at the first step >= K at which the
+    checkpointer reports its snapshot buffer prepared -- here the third step it is asked."""
+    asked = []
+    monkeypatch.setattr(AsyncCheckpointer, "prepared", property(lambda self: asked.append(1) or len(asked) >= 3))
+    t = _train(tmp_path, "--steps", "10", "--preempt-at-step", "2", "--preempt-when-ready")
+    assert t.run() == EXIT_PREEMPTED
+    assert complete_tags(str(tmp_path))[-1] == "global_step4" and len(asked) == 3
+
+
 def test_supervised_sigkill_auto_resume_mttr(tmp_path):
     """BASELINE config 4 plumbing: mid-run SIGKILL -> supervisor relaunch -> rollback -> MTTR recorded."""
     reg = JobRegistry()

@@ -6,6 +6,7 @@
             completed step after the restart), plus checkpoint capture / write / restore times
   spot    : SIGUSR1 at step K (what the spot manager sends) -> emergency checkpoint -> exit 4 ->
             restore on a fresh process -> first step
+  spot_warm: the same with the notice at the first step >= K at which the snapshot buffer is prepared
 """
 from __future__ import annotations
 
@@ -86,16 +87,18 @@ def drill_sigkill(a, work):
             "tail": log[-800:]}
 
 
-def drill_spot(a, work):
+def drill_spot(a, work, warm=False):
+    """warm: the notice lands once the snapshot buffer is prepared (--preempt-when-ready) instead of at step K."""
     ck = os.path.join(work, "ck_spot")
-    rc, out, dt = run(train_argv(a, ["--steps", str(a.k + 5), "--save-dir", ck, "--preempt-at-step", str(a.k)]),
+    notice = ["--preempt-at-step", str(a.k)] + (["--preempt-when-ready"] if warm else [])
+    rc, out, dt = run(train_argv(a, ["--steps", str(a.k + (400 if warm else 5)), "--save-dir", ck, *notice]),
                       a.timeout)
     em = re.findall(r"emergency checkpoint at step (\d+) in ([0-9.]+)s", out)
     rc2, out2, dt2 = run(train_argv(a, ["--steps", str(a.k + 1), "--save-dir", ck, "--resume", "auto"]), a.timeout)
     res = re.findall(r"resumed from step (\d+) in ([0-9.]+)s", out2)
     via = re.findall(r"resumed from step \d+ in [0-9.]+s via (\S+)", out2)
     stats = re.findall(r"restore (\{.*?\})\)", out2)
-    return {"drill": "spot", "restore_breakdown": [json.loads(x) for x in stats], "exit_code_preempted": rc,
+    return {"drill": "spot_warm" if warm else "spot", "restore_breakdown": [json.loads(x) for x in stats], "exit_code_preempted": rc,
             "emergency_ckpt": em, "restore_exit": rc2,
             "emergency_record": [json.loads(x) for x in re.findall(r"emergency checkpoint record: (\{.*?\})\n", out)],
             "memory": [json.loads(x) for x in re.findall(r"memory: (\{.*?\})", out + out2)],
@@ -141,7 +144,8 @@ def main():
            "data": "synthetic token ids, random-init weights"}
     for d in a.drills.split(","):
         t0 = time.time()
-        res[d] = {"nan": drill_nan, "sigkill": drill_sigkill, "spot": drill_spot}[d](a, work)
+        res[d] = {"nan": drill_nan, "sigkill": drill_sigkill, "spot": drill_spot,
+                  "spot_warm": lambda a_, w_: drill_spot(a_, w_, warm=True)}[d](a, work)
         res[d]["wall_s"] = round(time.time() - t0, 1)
         print(json.dumps({k: v for k, v in res[d].items() if k != "tail"})[:2000], flush=True)
         os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)

@@ -3,6 +3,7 @@
 # expert per layer on this rank, ZeRO-3 shards of the dense weights) alone on this GPU (--shadow-world 8), with the
 # expert token exchange on the device-driven xGMI mesh kernels (shadow mode: every peer slot is this rank's own heap).
 # spot: SIGUSR1 at step K -> emergency checkpoint into the /dev/shm tier -> exit 4 -> restore on a fresh process;
+# spot_warm: the same with the notice once the snapshot buffer is prepared (--preempt-when-ready);
 # sigkill: SIGKILL at step K under the supervisor -> auto-resume -> MTTR and restore breakdown.
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
