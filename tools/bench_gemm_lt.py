@@ -39,12 +39,12 @@ def timeit(fn, iters=10):
     return e0.elapsed_time(e1) / iters * 1e3  # us
 
 
-def problems(T, d=4096, qkv=6144, ffn=14336, vocab=128256):
+def problems(T, d=4096, qkv=6144, ffn=14336, vocab=128256, dense_mlp=True):
     dev = torch.device("cuda")
     bf = dict(dtype=torch.bfloat16, device=dev)
     out = []
-    for name, n_out, n_in in (("qkv", qkv, d), ("o", d, d), ("gate_up", 2 * ffn, d), ("down", d, ffn),
-                              ("lm_head", vocab, d)):
+    mats = [("qkv", qkv, d), ("o", d, d)] + ([("gate_up", 2 * ffn, d), ("down", d, ffn)] if dense_mlp else [])
+    for name, n_out, n_in in mats + [("lm_head", vocab, d)]:
         x = torch.randn(T, n_in, **bf) * 0.5
         w = torch.randn(n_out, n_in, **bf) * 0.02
         dy = torch.randn(T, n_out, **bf) * 0.01
@@ -61,6 +61,8 @@ def problems(T, d=4096, qkv=6144, ffn=14336, vocab=128256):
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--tokens", type=int, default=8192)
+    ap.add_argument("--model", default="llama3-8b", help="model preset whose dense GEMM shapes are tuned (an MoE "
+                    "model's expert GEMMs run on the grouped MFMA kernel and are skipped)")
     ap.add_argument("--topn", type=int, default=16)
     ap.add_argument("--all", action="store_true", help="also search every hipBLASLt solution")
     ap.add_argument("--write", action="store_true")
@@ -72,7 +74,11 @@ def main() -> int:
     ops = _native.hip_ops()
     ver = int(ops.gemm_lt_version())
     res, sols, measured = {}, {}, []
-    for name, out, x, y in problems(a.tokens):
+    from distributed_llm_training_gpu_manager_amd.models import get_config
+    mc = get_config(a.model)
+    probs = problems(a.tokens, d=mc.d_model, qkv=mc.qkv_dim, ffn=mc.ffn_dim, vocab=mc.vocab_size,
+                     dense_mlp=not mc.n_experts)
+    for name, out, x, y in probs:
         if a.only and not any(s in name for s in a.only.split(",")):
             continue
         beta = 1.0 if out.dtype == torch.float32 else 0.0
@@ -128,13 +134,16 @@ def main() -> int:
     if a.write:
         os.makedirs(G.TUNED_DIR, exist_ok=True)
         path = G.TUNED_DIR / f"gemm_lt_v{ver}.json"
-        old = json.load(open(path)).get("solutions", {}) if path.exists() else {}
+        prev = json.load(open(path)) if path.exists() else {}
+        old = prev.get("solutions", {})
         for k in measured:  # re-measured problems: drop entries that no longer win
             old.pop(k, None)
         old.update(sols)
+        meas = prev.get("measured", {})
+        meas.update({(name if a.model == "llama3-8b" else f"{a.model}:{name}"): row for name, row in res.items()})
         with open(path, "w") as f:
             json.dump({"hipblaslt_version": ver, "device": torch.cuda.get_device_properties(0).gcnArchName,
-                       "solutions": old, "measured": res}, f, indent=1)
+                       "solutions": old, "measured": meas}, f, indent=1)
         print("wrote", path)
     return 0
 
