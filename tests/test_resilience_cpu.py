@@ -244,3 +244,19 @@ def test_zero_to_fp32_offline_consolidation(tmp_path):
     from safetensors.torch import load_file
     sd = load_file(str(out))
     assert all(torch.equal(sd[k], v.to(torch.bfloat16)) for k, v in full.items())
+
+
+def test_checkpointer_reports_prepared_after_background_preparation(tmp_path):
+    """AsyncCheckpointer.prepared (what --preempt-when-ready waits for): False before the snapshot buffer exists,
+    True once the background preparation has reserved the whole /dev/shm file (no GPU: nothing to page-lock)."""
+    mc = get_config("llama-tiny")
+    eng = ZeroEngine(mc, EngineConfig(zero_stage=3, micro_batch_size=1, seq_len=32, grad_accum=1,
+                                      scheduler="constant", init_device="cpu"), torch.device("cpu"))
+    ck = AsyncCheckpointer(eng, str(tmp_path), shm=True, disk=False)
+    assert ck.mode == "shm" and not ck.prepared
+    ck.prepare_async()
+    ck._prep.join()
+    assert ck.prepared and ck._falloc_done == ck.snap_bytes
+    ck.save(1, {"step": 1}, blocking=True)
+    assert ck.prepared
+    ck.close(discard_shm=True)
