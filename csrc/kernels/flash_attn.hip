@@ -164,10 +164,13 @@ __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" :
 // One LDS-DMA piece through a buffer descriptor (buffer_load_dwordx4 ... lds): `base` and `nbytes`
 // are wave-uniform (the descriptor lives in SGPRs, reads at or past nbytes return zero), `voff`
 // is the per-lane byte offset, `soff` a wave-uniform byte offset (the tile advance).
-__device__ __forceinline__ void dma16(const void* base, int nbytes, uint32_t voff, uint32_t soff, void* lds) {
+__device__ __forceinline__ void dma16(const void* base, int nbytes, uint32_t voff, uint32_t soff, lptr_t lds) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, nbytes,
                                                                              0x00020000),
-                                           (lptr_t)lds, 16, voff, soff, 0, 0);
+                                           lds, 16, voff, soff, 0, 0);
+}
+__device__ __forceinline__ void dma16(const void* base, int nbytes, uint32_t voff, uint32_t soff, void* lds) {
+  dma16(base, nbytes, voff, soff, (lptr_t)lds);
 }
 
 // Loop-invariant LDS-DMA plan for a tile of ROWS x D bf16 rows that is re-staged every iteration
@@ -198,9 +201,19 @@ struct TileDma {
   __device__ __forceinline__ void extend(int64_t bytes) { nbytes += (int)bytes; }
   __device__ __forceinline__ void issue(E* img, int row0, uint32_t extra_soff = 0) const {
     if (!TAIL || row0 + ROWS <= nrows) {  // whole tile in range: scalar row advance
-      const uint32_t soff = (uint32_t)(row0 * stride * 2) + extra_soff, step = (uint32_t)(NW * PR * stride * 2);
+      const uint32_t step = (uint32_t)(NW * PR * stride * 2);
+      uint32_t soff = (uint32_t)(row0 * stride * 2) + extra_soff;
+      uint32_t lds = (uint32_t)(uintptr_t)(lptr_t)(img + wave * 512);  // LDS byte offset
+      // both offsets advance piece by piece in scalar registers, made opaque to the optimiser: hoisted out of the
+      // tile loop as PPW precomputed values per tile image they outgrew the SGPR file and came back through
+      // v_readlane -- two vector instructions per LDS-DMA piece in the forward / dQ loops
 #pragma unroll
-      for (int j = 0; j < PPW; ++j) dma16(base, nbytes, off0, soff + j * step, img + (wave + NW * j) * 512);
+      for (int j = 0; j < PPW; ++j) {
+        dma16(base, nbytes, off0, soff, (lptr_t)(uintptr_t)lds);
+        soff += step;
+        lds += NW * 512 * (uint32_t)sizeof(E);
+        asm volatile("" : "+s"(soff), "+s"(lds));
+      }
       return;
     }
     if constexpr (TAIL) {
