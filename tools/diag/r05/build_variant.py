@@ -2,7 +2,8 @@
 LLVM AMDGPU scheduling strategy), for same-process A/B through DLGM_HIP_LIB (tools/ab_kernels.sh).
 
     python tools/diag/r05/build_variant.py <tag> <source stem> <flag> [<flag> ...]
-    -> build/variants/_dlgm_hip_<tag>.so  (the other objects are the in-tree build's)
+    -> build/variants/_dlgm_hip_<tag>.so  (the other objects are the in-tree build's; the in-tree library is
+       (re)built from the current sources first, so it always matches them)
 Prints the kernel resource usage of the variant object (VGPRs / spills) for the kernels in that source."""
 import subprocess
 import sys
