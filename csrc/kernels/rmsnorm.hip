@@ -149,18 +149,23 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_kernel(
 // no LDS reduction, and the per-thread state is tiny (~80 VGPRs -> 5-6 waves per SIMD): the row is
 // loaded once (dy, h, dres together), reduced across the block through a 2-slot LDS array (one
 // barrier per row; slot parity keeps a fast wave from overwriting a value a slow wave still reads).
-template <typename E, int CPL, bool DRES>
+// GUARD: rows whose chunk count is not a multiple of 256 (D = 5120, 6144, 7168, ...; without it those widths took
+// the wave-per-row kernel at 16 chunks per lane, which spills 217-253 VGPRs): a thread's chunks past the row end
+// hold zeros and store nothing.
+template <typename E, int CPL, bool DRES, bool GUARD = false>
 __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_rowblock_kernel(
     const E* __restrict__ dy, const E* __restrict__ hin, const E* __restrict__ w,
     const float* __restrict__ rstd, const E* __restrict__ dres, E* __restrict__ dx,
     float* __restrict__ dw_part, int T, int D) {
   __shared__ float red[2][kWaves];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nch = D >> 3;
+  auto live = [&](int c) { return !GUARD || tid + c * kThreads < nch; };
   f32x8 acc[CPL], wv[CPL];
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
     acc[c] = (f32x8)(0.f);
-    wv[c] = load8f(w + (tid + c * kThreads) * 8);
+    wv[c] = live(c) ? load8f(w + (tid + c * kThreads) * 8) : (f32x8)(0.f);
   }
   const float inv_d = 1.f / (float)D;
   int it = 0;
@@ -171,9 +176,14 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_rowblock_kernel(
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
       const size_t off = base + (size_t)(tid + c * kThreads) * 8;
-      gr[c] = *reinterpret_cast<const vec8_t<E>*>(dy + off);
-      hr[c] = *reinterpret_cast<const vec8_t<E>*>(hin + off);
-      if constexpr (DRES) rr[c] = *reinterpret_cast<const vec8_t<E>*>(dres + off);
+      if (live(c)) {
+        gr[c] = *reinterpret_cast<const vec8_t<E>*>(dy + off);
+        hr[c] = *reinterpret_cast<const vec8_t<E>*>(hin + off);
+        if constexpr (DRES) rr[c] = *reinterpret_cast<const vec8_t<E>*>(dres + off);
+      } else {
+        gr[c] = hr[c] = (vec8_t<E>)((E)0.f);
+        if constexpr (DRES) rr[c] = (vec8_t<E>)((E)0.f);
+      }
     }
     float dot = 0.f;
 #pragma unroll
@@ -195,11 +205,12 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_bwd_rowblock_kernel(
       const f32x8 xh = __builtin_convertvector(hr[c], f32x8) * rs;
       f32x8 o = (gw - xh * dot) * rs;
       if constexpr (DRES) o += __builtin_convertvector(rr[c], f32x8);
-      store8f(dx + base + (size_t)(tid + c * kThreads) * 8, o);
+      if (live(c)) store8f(dx + base + (size_t)(tid + c * kThreads) * 8, o);
     }
   }
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
+    if (!live(c)) continue;
     float* dst = dw_part + (size_t)blockIdx.x * D + (size_t)(tid + c * kThreads) * 8;
     *reinterpret_cast<f32x4*>(dst) = (f32x4){acc[c][0], acc[c][1], acc[c][2], acc[c][3]};
     *reinterpret_cast<f32x4*>(dst + 4) = (f32x4){acc[c][4], acc[c][5], acc[c][6], acc[c][7]};
@@ -339,6 +350,7 @@ at::Tensor dlgm_rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at:
   TORCH_CHECK(h.scalar_type() == dy.scalar_type() && w.scalar_type() == dy.scalar_type() &&
                   (!has_dres || dres->scalar_type() == dy.scalar_type()), "rmsnorm_bwd: mixed dtypes");
   const int cpl = (D % (8 * kThreads) == 0) ? (int)(D / (8 * kThreads)) : 0;
+  const bool guarded = cpl == 0 && D > 4096;  // 4096 < D <= 8192, not a multiple of 2048: guarded 4-chunk row block
 #define LAUNCH_ROWBLOCK(C)                                                                                  \
     if (has_dres)                                                                                           \
       rmsnorm_bwd_rowblock_kernel<E, C, true><<<nblk, kThreads, 0, stream>>>(dyp, hp, wp, rstd.data_ptr<float>(), \
@@ -346,6 +358,13 @@ at::Tensor dlgm_rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at:
     else                                                                                                    \
       rmsnorm_bwd_rowblock_kernel<E, C, false><<<nblk, kThreads, 0, stream>>>(dyp, hp, wp, rstd.data_ptr<float>(), \
                                                                          drp, dxp, part.data_ptr<float>(), T, D);
+#define LAUNCH_ROWBLOCK_GUARD                                                                              \
+    if (has_dres)                                                                                           \
+      rmsnorm_bwd_rowblock_kernel<E, 4, true, true><<<nblk, kThreads, 0, stream>>>(                         \
+          dyp, hp, wp, rstd.data_ptr<float>(), drp, dxp, part.data_ptr<float>(), T, D);                     \
+    else                                                                                                    \
+      rmsnorm_bwd_rowblock_kernel<E, 4, false, true><<<nblk, kThreads, 0, stream>>>(                        \
+          dyp, hp, wp, rstd.data_ptr<float>(), drp, dxp, part.data_ptr<float>(), T, D);
 #define LAUNCH_BWD(C)                                                                                \
     if (has_dres)                                                                                    \
       rmsnorm_bwd_kernel<E, C, true><<<nblk, kThreads, 0, stream>>>(dyp, hp, wp, rstd.data_ptr<float>(),  \
@@ -359,15 +378,19 @@ at::Tensor dlgm_rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at:
   auto wp = reinterpret_cast<const E*>(w.data_ptr());
   auto drp = has_dres ? reinterpret_cast<const E*>(dres->data_ptr()) : nullptr;
   auto dxp = reinterpret_cast<E*>(dx.data_ptr());
-  if (cpl == 1 || cpl == 2 || cpl == 4) {
+  if (cpl == 1 || cpl == 2 || cpl == 4 || guarded) {
     // block-per-row kernel: 1024 blocks (~5 resident per CU), 8 rows each at T = 8192
     nblk = std::max<int64_t>(1, std::min<int64_t>(T, 1024));
     part = at::empty({nblk, D}, dy.options().dtype(at::kFloat));
     if (T > 0) {
-      switch (cpl) {
-        case 1: LAUNCH_ROWBLOCK(1); break;
-        case 2: LAUNCH_ROWBLOCK(2); break;
-        default: LAUNCH_ROWBLOCK(4); break;
+      if (guarded) {
+        LAUNCH_ROWBLOCK_GUARD;
+      } else {
+        switch (cpl) {
+          case 1: LAUNCH_ROWBLOCK(1); break;
+          case 2: LAUNCH_ROWBLOCK(2); break;
+          default: LAUNCH_ROWBLOCK(4); break;
+        }
       }
     } else {
       part.zero_();
@@ -385,6 +408,7 @@ at::Tensor dlgm_rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at:
   }
   });
 #undef LAUNCH_ROWBLOCK
+#undef LAUNCH_ROWBLOCK_GUARD
 #undef LAUNCH_BWD
   DLGM_CHECK_HIP(hipGetLastError());
   // many partial rows: fold them 16 at a time in a wide first pass (fixed order: deterministic)

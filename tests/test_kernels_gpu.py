@@ -26,7 +26,7 @@ def test_native_library_loaded():
     assert hasattr(torch.ops.dlgm, "flash_attn_fwd")
 
 
-@pytest.mark.parametrize("D", [128, 768, 2048, 4096, 8192])
+@pytest.mark.parametrize("D", [128, 768, 2048, 4096, 5120, 6656, 8192])
 @pytest.mark.parametrize("resid", [False, True])
 def test_rmsnorm_fwd_bwd(D, resid):
     torch.manual_seed(0)
