@@ -138,7 +138,7 @@ def main() -> int:
         return 2
 
     from distributed_llm_training_gpu_manager_amd.models import get_config
-    from distributed_llm_training_gpu_manager_amd.parallel.comm import Comm, init_distributed
+    from distributed_llm_training_gpu_manager_amd.parallel.comm import Comm, init_distributed, rccl_env
     from distributed_llm_training_gpu_manager_amd.parallel.zero import EngineConfig, ZeroEngine
     from distributed_llm_training_gpu_manager_amd import _native
 
@@ -249,6 +249,7 @@ def main() -> int:
                                         "per_step" if eng.local_grads else "per_micro_batch"),
                 "hip_graphs": eng._graph is not None,
                 "transport": ("xgmi_mesh" if eng.mesh is not None else "rccl") if eng.W > 1 else "none",
+                "step_reduce_dtype": str(ecfg.step_comm_dtype).replace("torch.", "") if eng.local_grads else None,
             },
             "extra": {
                 "tokens_per_sec_per_gpu": round(tps / env.world, 2),
@@ -265,6 +266,7 @@ def main() -> int:
                 "launch": "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ else "single process",
                 "telemetry": telem,
                 "comm_busbw": None,
+                "comm_env": rccl_env(apply=False) if env.backend == "nccl" else None,
             },
         }
     if args.comm_sweep == "on" or (args.comm_sweep == "auto" and env.world > 1):

@@ -85,10 +85,10 @@ void dlgm_mesh_sync(at::Tensor state, const at::Tensor& peers, int64_t me, int64
 void dlgm_mesh_pull(at::Tensor out, const at::Tensor& peers, int64_t src_off, int64_t heap_bytes);
 void dlgm_mesh_rs_push(const at::Tensor& x, const at::Tensor& peers, at::Tensor state, int64_t me, int64_t ch,
                        int64_t region_off, int64_t slot_bytes, int64_t rank_stride, int64_t slots,
-                       int64_t heap_bytes);
+                       int64_t heap_bytes, bool fp32_slots);
 void dlgm_mesh_rs_reduce(at::Tensor out, double scale, bool accumulate, const at::Tensor& peers, at::Tensor state,
                          int64_t me, int64_t ch, int64_t region_off, int64_t slot_bytes, int64_t rank_stride,
-                         int64_t slots, int64_t heap_bytes);
+                         int64_t slots, int64_t heap_bytes, bool fp32_slots);
 std::vector<int64_t> dlgm_mesh_plan_layout(int64_t W, int64_t E);
 void dlgm_mesh_ep_plan(const at::Tensor& offsets, at::Tensor plan, int64_t capacity, const at::Tensor& peers,
                        at::Tensor state, int64_t me, int64_t ch, int64_t region_off, int64_t slot_bytes,
@@ -120,7 +120,7 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("moe_pad_plan_multi(Tensor offsets, int padded_rows, int align) -> (Tensor, Tensor)");
   m.def("transpose_multi(Tensor[] xs, Tensor rows) -> Tensor");
   m.def("transpose(Tensor x, Tensor(a!)? out=None, Tensor? rows=None) -> Tensor");
-  m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, float softmax_scale, bool causal, Tensor? dqkv=None) -> (Tensor, Tensor, Tensor)");
+  m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, float softmax_scale, bool causal, Tensor(a!)? dqkv=None) -> (Tensor, Tensor, Tensor)");
   m.def("embedding_fwd(Tensor table, Tensor ids) -> Tensor");
   m.def("embedding_bwd_(Tensor(a!) grad, Tensor dy, Tensor sorted_ids, Tensor order) -> ()");
   m.def("router_topk(Tensor logits, int k) -> (Tensor, Tensor, Tensor)");
@@ -136,8 +136,8 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("mesh_plan_layout(int W, int E) -> int[]", &dlgm_mesh_plan_layout);
   m.def("mesh_sync(Tensor(a!) state, Tensor peers, int me, int ch, int inc, int val, int store_kind, int wait_kind, int lag, int timeout) -> ()");
   m.def("mesh_pull(Tensor(a!) out, Tensor peers, int src_off, int heap_bytes) -> ()");
-  m.def("mesh_rs_push(Tensor x, Tensor peers, Tensor(a!) state, int me, int ch, int region_off, int slot_bytes, int rank_stride, int slots, int heap_bytes) -> ()");
-  m.def("mesh_rs_reduce(Tensor(a!) out, float scale, bool accumulate, Tensor peers, Tensor(b!) state, int me, int ch, int region_off, int slot_bytes, int rank_stride, int slots, int heap_bytes) -> ()");
+  m.def("mesh_rs_push(Tensor x, Tensor peers, Tensor(a!) state, int me, int ch, int region_off, int slot_bytes, int rank_stride, int slots, int heap_bytes, bool fp32_slots=False) -> ()");
+  m.def("mesh_rs_reduce(Tensor(a!) out, float scale, bool accumulate, Tensor peers, Tensor(b!) state, int me, int ch, int region_off, int slot_bytes, int rank_stride, int slots, int heap_bytes, bool fp32_slots=False) -> ()");
   m.def("mesh_ep_plan(Tensor offsets, Tensor(a!) plan, int capacity, Tensor peers, Tensor(b!) state, int me, int ch, int region_off, int slot_bytes, int slots, int heap_bytes, int timeout) -> ()");
   m.def("mesh_push_rows(Tensor x, Tensor plan, bool combine, Tensor peers, Tensor(a!) state, int me, int ch, int region_off, int slot_bytes, int hdr_bytes, int slots, int slot_rows, int heap_bytes, int n_experts) -> ()");
   m.def("mesh_copy_rows(Tensor(a!) out, Tensor? nrows, Tensor peers, Tensor(b!) state, int me, int ch, int region_off, int slot_bytes, int hdr_bytes, int slots, int heap_bytes) -> ()");

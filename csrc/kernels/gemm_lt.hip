@@ -15,7 +15,7 @@
 // library build; ops/gemm.py keys its table by (shape, layouts, dtypes, beta) and records the
 // library version beside it. Operands may be row-major or transposed views (one unit stride);
 // the descriptors, layouts and resolved algorithm of each problem are cached, so a steady-state
-// call is one hipblasLtMatmul on the current HIP stream.
+// call is one hipblasLtMatmul on the current HIP stream, with that stream's own workspace.
 #include <ATen/hip/HIPContext.h>
 #include <c10/hip/HIPStream.h>
 #include <hipblaslt/hipblaslt-ext.hpp>
@@ -51,7 +51,10 @@ struct Problem {
 
 struct State {
   hipblasLtHandle_t handle = nullptr;
-  at::Tensor workspace;
+  // One scratch per (device, HIP stream), as torch keys its own hipBLASLt workspaces: stream-K / split-K solutions
+  // keep partial tiles and fix-up flags there, so two GEMMs on different streams must never share one. Each is
+  // allocated from the caching allocator while its stream is current and is never freed.
+  std::map<std::pair<int, hipStream_t>, at::Tensor> workspaces;
   std::map<Key, Problem> problems;
   std::mutex mu;
 };
@@ -100,8 +103,15 @@ Problem& problem(State& S, const at::Tensor& out, const at::Tensor& a, const at:
 
 void init(State& S) {
   if (S.handle == nullptr) LT_CHECK(hipblasLtCreate(&S.handle));
-  if (!S.workspace.defined() || S.workspace.device() != at::Device(at::kCUDA, c10::hip::current_device()))
-    S.workspace = at::empty({(int64_t)kWorkspace}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA));
+}
+
+// the workspace of the current (device, stream)
+void* workspace(State& S, hipStream_t stream) {
+  const int dev = c10::hip::current_device();
+  auto& w = S.workspaces[{dev, stream}];
+  if (!w.defined())
+    w = at::empty({(int64_t)kWorkspace}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA, dev));
+  return w.data_ptr();
 }
 
 void check_args(const at::Tensor& out, const at::Tensor& a, const at::Tensor& b) {
@@ -145,7 +155,7 @@ std::vector<hipblasLtMatmulHeuristicResult_t> heuristic(State& S, Problem& p, in
 void run(State& S, Problem& p, const hipblasLtMatmulAlgo_t* algo, const void* alpha, const void* beta,
          const at::Tensor& out, const at::Tensor& a, const at::Tensor& b, hipStream_t stream) {
   LT_CHECK(hipblasLtMatmul(S.handle, p.desc, alpha, b.data_ptr(), p.la, a.data_ptr(), p.lb, beta, out.data_ptr(),
-                           p.lc, out.data_ptr(), p.lc, algo, S.workspace.data_ptr(), kWorkspace, stream));
+                           p.lc, out.data_ptr(), p.lc, algo, workspace(S, stream), kWorkspace, stream));
 }
 
 }  // namespace
@@ -217,7 +227,7 @@ at::Tensor dlgm_gemm_lt_tune(const at::Tensor& out, const at::Tensor& a, const a
   std::vector<std::pair<float, int>> timed;
   for (size_t i = 0; i < cands.size(); ++i) {
     if (hipblasLtMatmul(S.handle, p.desc, &alpha, b.data_ptr(), p.la, a.data_ptr(), p.lb, &beta, scratch.data_ptr(),
-                        p.lc, scratch.data_ptr(), p.lc, &cands[i], S.workspace.data_ptr(), kWorkspace,
+                        p.lc, scratch.data_ptr(), p.lc, &cands[i], workspace(S, stream), kWorkspace,
                         stream) != HIPBLAS_STATUS_SUCCESS)
       continue;  // warm-up launch; a solution that fails to launch is skipped
     hipEventRecord(e0, stream);

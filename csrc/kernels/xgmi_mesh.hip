@@ -183,9 +183,28 @@ __device__ __forceinline__ bf16x8 to_bf16x8(const float* p) {
 
 __device__ __forceinline__ bf16x8 to_bf16x8(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
-// reduce-scatter, push half: chunk p of x ([W * n], fp32 or bf16) -> bf16 into slot `me` of rank p's RS region
-// (blockIdx.y = p). n % 8 == 0.
-template <typename TI>
+// reduce-scatter, push half: chunk p of x ([W * n], fp32 or bf16) -> slot `me` of rank p's RS region as TS (bf16: the
+// per-micro-batch scratch path; fp32: the once-per-step reduce of the fp32 local accumulator, no rounding before the
+// sum) (blockIdx.y = p). n % 8 == 0.
+__device__ __forceinline__ void store8(bf16* dst, const float* src) {
+  *reinterpret_cast<bf16x8*>(dst) = to_bf16x8(src);
+}
+__device__ __forceinline__ void store8(bf16* dst, const bf16* src) {
+  *reinterpret_cast<bf16x8*>(dst) = *reinterpret_cast<const bf16x8*>(src);
+}
+__device__ __forceinline__ void store8(float* dst, const float* src) {
+  *reinterpret_cast<f32x4*>(dst) = *reinterpret_cast<const f32x4*>(src);
+  *reinterpret_cast<f32x4*>(dst + 4) = *reinterpret_cast<const f32x4*>(src + 4);
+}
+__device__ __forceinline__ f32x8 load8f(const bf16* p) {
+  return __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p), f32x8);
+}
+__device__ __forceinline__ f32x8 load8f(const float* p) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+  return f32x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+template <typename TI, typename TS>
 __global__ __launch_bounds__(kThreads) void mesh_rs_push_kernel(const TI* __restrict__ x, int64_t n,
                                                                 const int64_t* peers, int64_t region_off,
                                                                 int64_t slot_bytes, int64_t rank_stride, int S,
@@ -193,17 +212,17 @@ __global__ __launch_bounds__(kThreads) void mesh_rs_push_kernel(const TI* __rest
   const int p = blockIdx.y;
   const int64_t e = get_word(st, kStEpoch + ch);
   const int row = get_word(st, kStShadow) ? p : me;
-  bf16* dst = reinterpret_cast<bf16*>(peers[p] + region_off + (e % S) * slot_bytes + row * rank_stride);
+  TS* dst = reinterpret_cast<TS*>(peers[p] + region_off + (e % S) * slot_bytes + row * rank_stride);
   const TI* src = x + (int64_t)p * n;
   const int64_t n8 = n / 8, stride = (int64_t)gridDim.x * kThreads;
-  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n8; i += stride)
-    *reinterpret_cast<bf16x8*>(dst + i * 8) = to_bf16x8(src + i * 8);
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n8; i += stride) store8(dst + i * 8, src + i * 8);
   last_block_signal(st, kStPushCtr + ch, peers, W, me, kData, ch, e);
 }
 
 // reduce-scatter, reduce half: out = [out +] (sum over ranks s = 0..W-1, in rank order, in fp32, of slot s) * scale
 // (unfused multiply and add: bit-reproducible against the same expression in PyTorch). Then ACK every rank.
-template <typename TO>
+// TS: the slot element type the push wrote.
+template <typename TO, typename TS>
 __global__ __launch_bounds__(kThreads) void mesh_rs_reduce_kernel(TO* __restrict__ out, int64_t n, float scale,
                                                                   int accumulate, const int64_t* peers,
                                                                   int64_t region_off, int64_t slot_bytes,
@@ -213,9 +232,10 @@ __global__ __launch_bounds__(kThreads) void mesh_rs_reduce_kernel(TO* __restrict
   const char* base = reinterpret_cast<const char*>(peers[me] + region_off + (e % S) * slot_bytes);
   const int64_t n8 = n / 8, stride = (int64_t)gridDim.x * kThreads;
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n8; i += stride) {
-    f32x8 acc = __builtin_convertvector(*reinterpret_cast<const bf16x8*>(base + i * 16), f32x8);
+    constexpr int64_t B8 = 8 * sizeof(TS);  // bytes of 8 slot elements
+    f32x8 acc = load8f(reinterpret_cast<const TS*>(base + i * B8));
     for (int s = 1; s < W; ++s) {
-      const f32x8 v = __builtin_convertvector(*reinterpret_cast<const bf16x8*>(base + s * rank_stride + i * 16), f32x8);
+      const f32x8 v = load8f(reinterpret_cast<const TS*>(base + s * rank_stride + i * B8));
 #pragma unroll
       for (int k = 0; k < 8; ++k) acc[k] = __fadd_rn(acc[k], v[k]);
     }
@@ -573,25 +593,30 @@ void dlgm_mesh_pull(at::Tensor out, const at::Tensor& peers, int64_t src_off, in
 
 void dlgm_mesh_rs_push(const at::Tensor& x, const at::Tensor& peers, at::Tensor state, int64_t me, int64_t ch,
                        int64_t region_off, int64_t slot_bytes, int64_t rank_stride, int64_t slots,
-                       int64_t heap_bytes) {
+                       int64_t heap_bytes, bool fp32_slots) {
   const int W = (int)peers.numel();
   check_geom(W, (int)me, (int)ch);
   TORCH_CHECK(x.is_cuda() && x.is_contiguous() && (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16),
               "mesh_rs_push: contiguous fp32 / bf16 GPU input");
   TORCH_CHECK(x.numel() % (8 * W) == 0, "mesh_rs_push: numel must be a multiple of 8 * W");
   const int64_t n = x.numel() / W;
-  TORCH_CHECK(n * 2 <= rank_stride && rank_stride % 16 == 0 && (int64_t)W * rank_stride <= slot_bytes &&
+  TORCH_CHECK(!fp32_slots || x.scalar_type() == at::kFloat, "mesh_rs_push: fp32 slots take an fp32 input");
+  TORCH_CHECK(n * (fp32_slots ? 4 : 2) <= rank_stride && rank_stride % 16 == 0 && (int64_t)W * rank_stride <= slot_bytes &&
                   region_off % 16 == 0 && region_off + slots * slot_bytes <= heap_bytes && slots >= 1,
               "mesh_rs_push: chunk does not fit the reduce-scatter slot");
   const unsigned gx = grid_for(n / 8, std::max(1, 1024 / W));
   dim3 grid(gx, W);
   auto s = c10::hip::getCurrentHIPStream();
-  if (x.scalar_type() == at::kFloat)
-    mesh_rs_push_kernel<float><<<grid, kThreads, 0, s>>>(x.data_ptr<float>(), n, peers_ptr(peers, W), region_off,
-                                                         slot_bytes, rank_stride, (int)slots, state_ptr(state),
-                                                         (int)ch, (int)me, W);
+  if (fp32_slots)
+    mesh_rs_push_kernel<float, float><<<grid, kThreads, 0, s>>>(x.data_ptr<float>(), n, peers_ptr(peers, W),
+                                                                region_off, slot_bytes, rank_stride, (int)slots,
+                                                                state_ptr(state), (int)ch, (int)me, W);
+  else if (x.scalar_type() == at::kFloat)
+    mesh_rs_push_kernel<float, bf16><<<grid, kThreads, 0, s>>>(x.data_ptr<float>(), n, peers_ptr(peers, W), region_off,
+                                                               slot_bytes, rank_stride, (int)slots, state_ptr(state),
+                                                               (int)ch, (int)me, W);
   else
-    mesh_rs_push_kernel<bf16><<<grid, kThreads, 0, s>>>(reinterpret_cast<const bf16*>(x.data_ptr()), n,
+    mesh_rs_push_kernel<bf16, bf16><<<grid, kThreads, 0, s>>>(reinterpret_cast<const bf16*>(x.data_ptr()), n,
                                                         peers_ptr(peers, W), region_off, slot_bytes, rank_stride,
                                                         (int)slots, state_ptr(state), (int)ch, (int)me, W);
   DLGM_CHECK_HIP(hipGetLastError());
@@ -599,7 +624,7 @@ void dlgm_mesh_rs_push(const at::Tensor& x, const at::Tensor& peers, at::Tensor 
 
 void dlgm_mesh_rs_reduce(at::Tensor out, double scale, bool accumulate, const at::Tensor& peers, at::Tensor state,
                          int64_t me, int64_t ch, int64_t region_off, int64_t slot_bytes, int64_t rank_stride,
-                         int64_t slots, int64_t heap_bytes) {
+                         int64_t slots, int64_t heap_bytes, bool fp32_slots) {
   const int W = (int)peers.numel();
   check_geom(W, (int)me, (int)ch);
   TORCH_CHECK(out.is_cuda() && out.is_contiguous() &&
@@ -607,20 +632,26 @@ void dlgm_mesh_rs_reduce(at::Tensor out, double scale, bool accumulate, const at
                   reinterpret_cast<uintptr_t>(out.data_ptr()) % 32 == 0,
               "mesh_rs_reduce: contiguous 32-byte aligned fp32 / bf16 GPU output");
   const int64_t n = out.numel();
-  TORCH_CHECK(n % 8 == 0 && n * 2 <= rank_stride && (int64_t)W * rank_stride <= slot_bytes &&
+  TORCH_CHECK(n % 8 == 0 && n * (fp32_slots ? 4 : 2) <= rank_stride && (int64_t)W * rank_stride <= slot_bytes &&
                   region_off + slots * slot_bytes <= heap_bytes && slots >= 1,
               "mesh_rs_reduce: shard does not fit the reduce-scatter slot");
   const unsigned gx = grid_for(n / 8, 1024);
   auto s = c10::hip::getCurrentHIPStream();
-  if (out.scalar_type() == at::kFloat)
-    mesh_rs_reduce_kernel<float><<<gx, kThreads, 0, s>>>(out.data_ptr<float>(), n, (float)scale, accumulate ? 1 : 0,
-                                                         peers_ptr(peers, W), region_off, slot_bytes, rank_stride,
-                                                         (int)slots, state_ptr(state), (int)ch, (int)me, W);
-  else
-    mesh_rs_reduce_kernel<bf16><<<gx, kThreads, 0, s>>>(reinterpret_cast<bf16*>(out.data_ptr()), n, (float)scale,
-                                                        accumulate ? 1 : 0, peers_ptr(peers, W), region_off,
-                                                        slot_bytes, rank_stride, (int)slots, state_ptr(state),
-                                                        (int)ch, (int)me, W);
+  auto go = [&](auto to, auto ts) {
+    using TO = decltype(to);
+    using TS = decltype(ts);
+    mesh_rs_reduce_kernel<TO, TS><<<gx, kThreads, 0, s>>>(reinterpret_cast<TO*>(out.data_ptr()), n, (float)scale,
+                                                          accumulate ? 1 : 0, peers_ptr(peers, W), region_off,
+                                                          slot_bytes, rank_stride, (int)slots, state_ptr(state),
+                                                          (int)ch, (int)me, W);
+  };
+  if (out.scalar_type() == at::kFloat) {
+    if (fp32_slots) go(float{}, float{});
+    else go(float{}, bf16{});
+  } else {
+    TORCH_CHECK(!fp32_slots, "mesh_rs_reduce: fp32 slots reduce into an fp32 output");
+    go(bf16{}, bf16{});
+  }
   DLGM_CHECK_HIP(hipGetLastError());
 }
 

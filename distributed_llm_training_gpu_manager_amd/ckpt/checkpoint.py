@@ -472,7 +472,7 @@ class AsyncCheckpointer:
             while self._falloc_done < off + ln and not res_err:
                 time.sleep(0.0005)
             if res_err:
-                raise RuntimeError(f"shm snapshot: {res_err[0]}")
+                raise _ReserveFailed(res_err[0])
             t1 = time.time()
             ev.synchronize()
             t2 = time.time()
@@ -515,10 +515,7 @@ class AsyncCheckpointer:
                     a, b = max(off, base), min(off + ln, base + src.numel())
                     if a < b:
                         self._snap[a:b].copy_(src[a - base:b - base], non_blocking=True)
-        try:
-            return self._ready_pipeline(hi, on_locked=dma)
-        except _ReserveFailed as e:
-            raise RuntimeError(f"shm snapshot: {e}") from e
+        return self._ready_pipeline(hi, on_locked=dma)  # _ReserveFailed: save() falls back to the host tier
 
     def prepare_async(self) -> None:
         """Reserve (and page-lock) the snapshot buffer on a background thread while training runs, so the
@@ -541,6 +538,46 @@ class AsyncCheckpointer:
                 "bf16": snap[12 * n:14 * n].view(self.engine.p16_shard.dtype)}
 
     # ------------------------------------------------------------------ save
+    def _capture_device(self, srcs) -> Optional[Tuple[int, List[int]]]:
+        """Queue the D2H capture of `srcs` (snapshot view, device tensor) on the checkpoint stream. shm tier: the
+        page-locked prefix by DMA; a save that came before the preparation finished page-locks the rest itself,
+        piece by piece, each piece's DMA queued as soon as it is locked (_lock_and_dma); anything that could not be
+        locked goes through the pinned slots (the returned CRCs). Raises _ReserveFailed when the rest of the shm file
+        cannot be reserved."""
+        dma_end = self._reg_done if (self.mode == "shm" and not self._pinned_shm) else self.snap_bytes
+        with torch.cuda.stream(self._stream):
+            for dst, s in srcs:
+                a = dst.data_ptr() - self._snap.data_ptr()
+                n_dma = max(0, min(dst.numel() * dst.element_size(), dma_end - a)) // dst.element_size()
+                if n_dma:
+                    self._copy_to_snap(dst[:n_dma], s[:n_dma])
+        if dma_end >= self.snap_bytes:
+            return None
+        segs = [(dst.data_ptr() - self._snap.data_ptr(), s.reshape(-1).view(torch.uint8)) for dst, s in srcs]
+        tr = time.time()
+        locked = self._lock_and_dma(segs, dma_end, self.snap_bytes) if not self._reg_failed else dma_end
+        self.last_ring.update(locked_bytes=locked - dma_end, lock_s=round(time.time() - tr, 3))
+        if locked >= self.snap_bytes:
+            return None
+        tr = time.time()
+        crcs = (locked, self._ring_capture(segs, locked, self.snap_bytes))
+        self.last_ring.update(bytes=self.snap_bytes - locked, s=round(time.time() - tr, 3))
+        return crcs
+
+    def _fall_back_to_host(self, why: str) -> None:
+        """shm tier -> pinned host tier inside a save: the DMAs already queued into the mapping finish before its
+        pages are unlocked and the file is dropped."""
+        self._stream.synchronize()
+        self._unregister_all()
+        self.tier_notes.append(f"shm snapshot failed during a save ({why}); snapshot tier -> host memory")
+        self.last_ring["fell_back_to_host"] = why
+        try:
+            os.unlink(self.shm_path)
+        except OSError:
+            pass
+        self.mode = "host"
+        self._snap = torch.empty(self.snap_bytes, dtype=torch.uint8, pin_memory=self.cuda)
+
     def save(self, step: int, client_state: Optional[Dict[str, Any]] = None, blocking: bool = False) -> str:
         t0 = time.time()
         tag = _tag(step)
@@ -574,25 +611,17 @@ class AsyncCheckpointer:
         if self.cuda:
             cur = torch.cuda.current_stream(self.dev)
             self._stream.wait_stream(cur)
-            # shm tier: the page-locked prefix by DMA; a save that came before the preparation finished page-locks the
-            # rest itself, piece by piece, each piece's DMA queued as soon as it is locked (_lock_and_dma); anything
-            # that could not be locked goes through the pinned slots
-            dma_end = self._reg_done if (self.mode == "shm" and not self._pinned_shm) else self.snap_bytes
-            with torch.cuda.stream(self._stream):
-                for dst, s in srcs:
-                    a = dst.data_ptr() - self._snap.data_ptr()
-                    n_dma = max(0, min(dst.numel() * dst.element_size(), dma_end - a)) // dst.element_size()
-                    if n_dma:
-                        self._copy_to_snap(dst[:n_dma], s[:n_dma])
-            if dma_end < self.snap_bytes:
-                segs = [(dst.data_ptr() - self._snap.data_ptr(), s.reshape(-1).view(torch.uint8)) for dst, s in srcs]
-                tr = time.time()
-                locked = self._lock_and_dma(segs, dma_end, self.snap_bytes) if not self._reg_failed else dma_end
-                self.last_ring.update(locked_bytes=locked - dma_end, lock_s=round(time.time() - tr, 3))
-                if locked < self.snap_bytes:
-                    tr = time.time()
-                    ring_crcs = (locked, self._ring_capture(segs, locked, self.snap_bytes))
-                    self.last_ring.update(bytes=self.snap_bytes - locked, s=round(time.time() - tr, 3))
+            try:
+                ring_crcs = self._capture_device(srcs)
+            except _ReserveFailed as e:
+                # the tmpfs filled up while this save reserved the rest of the snapshot file (an early spot notice
+                # that interrupted the background preparation): the emergency checkpoint must still happen, so the
+                # state goes to a pinned host buffer instead, the way _alloc_snapshot falls back
+                self._fall_back_to_host(str(e))
+                v = self._views(self._snap)
+                srcs = [(v["master"], eng.master), (v["exp_avg"], eng.exp_avg), (v["exp_avg_sq"], eng.exp_avg_sq),
+                        (v["bf16"], eng.p16_shard)]
+                ring_crcs = self._capture_device(srcs)
             with torch.cuda.stream(self._stream):
                 ev = torch.cuda.Event()
                 ev.record(self._stream)
@@ -1054,6 +1083,11 @@ class AsyncCheckpointer:
         self._moments = None
         if self._await_moments in self.engine.pre_step_hooks:
             self.engine.pre_step_hooks.remove(self._await_moments)
+        # every rank deferred its moments (the same restore decision), so every rank reaches this point once, before
+        # its first optimizer collective: agree on the outcome there. A checksum failure on ONE rank then fails every
+        # rank together (the coordinated rollback load() promises), instead of leaving the healthy ranks blocked in
+        # the gradient-statistics all-reduce until the process-group timeout
+        ok = _Agree(self.engine).min(0.0 if self._moments_err is not None else 1.0)
         if self._moments_err is not None:
             try:
                 with open(self.shm_src_meta + ".bad", "w") as f:
@@ -1061,6 +1095,8 @@ class AsyncCheckpointer:
             except OSError:
                 pass
             raise CorruptCheckpoint(f"shm snapshot: Adam moments failed to restore: {self._moments_err}")
+        if ok < 1.0:
+            raise CorruptCheckpoint("shm snapshot: Adam moments failed to restore on another rank")
         if self._moments_ev is not None:
             torch.cuda.current_stream(self.dev).wait_event(self._moments_ev)
 

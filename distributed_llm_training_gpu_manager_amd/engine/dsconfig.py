@@ -96,6 +96,9 @@ def engine_config_from_ds(ds: Union[str, Dict[str, Any]], seq_len: int, model_cf
         cfg.ep_capacity_factor = None if v in (None, "dropless", "auto") else float(v)
     if mi.get("comm_dtype"):
         cfg.comm_dtype = {"fp32": torch.float32, "float32": torch.float32}.get(mi["comm_dtype"], torch.bfloat16)
+    if mi.get("step_comm_dtype"):  # the once-per-step reduce of the local fp32 accumulator (default fp32)
+        cfg.step_comm_dtype = {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16}.get(mi["step_comm_dtype"],
+                                                                                      torch.float32)
     if auto_mbs:
         _auto_micro_batch(cfg, ds, model_cfg, world, notes)
     for k, v in overrides.items():

@@ -30,13 +30,47 @@ import torch
 from ..ckpt.checkpoint import AsyncCheckpointer, export_consolidated
 from ..health.loss_monitor import json_safe, LossSpikeMonitor, MonitorConfig, TrainingMetrics
 from ..health.nan_trap import NanTrap
-from ..launcher.supervisor import EXIT_NAN_HALT, EXIT_PREEMPTED, EXIT_TRANSPORT, write_heartbeat, write_status
+from ..launcher.supervisor import (EXIT_EP_OVERFLOW, EXIT_NAN_HALT, EXIT_PREEMPTED, EXIT_TRANSPORT, write_heartbeat,
+                                   write_status)
 from ..models import get_config
 from ..parallel.comm import Comm, init_distributed
 from ..parallel.zero import EngineConfig, ZeroEngine
 from ..utils.profiling import trace_window
 from .dsconfig import engine_config_from_ds
 
+
+
+class HeartbeatTicker:
+    """Heartbeats from a side thread while this rank blocks outside the step loop -- the final checkpoint write-out,
+    export_consolidated, a blocking emergency save, a save waiting for the previous write-out: the
+    supervisor's hang bound is sized to the step time, and those phases can take minutes on a large model or a slow
+    disk. The beats carry ``phase`` (BLOCKING_PHASES: the supervisor applies its start-up bound) and
+    ``blocked_since`` (a block longer than BLOCK_LIMIT_MULT bounds is still a hang)."""
+
+    def __init__(self, rank: int, step: int, phase: str, interval_s: float = 5.0):
+        self.rank, self.step, self.phase, self.interval_s = rank, step, phase, interval_s
+        self._stop = threading.Event()
+        self._t: Optional[threading.Thread] = None
+
+    def _beat(self, since: float) -> None:
+        write_heartbeat(self.rank, self.step, phase=self.phase, blocked_since=since)
+
+    def __enter__(self):
+        since = time.time()
+        self._beat(since)
+
+        def run():
+            while not self._stop.wait(self.interval_s):
+                self._beat(since)
+        self._t = threading.Thread(target=run, daemon=True, name=f"heartbeat-{self.phase}")
+        self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        if self._t is not None:
+            self._t.join()
+        return False
 
 class SyntheticData:
     """Deterministic random token batches: (seed, rank, step, micro) -> the same tokens after a restart."""
@@ -310,7 +344,9 @@ class Trainer:
                 self.engine.check_transport()
             except RuntimeError as e:
                 self._say(str(e))
-            return EXIT_TRANSPORT
+            word = int(rec["transport"])
+            # word 1: a wait timed out (resumable); word 2 alone: an explicit EP capacity overflowed (not resumable)
+            return EXIT_EP_OVERFLOW if (word & 2) and not (word & 1) else EXIT_TRANSPORT
         if rec["nonfinite"] > 0 and a.halt_on_nan:
             self._say(f"NaN/Inf gradients at step {rec['step']} ({int(rec['nonfinite'])} elements): update skipped "
                       f"on device; halting")
@@ -352,6 +388,7 @@ class Trainer:
         self._reports, self._last_step_s, self._last_reported = 0, None, start
         self._step_timing = int(os.environ.get("DLGM_STEP_TIMING", "0") or 0)
         write_heartbeat(self.env.rank, start, phase="ready")  # restored / initialised: the first step is next
+        self._hb_tick = float(os.environ.get("DLGM_HEARTBEAT_TICK_S", "5"))
         self.engine.sync_flags = self.env.world > 1
         first_attempt = os.environ.get("DLGM_RESTART", "0") == "0"
         self._notice_sent = False
@@ -407,8 +444,9 @@ class Trainer:
                 if self._prep_after_first:
                     self._prep_after_first = False
                     self.ckpt.prepare_async()
-                if save_due:
-                    self.ckpt.save(step, client_state={"step": step, "global_batch": self.global_batch})
+                if save_due:  # may wait for the previous write-out
+                    with HeartbeatTicker(self.env.rank, step, "saving", self._hb_tick):
+                        self.ckpt.save(step, client_state={"step": step, "global_batch": self.global_batch})
             else:
                 prev = (step, issued)
             if a.kill_at_step == step and first_attempt and self.env.rank == a.kill_rank:
@@ -435,8 +473,9 @@ class Trainer:
                         break
                 t0 = time.time()
                 if self.ckpt is not None:
-                    self.ckpt.save(step, client_state={"step": step, "preempted": True,
-                                                          "global_batch": self.global_batch}, blocking=True)
+                    with HeartbeatTicker(self.env.rank, step, "saving", self._hb_tick):
+                        self.ckpt.save(step, client_state={"step": step, "preempted": True,
+                                                              "global_batch": self.global_batch}, blocking=True)
                 self._say(f"preemption: emergency checkpoint at step {step} in {time.time() - t0:.2f}s; exiting")
                 if self.ckpt is not None and self.ckpt.history:
                     self._say("emergency checkpoint record: " + json.dumps(json_safe(self.ckpt.history[-1])))
@@ -448,8 +487,9 @@ class Trainer:
         if rc == 0 and self.preempt and self.env.world == 1:
             # a notice that arrived after the last step was queued (one rank: no agreement needed)
             if self.ckpt is not None:
-                self.ckpt.save(last, client_state={"step": last, "preempted": True,
-                                                      "global_batch": self.global_batch}, blocking=True)
+                with HeartbeatTicker(self.env.rank, last, "saving", self._hb_tick):
+                    self.ckpt.save(last, client_state={"step": last, "preempted": True,
+                                                          "global_batch": self.global_batch}, blocking=True)
             rc = EXIT_PREEMPTED
         if self.env.device.type == "cuda":
             dv = self.env.device
@@ -459,7 +499,8 @@ class Trainer:
                 "alloc_retries": int(torch.cuda.memory_stats(dv).get("num_alloc_retries", 0)),
                 "hbm_GiB": round(torch.cuda.get_device_properties(dv).total_memory / 2 ** 30, 1)}))
         if self.ckpt is not None:
-            self.ckpt.wait()
+            with HeartbeatTicker(self.env.rank, last, "finishing", self._hb_tick):
+                self.ckpt.wait()
             if self.ckpt.prep_stats:
                 ps = dict(self.ckpt.prep_stats)
                 t0 = ps.pop("started_at", None)
@@ -468,7 +509,8 @@ class Trainer:
                     ps["started_after_process_s"] = round(t0 - self.timeline["process_start"], 2)
                 self._say("ckpt prepare: " + json.dumps(ps))
             if rc == 0 and a.export:
-                export_consolidated(self.engine, a.export)
+                with HeartbeatTicker(self.env.rank, last, "finishing", self._hb_tick):
+                    export_consolidated(self.engine, a.export)
             # a finished job has nothing to resume: give the host RAM of the shm snapshot tier back
             self.ckpt.close(discard_shm=rc == 0)
         self.trap.close()

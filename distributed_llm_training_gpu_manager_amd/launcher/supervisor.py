@@ -45,7 +45,10 @@ from typing import Dict, List, Optional
 
 EXIT_NAN_HALT = 3
 EXIT_PREEMPTED = 4
-EXIT_TRANSPORT = 5  # xGMI mesh wait timed out / EP capacity overflow: resumed like a crash
+EXIT_TRANSPORT = 5  # an xGMI mesh wait timed out (a peer died or stalled): resumed like a crash
+# an EP routing overflowed an explicit ep_capacity_factor: a deterministic configuration error -- the resumed job would
+# replay the same routing and overflow again, so it is not auto-resumed
+EXIT_EP_OVERFLOW = 6
 
 
 @dataclass
@@ -211,6 +214,15 @@ class Supervisor(threading.Thread):
             b = beats.get(r)
             if b is None:  # never beat in this attempt: the startup bound (at least the steady-state one)
                 age, bound = now - attempt_t0, max(spec.startup_timeout_s, timeout)
+            elif b.get("phase") in BLOCKING_PHASES:
+                # a blocking checkpoint write-out / export (engine/trainer.py HeartbeatTicker): the rank beats from a
+                # ticker thread meanwhile, under the start-up bound; a block that outlasts BLOCK_LIMIT_MULT start-up
+                # bounds is a hang even while the ticker runs (a deadlocked writer, a collective that never returns)
+                bound = max(spec.startup_timeout_s, timeout)
+                age = now - float(b.get("time", attempt_t0))
+                since = float(b.get("blocked_since") or b.get("time", attempt_t0))
+                if now - since > BLOCK_LIMIT_MULT * bound:
+                    age, bound = now - since, BLOCK_LIMIT_MULT * bound
             elif not b.get("step_s") and spec.heartbeat_timeout_s < 0:
                 # ready, no step finished yet (restore, warm-up, the first step): no step time to scale by
                 age, bound = now - float(b.get("time", attempt_t0)), max(spec.startup_timeout_s, timeout)
@@ -317,6 +329,10 @@ class Supervisor(threading.Thread):
             if preempted and not spec.restart_on_preempt:
                 job.status = "preempted"
                 break
+            if rc == EXIT_EP_OVERFLOW:
+                job.status = "failed"
+                job.event("ep_capacity_overflow", hint="raise mi355x.ep_capacity_factor or use the dropless default")
+                break
             nan = rc == EXIT_NAN_HALT
             if nan:
                 job.nan_halts += 1
@@ -418,6 +434,11 @@ def write_status(step: int, **kw) -> None:
     if not path:
         return
     _write_json(path, {"step": step, "time": time.time(), "restart": int(os.environ.get("DLGM_RESTART", "0")), **kw})
+
+
+# heartbeat phases written while a rank blocks outside the step loop (final checkpoint flush, export, emergency save)
+BLOCKING_PHASES = ("saving", "finishing")
+BLOCK_LIMIT_MULT = 4.0
 
 
 def write_heartbeat(rank: int, step: int, **kw) -> None:

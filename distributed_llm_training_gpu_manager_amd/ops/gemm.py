@@ -155,19 +155,25 @@ def _f16_load() -> None:
 
 
 def _f16_persist(key: str, idx: int) -> None:
-    """Merge one timed pick into the host cache (atomic replace): every later process reuses it."""
+    """Merge one timed pick into the host cache (atomic replace): every later process reuses it. The
+    read-merge-replace holds an exclusive lock on a sidecar file, so ranks tuning at the same time never drop each
+    other's picks (a lost pick would be re-timed later and could differ: different bits across processes)."""
+    import fcntl
     path = _f16_cache_path()
     try:
         path.parent.mkdir(parents=True, exist_ok=True)
-        cur = {}
-        if path.exists():
-            with open(path) as f:
-                cur = json.load(f).get("solutions", {})
-        cur.setdefault(key, idx)
-        tmp = path.with_suffix(f".{os.getpid()}.tmp")
-        with open(tmp, "w") as f:
-            json.dump({"solutions": cur}, f, indent=1, sort_keys=True)
-        os.replace(tmp, path)
+        with open(path.with_suffix(".lock"), "a") as lk:
+            fcntl.flock(lk, fcntl.LOCK_EX)
+            cur = {}
+            if path.exists():
+                with open(path) as f:
+                    cur = json.load(f).get("solutions", {})
+            cur.setdefault(key, idx)
+            _F16_PICK[key] = int(cur[key])  # a pick another process recorded first wins here too
+            tmp = path.with_suffix(f".{os.getpid()}.tmp")
+            with open(tmp, "w") as f:
+                json.dump({"solutions": cur}, f, indent=1, sort_keys=True)
+            os.replace(tmp, path)
     except (OSError, ValueError):
         pass
 
@@ -186,6 +192,7 @@ def _f16_solution(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, beta: flo
         idx = int(res[0, 0]) if res.shape[0] else -1
         _F16_PICK[key] = idx
         _f16_persist(key, idx)
+        idx = _F16_PICK[key]
     return idx
 
 

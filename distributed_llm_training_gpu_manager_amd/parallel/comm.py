@@ -60,6 +60,31 @@ class DistEnv:
     device: torch.device = torch.device("cpu")
 
 
+# RCCL / ProcessGroupNCCL settings applied before the process group is formed (setdefault: an operator's own value
+# always wins). SURVEY.md §5.8: the 8 MI355X of a node are a full xGMI mesh, 7 point-to-point links per GPU (~153 GB/s
+# each), so one ring is bound by one link; RCCL needs several channels per link direction to cover all of them
+# (7 links x 2 directions x 2 = 28 -> 32 channels). NCCL_MIN_NCHANNELS only RAISES RCCL's own choice, and the
+# collectives of the default plan (one all-gather per unit per step, one reduce-scatter per step, overlapped with
+# compute) are few, so the 32 workgroups it can take while a collective runs are a small, bounded cost.
+# TORCH_NCCL_AVOID_RECORD_STREAMS: ProcessGroupNCCL keeps each collective's tensors alive until its work is waited
+# for instead of record_stream-ing them to its pool-drawn streams; the engine's gather run-ahead limiter
+# (parallel/zero.py _bound_run_ahead) then governs when a gathered buffer's block is reused, with no allocator
+# events deferred behind RCCL's streams.
+RCCL_ENV_DEFAULTS = {
+    "TORCH_NCCL_AVOID_RECORD_STREAMS": "1",
+    "NCCL_MIN_NCHANNELS": "32",
+}
+
+
+def rccl_env(apply: bool = True) -> dict:
+    """Apply the RCCL defaults (unless already set) and return every RCCL / NCCL / torch-NCCL variable in effect."""
+    if apply:
+        for k, v in RCCL_ENV_DEFAULTS.items():
+            os.environ.setdefault(k, v)
+    return {k: v for k, v in sorted(os.environ.items())
+            if k.startswith(("NCCL_", "RCCL_", "TORCH_NCCL_", "HSA_ENABLE_IPC"))}
+
+
 def init_distributed(device_type: str = "auto", timeout_s: Optional[int] = None) -> DistEnv:
     """Initialise the default process group from torchrun-style env vars (idempotent). The collective timeout is
     ``DLGM_PG_TIMEOUT_S`` when set (the supervisor sets it to its hang bound), else 1800 s (torch's default)."""
@@ -81,6 +106,8 @@ def init_distributed(device_type: str = "auto", timeout_s: Optional[int] = None)
     if (world > 1 or launched) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
+        if backend == "nccl":
+            rccl_env()
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
             kw["device_id"] = device

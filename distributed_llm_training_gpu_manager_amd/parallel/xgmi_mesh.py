@@ -118,6 +118,10 @@ class XgmiMesh:
                         ptrs[r] = p
         self.peers = torch.tensor(ptrs, dtype=torch.int64, device=device)
         self.state = torch.zeros(int(ops.mesh_state_words()), dtype=torch.int64, device=device)
+        # per-channel epoch / counter words, updated by device-side atomics from the mesh's several streams: ordered
+        # by the protocol in xgmi_mesh.hip, not by stream edges (the stream audit leaves them to that protocol)
+        from ..utils.stream_audit import protocol_memory
+        protocol_memory(self.state, "xGMI mesh state words (device atomics, one word set per channel)")
         if self.shadow:
             self.state[ST_SHADOW] = 1
         self.timeout_ticks = int(timeout_s * 100e6)  # s_memrealtime runs at 100 MHz on MI355X
@@ -226,12 +230,14 @@ class XgmiMesh:
         hip_ops().mesh_pull(out, self.peers, off, self.heap_bytes)
 
     def reduce_scatter(self, out: torch.Tensor, x: torch.Tensor, scale: float, accumulate: bool,
-                       region: str = "rs") -> None:
-        """out (+)= scale * sum over ranks of x[rank's chunk] (fp32 sum of the bf16-rounded chunks, rank order)."""
+                       region: str = "rs", fp32: bool = False) -> None:
+        """out (+)= scale * sum over ranks of x[rank's chunk], summed in fp32 in rank order. The chunks travel as bf16
+        (rounded on the fly) or, with ``fp32`` (an fp32 `x`: the once-per-step reduce of the local accumulator), as
+        fp32: the same sum RCCL's fp32 reduce-scatter computes, up to the order of the fp32 additions."""
         r = self.regions[region]
         rank_stride = r.slot_bytes // self.W // 256 * 256
         args = (self.peers, self.state, self.rank, CH_RS, r.offset, r.slot_bytes, rank_stride, r.slots,
-                self.heap_bytes)
+                self.heap_bytes, bool(fp32))
         self.begin(CH_RS, r.slots)
         hip_ops().mesh_rs_push(x.contiguous(), *args)
         self.wait_data(CH_RS)

@@ -87,6 +87,12 @@ class EngineConfig:
     warmup_min_lr: float = 0.0
     warmup_type: str = "log"  # DeepSpeed WarmupLR default
     comm_dtype: torch.dtype = torch.bfloat16
+    # dtype of the ONCE-per-step reduce-scatter of the fp32 local gradient accumulator (local_grad_accum): fp32 by
+    # default -- RCCL's ring and the xGMI mesh then reduce the same fp32 values (no bf16 rounding before the sum,
+    # equal up to the order of the fp32 additions), for 2x the bytes of one reduce-scatter per step, overlapped with
+    # the last backward. comm_dtype (DeepSpeed communication_data_type) keeps governing the
+    # per-micro-batch reduce-scatters of the scratch path.
+    step_comm_dtype: torch.dtype = torch.float32
     activation_checkpointing: bool = False
     cpu_checkpointing: bool = False
     prefetch: bool = True
@@ -505,7 +511,9 @@ class ZeroEngine:
         dense = [g for g in self.groups if self._mesh_group(g)]
         regions = {"p16": (self.shard_total * 2, 1)}
         if dense and self.stage in (2, 3):
-            regions["rs"] = (rs_region_bytes(self.W, max(g.shard_numel for g in dense)), 2)
+            # fp32 slots when the once-per-step reduce of the local accumulator travels in fp32
+            esz = 4 if (self._want_local_grads() and c.step_comm_dtype == torch.float32) else 2
+            regions["rs"] = (rs_region_bytes(self.W, max(g.shard_numel for g in dense), esz), 2)
         self.mesh = XgmiMesh(self.comm, self.device, regions, c.mesh_timeout_s)
         if self.ep_size > 1 and self.ep_comm is not None and self.ep_comm.world > 1:
             from .ep import MeshExpertDispatcher
@@ -652,7 +660,7 @@ class ZeroEngine:
         if isinstance(v, str):
             if v not in ("hbm", "auto"):
                 raise ValueError(f"local_grad_accum must be a bool or 'hbm', got {v!r}")
-            if self.cfg.grad_accum <= 1 or not self.is_cuda:
+            if self.cfg.grad_accum <= 1 or self.device.type != "cuda":
                 return False
             hbm = torch.cuda.get_device_properties(self.device).total_memory
             return self.gfull_total * 4 <= self.cfg.local_grad_hbm_fraction * hbm
@@ -772,7 +780,13 @@ class ZeroEngine:
                 ev.record(self._h2d)
                 return stage, Handle(post=lambda: torch.cuda.current_stream(self.device).wait_event(ev))
             buf = torch.empty(g.numel, dtype=self.dtype, device=self.device)
-            return buf, g.gcomm.all_gather(buf, stage, async_op=True)
+            h = g.gcomm.all_gather(buf, stage, async_op=True)
+            # the gather was issued on the H2D stream: the consumer waits for the collective (RCCL work) AND for the
+            # H2D stream itself -- a communicator that runs the gather inline on the issuing stream (a synchronous
+            # shadow rank) returns a done handle, and the compute stream would read buf unordered (stream audit)
+            ev = torch.cuda.Event()
+            ev.record(self._h2d)
+            return buf, Handle(post=lambda: (h.wait(), torch.cuda.current_stream(self.device).wait_event(ev)))
 
     # ------------------------------------------------------------------ params
     def _all_gather(self, g: FlatGroup, out: torch.Tensor, shard: torch.Tensor) -> Handle:
@@ -991,23 +1005,25 @@ class ZeroEngine:
             # EP size so expert grads are the global mean like the dense grads (which are AVG-reduced)
             tgt.mul_(1.0 / self.ep_size)
         avg, post = not self.cfg.prescale_gradients, self._post(g)
-        if (g.P > 1 and self.local_grads and self.cfg.comm_dtype == torch.bfloat16 and tgt.dtype == torch.float32
+        step_dt = self.cfg.step_comm_dtype
+        if (g.P > 1 and self.local_grads and step_dt in (torch.bfloat16, torch.float32) and tgt.dtype == torch.float32
                 and self._mesh_ok(g, tgt)):
-            # mesh: the fp32 accumulator is cast to bf16 on the fly as it is pushed; the reduce writes the shard
+            # mesh: the fp32 accumulator is pushed as fp32 (or cast to bf16 on the fly); the reduce writes the shard
             shard_tgt = self._st_grad_shard.narrow(0, g.shard_off, g.shard_numel)
             scale = (1.0 / g.comm.world if avg else 1.0) * post
             m = self.mesh
-            h = m.run_async(lambda: m.reduce_scatter(shard_tgt, tgt, scale, False), [tgt, shard_tgt], "rs")
+            f32 = step_dt == torch.float32
+            h = m.run_async(lambda: m.reduce_scatter(shard_tgt, tgt, scale, False, fp32=f32), [tgt, shard_tgt], "rs")
             pending.append((h, _Scaled(shard_tgt, 1.0, tgt)))
-        elif g.P > 1 and self.local_grads and self.cfg.comm_dtype != tgt.dtype:
-            # ZeRO-2/3 local accumulation: one reduce-scatter per step in comm_dtype (half the bytes of
-            # fp32), then the shard is written (beta = 0) from the reduced chunk
-            src = tgt.to(self.cfg.comm_dtype)
+        elif g.P > 1 and self.local_grads and step_dt != tgt.dtype:
+            # ZeRO-2/3 local accumulation, reduced in a 16-bit step_comm_dtype: half the bytes of fp32, then the
+            # shard is written (beta = 0) from the reduced chunk
+            src = tgt.to(step_dt)
             out = torch.empty(g.shard_numel, dtype=src.dtype, device=self.device)
             shard_tgt = self._st_grad_shard.narrow(0, g.shard_off, g.shard_numel)
             pending.append((g.comm.reduce_scatter(out, src, avg=avg, async_op=True),
                             (shard_tgt, out, 0.0, None, post, src)))
-        elif g.P > 1:  # ZeRO-1 (or fp32 comm): reduce-scatter the local accumulator into this rank's shard
+        elif g.P > 1:  # ZeRO-1, or fp32 step comm: reduce-scatter the local accumulator into this rank's shard
             out = self._st_grad_shard.narrow(0, g.shard_off, g.shard_numel)
             pending.append((g.comm.reduce_scatter(out, tgt, avg=avg, async_op=True), _Scaled(out, post, tgt)))
         elif g.comm.world > 1:  # ZeRO-0 / persistent (replicated) group: plain data parallel

@@ -74,6 +74,8 @@ def dedicated_stream(device: torch.device, name: str) -> "torch.cuda.Stream":
             s = _STREAMS.get(key)
             if s is None:
                 s = _STREAMS[key] = _new_stream(idx)
+                from .stream_audit import _NAMES
+                _NAMES[int(s.cuda_stream)] = name  # reports of the stream audit name the queue
     return s
 
 

@@ -105,6 +105,44 @@ def test_shm_restore_defers_moments_behind_the_first_step(tmp_path):
     AsyncCheckpointer(_engine(), str(tmp_path), shm=True, disk=False).close(discard_shm=True)
 
 
+@pytest.mark.gpu
+def test_shm_save_falls_back_to_host_when_the_reservation_fails(tmp_path, monkeypatch):
+    """an early save reserves the rest of the shm file itself; when the tmpfs fills up there (a failed
+    posix_fallocate), the save must not crash and lose the emergency checkpoint: it drops the shm file and captures
+    the state into a pinned host buffer instead."""
+    from distributed_llm_training_gpu_manager_amd.ckpt import checkpoint as C
+
+    monkeypatch.setattr(C, "REG_CHUNK", 64 << 20)
+    monkeypatch.setattr(C, "REG_PAUSE_S", 0.05)
+    e = _engine()
+    t = torch.randint(0, 32768, (1, 257), device="cuda")
+    e.train_step([(t[:, :-1], t[:, 1:])])
+    ck = C.AsyncCheckpointer(e, str(tmp_path), shm=True, disk=False)
+    assert ck.mode == "shm" and ck.snap_bytes > 4 * (64 << 20)
+    ck.prepare_async()
+    time.sleep(0.12)  # a few pieces prepared, most not
+    real, calls = ck._reserve, []
+
+    def full_after_two(fd, off, ln):
+        calls.append(off)
+        if len(calls) > 2:
+            ck.tier_notes.append("No space left on device (simulated)")
+            return False
+        return real(fd, off, ln)
+    monkeypatch.setattr(ck, "_reserve", full_after_two)
+    ck.save(1, {"step": 1}, blocking=True)
+    rec = ck.history[-1]
+    assert ck.mode == "host" and rec["mode"] == "host", rec
+    assert any("snapshot tier -> host memory" in n for n in ck.tier_notes), ck.tier_notes
+    assert not os.path.exists(ck.shm_path) and not os.path.exists(ck.shm_meta)
+    assert torch.equal(ck._snap[:4 * ck.n].view(torch.float32), e.master.cpu())
+    e.train_step([(t[:, :-1], t[:, 1:])])
+    ck.save(2, {"step": 2}, blocking=True)  # later saves keep working on the host tier
+    assert torch.equal(ck._snap[:4 * ck.n].view(torch.float32), e.master.cpu())
+    ck.close()
+
+
+
 @pytest.mark.parametrize("register_fails", [False, True])
 def test_shm_save_before_preparation_finishes(tmp_path, monkeypatch, register_fails):
     """An early save (a spot notice in the first steps) interrupts the background reservation / page-locking: the

@@ -96,3 +96,42 @@ def test_sigstopped_rank_is_detected_and_job_resumes_at_full_world(tmp_path):
     assert "resumed from step 2" in log
     d = [torch.load(os.path.join(tmp_path / "dump", f"rank{r}.pt"), weights_only=True) for r in range(4)]
     assert [x["rc"] for x in d] == [0] * 4 and all(x["step_count"] == 6 for x in d)
+
+
+def test_blocking_phases_get_the_startup_bound_and_a_ticker(tmp_path, monkeypatch):
+    """a rank blocked in the final checkpoint write-out / export beats from a ticker thread with
+    phase 'saving' / 'finishing'; the supervisor gives those beats the start-up bound, and a block that outlasts
+    BLOCK_LIMIT_MULT such bounds is still named hung (a deadlocked writer keeps ticking)."""
+    from distributed_llm_training_gpu_manager_amd.engine.trainer import HeartbeatTicker
+    from distributed_llm_training_gpu_manager_amd.launcher.supervisor import BLOCK_LIMIT_MULT
+
+    job = Job(JobSpec(job_id="hb2", argv=["x", "--nproc-per-node", "1"], run_dir=str(tmp_path / "run"),
+                      heartbeat_min_s=10.0, startup_timeout_s=100.0))
+    sup = Supervisor(job)
+    t0 = 1000.0
+    d = job.heartbeat_dir
+    os.makedirs(d, exist_ok=True)
+
+    def beat(**kw):
+        with open(os.path.join(d, "rank0.json"), "w") as f:
+            json.dump({"rank": 0, "step": 9, "restart": 0, **kw}, f)
+    # steady 2 s steps: the bound is 20 s; a 'finishing' beat 60 s old is within the 100 s start-up bound
+    beat(time=t0 + 10, phase="finishing", blocked_since=t0 + 10)
+    assert sup.hung_rank(t0, 1, now=t0 + 70) is None
+    assert sup.hung_rank(t0, 1, now=t0 + 120)["rank"] == 0  # the ticker died: past the start-up bound
+    # a ticker still beating, but blocked for longer than BLOCK_LIMIT_MULT start-up bounds
+    beat(time=t0 + 500, phase="saving", blocked_since=t0 + 200)
+    assert sup.hung_rank(t0, 1, now=t0 + 501) is None
+    beat(time=t0 + 600, phase="saving", blocked_since=t0 + 200)
+    h = sup.hung_rank(t0, 1, now=t0 + 200 + BLOCK_LIMIT_MULT * 100 + 1)
+    assert h is not None and h["bound_s"] == BLOCK_LIMIT_MULT * 100
+
+    # the ticker itself: fresh beats while the body blocks, phase and blocked_since recorded
+    monkeypatch.setenv("DLGM_HEARTBEAT_DIR", str(tmp_path / "hb"))
+    path = tmp_path / "hb" / "rank3.json"
+    with HeartbeatTicker(3, 41, "finishing", interval_s=0.1):
+        first = json.loads(path.read_text())
+        time.sleep(0.35)
+        later = json.loads(path.read_text())
+    assert first["phase"] == later["phase"] == "finishing" and first["step"] == 41
+    assert later["time"] > first["time"] and later["blocked_since"] == first["blocked_since"]

@@ -651,3 +651,35 @@ def test_checkpoint_module_holds_16bit_weights(tmp_path, model, stage, ep):
     assert got["step"] == 2
     for k, v in want.items():
         assert torch.equal(got["params"][k], v), k
+
+
+def _moments_worker(rank, world, port, path, out):
+    _init(rank, world, port)
+    import threading
+    from distributed_llm_training_gpu_manager_amd.ckpt.checkpoint import AsyncCheckpointer, CorruptCheckpoint
+    eng = ZeroEngine(_model("llama-tiny"), _cfg(2, 1), torch.device("cpu"), Comm())
+    ck = AsyncCheckpointer(eng, os.path.join(path, f"r{rank}"), shm=False, disk=False)
+    # a deferred Adam-moment restore (shm tier, GPU) that failed its checksum on rank 1 only
+    ck._moments = threading.Thread(target=lambda: None)
+    ck._moments.start()
+    ck._moments_err = CorruptCheckpoint("checksum mismatch") if rank == 1 else None
+    ck._moments_ev = None
+    ck.shm_src_meta = os.path.join(path, f"meta{rank}.json")
+    try:
+        ck._await_moments()
+        res = "ok"
+    except CorruptCheckpoint as e:
+        res = str(e)
+    with open(os.path.join(out, f"{rank}.txt"), "w") as f:
+        f.write(res)
+    dist.destroy_process_group()
+
+
+def test_deferred_moment_failure_on_one_rank_fails_every_rank(tmp_path):
+    """the deferred Adam-moment restore agrees on its outcome before the first optimizer collective, so
+    a checksum failure on one rank ends every rank at once (no peer left waiting for the PG timeout)."""
+    world = 3
+    mp.spawn(_moments_worker, args=(world, _port(), str(tmp_path), str(tmp_path)), nprocs=world, join=True)
+    res = {r: (tmp_path / f"{r}.txt").read_text() for r in range(world)}
+    assert "checksum mismatch" in res[1] and (tmp_path / "meta1.json.bad").exists()
+    assert all("another rank" in res[r] for r in (0, 2)), res

@@ -100,3 +100,18 @@ def test_supervisor_cli_restarts_then_succeeds(tmp_path):
     assert r.returncode == 0, r.stderr
     rec = json.loads(r.stdout.strip().splitlines()[-1])
     assert rec["status"] == "succeeded" and rec["restarts"] == 1 and rec["exit_codes"] == [7, 0]
+
+
+def test_ep_capacity_overflow_is_not_resumed(tmp_path):
+    """an EP overflow of an explicit capacity (exit 6) replays identically on resume: it fails the job at
+    once, while a mesh timeout (exit 5) is resumed like a crash."""
+    from distributed_llm_training_gpu_manager_amd.launcher.supervisor import EXIT_EP_OVERFLOW, EXIT_TRANSPORT
+    reg = JobRegistry()
+    job = reg.submit(JobSpec(job_id="ovf", argv=[sys.executable, "-c", f"import sys; sys.exit({EXIT_EP_OVERFLOW})"],
+                             run_dir=str(tmp_path / "r1"), max_restarts=3))
+    assert _wait(job, ("failed", "succeeded")) == "failed" and job.exit_codes == [EXIT_EP_OVERFLOW]
+    assert job.restarts == 0 and any(e["event"] == "ep_capacity_overflow" for e in job.to_dict()["events"])
+    job2 = reg.submit(JobSpec(job_id="tmo", argv=[sys.executable, "-c", f"import sys; sys.exit({EXIT_TRANSPORT})"],
+                              run_dir=str(tmp_path / "r2"), max_restarts=1))
+    assert _wait(job2, ("failed", "succeeded")) == "failed"
+    assert job2.restarts == 1 and job2.exit_codes == [EXIT_TRANSPORT, EXIT_TRANSPORT]
