@@ -114,6 +114,56 @@ def _source_rank(eng) -> int:
     return eng.rank % eng.ep_size if eng.ep_size > 1 else 0
 
 
+def shm_snapshot_path(save_dir: str, rank: int) -> str:
+    """The /dev/shm snapshot file of `rank` for a job checkpointing into `save_dir` (the checkpointer's and the
+    supervisor's shared naming: the supervisor reserves it before the first launch, launcher/supervisor.py)."""
+    key = hashlib.sha1(os.path.abspath(save_dir).encode()).hexdigest()[:12]
+    return f"/dev/shm/dlgm-ckpt-{key}-r{int(rank)}.snap"
+
+
+def reserve_snapshot_files(save_dir: str, ranks, nbytes: int, threads: int = 8) -> Dict[str, Any]:
+    """Reserve (posix_fallocate: tmpfs pages allocated and zeroed) the snapshot file of every rank in `ranks`, at
+    least `nbytes` each, WITHOUT touching what a file already holds (a previous attempt's snapshot is the restore
+    source): only missing bytes past its current allocation are added. Runs in the supervisor, which outlives the
+    ranks, before the first launch: the ranks' own background preparation then finds every page
+    reserved, and a spot notice at step 1 pays only for mapping and page-locking (~15-55 GB/s) instead of the
+    3.5-6 GB/s of fresh tmpfs pages. Returns {files, bytes_added, seconds}."""
+    import concurrent.futures as cf
+    t0 = time.time()
+    if not os.path.isdir("/dev/shm") or nbytes <= 0:
+        return {"files": [], "bytes_added": 0, "seconds": 0.0, "skipped": "no /dev/shm"}
+    st = os.statvfs("/dev/shm")
+    jobs = []
+    for r in ranks:
+        path = shm_snapshot_path(save_dir, r)
+        have = 0
+        if os.path.exists(path):
+            s_ = os.stat(path)
+            have = min(s_.st_size, s_.st_blocks * 512)
+        if have < nbytes:
+            jobs.append((path, have))
+    need = sum(nbytes - h for _, h in jobs)
+    if need > st.f_bavail * st.f_frsize - (8 << 30):
+        return {"files": [p for p, _ in jobs], "bytes_added": 0, "seconds": round(time.time() - t0, 2),
+                "skipped": f"/dev/shm too small for {need} B"}
+    piece = 1 << 30
+
+    def work(item):
+        path, off = item
+        fd = os.open(path, os.O_RDWR | os.O_CREAT, 0o600)
+        try:
+            if os.fstat(fd).st_size < nbytes:
+                os.ftruncate(fd, nbytes)
+            pieces = [(o, min(piece, nbytes - o)) for o in range(off - off % piece, nbytes, piece)]
+            with cf.ThreadPoolExecutor(max(1, threads // max(1, len(jobs)))) as ex:
+                list(ex.map(lambda a: os.posix_fallocate(fd, a[0], a[1]), pieces))
+        finally:
+            os.close(fd)
+    with cf.ThreadPoolExecutor(max(1, min(len(jobs), threads))) as ex:
+        list(ex.map(work, jobs))
+    return {"files": [p for p, _ in jobs], "bytes_added": int(need), "seconds": round(time.time() - t0, 2)}
+
+
 class _Agree:
     """Cross-rank agreement on small integers (restore decisions), over the engine's communicator."""
 
@@ -157,12 +207,11 @@ class AsyncCheckpointer:
         self.manifest_timeout_s = manifest_timeout_s
         self.layout = _layout(eng)
         self.sig = hashlib.sha1(json.dumps(self.layout, sort_keys=True).encode()).hexdigest()[:16]
-        key = hashlib.sha1(self.save_dir.encode()).hexdigest()[:12]
-        self.shm_path = f"/dev/shm/dlgm-ckpt-{key}-r{self.rank}.snap"
+        self.shm_path = shm_snapshot_path(self.save_dir, self.rank)
         self.shm_meta = self.shm_path[:-5] + ".json"
         # restore reads the snapshot of the rank whose files restore this one (a ZeRO-0 twin reads its writer's)
         self.src_rank = _source_rank(eng)
-        self.shm_src_path = f"/dev/shm/dlgm-ckpt-{key}-r{self.src_rank}.snap"
+        self.shm_src_path = shm_snapshot_path(self.save_dir, self.src_rank)
         self.shm_src_meta = self.shm_src_path[:-5] + ".json"
         self.tier_notes: List[str] = []
         self.shm_need_bytes = 0
@@ -271,6 +320,11 @@ class AsyncCheckpointer:
                     fd = os.open(self.shm_path, os.O_RDWR | os.O_CREAT, 0o600)
                     try:
                         os.ftruncate(fd, nb)
+                        if os.fstat(fd).st_blocks * 512 >= nb:
+                            # every page already reserved (the supervisor's reserve_snapshot_files, or a previous
+                            # attempt's file): the preparation only maps and page-locks
+                            self._falloc_done = nb
+                            self.prep_stats["pre_reserved"] = True
                     finally:
                         os.close(fd)
                     self._snap = torch.from_file(self.shm_path, shared=True, size=nb, dtype=torch.uint8)

@@ -50,6 +50,9 @@ class MI355XOptions(BaseModel):
     checkpoint_interval: int = Field(default=0, ge=0, description="optimizer steps between async checkpoints")
     pinned_ring_gb: float = Field(default=0.0, ge=0, description="0 = size to one full shard snapshot")
     save_dir: Optional[str] = None
+    shm_reserve: bool = Field(default=True, description="with save_dir: the supervisor reserves every rank's /dev/shm "
+                              "snapshot file before the first launch (an early spot notice never waits for fresh "
+                              "host pages) and keeps it across restarts")
     auto_resume: bool = True
     max_restarts: int = Field(default=3, ge=0)
     heartbeat_timeout_s: float = Field(

@@ -27,7 +27,7 @@ import uuid
 from typing import Dict, List, Optional
 
 from .config import DeepSpeedConfig, LaunchResult, OffloadDevice, ZeROStage, generate_config, presets, utcnow
-from .supervisor import JobRegistry, JobSpec, default_registry
+from .supervisor import planned_snapshot_bytes, JobRegistry, JobSpec, default_registry
 
 
 def _stamp() -> str:
@@ -124,7 +124,9 @@ class ZeroLauncher:
                        save_dir=(opts.save_dir if opts and opts.save_dir else None),
                        heartbeat_timeout_s=opts.heartbeat_timeout_s if opts else -1.0,
                        heartbeat_min_s=opts.heartbeat_min_s if opts else 120.0,
-                       startup_timeout_s=opts.startup_timeout_s if opts else 900.0)
+                       startup_timeout_s=opts.startup_timeout_s if opts else 900.0,
+                       shm_reserve_bytes=(planned_snapshot_bytes(argv, config.num_gpus)
+                                          if opts and opts.save_dir and opts.shm_reserve else 0))
         try:
             job = self.registry.submit(spec)
             result.status = "launched"

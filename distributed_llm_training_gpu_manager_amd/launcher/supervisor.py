@@ -75,6 +75,37 @@ class JobSpec:
     max_world: int = 0
     global_batch: int = 0
     micro_batch: int = 1
+    # /dev/shm snapshot tier owned by the supervisor: before the first launch, reserve this many
+    # bytes of every local rank's snapshot file (ckpt/checkpoint.py reserve_snapshot_files), kept across restarts
+    shm_reserve_bytes: int = 0
+    shm_reserve_ranks: Optional[List[int]] = None
+
+
+def _arg(argv: List[str], key: str) -> Optional[str]:
+    for i, a in enumerate(argv):
+        if a == key and i + 1 < len(argv):
+            return argv[i + 1]
+        if a.startswith(key + "="):
+            return a.split("=", 1)[1]
+    return None
+
+
+def planned_snapshot_bytes(argv: List[str], nproc: Optional[int]) -> int:
+    """Per-rank snapshot bytes of a training command (train.py options: --model, --zero-stage, --expert-parallel,
+    --n-layers, --shadow-world), from the planner; 0 when the command does not say enough."""
+    model = _arg(argv, "--model")
+    if not model:
+        return 0
+    try:
+        from ..models import get_config
+        from ..parallel.planner import snapshot_bytes
+        nl = int(_arg(argv, "--n-layers") or 0)
+        m = get_config(model, **({"n_layers": nl} if nl else {}))
+        world = int(_arg(argv, "--shadow-world") or 0) or (nproc or 1)
+        return snapshot_bytes(m, world=world, zero_stage=int(_arg(argv, "--zero-stage") or 3),
+                              ep_size=int(_arg(argv, "--expert-parallel") or 1))
+    except (KeyError, ValueError):
+        return 0
 
 
 class Job:
@@ -290,11 +321,27 @@ class Supervisor(threading.Thread):
                 pass
             proc.wait()
 
+    def reserve_shm(self) -> None:
+        """The snapshot files of this node's ranks, reserved before the first launch and kept across restarts."""
+        job, spec = self.job, self.job.spec
+        if spec.shm_reserve_bytes <= 0 or not spec.save_dir:
+            return
+        from ..ckpt.checkpoint import reserve_snapshot_files
+        ranks = spec.shm_reserve_ranks if spec.shm_reserve_ranks is not None else \
+            list(range(self.nproc_of(spec.argv) or 1))
+        try:
+            rec = reserve_snapshot_files(spec.save_dir, ranks, spec.shm_reserve_bytes)
+        except OSError as e:
+            rec = {"error": str(e)}
+        job.event("shm_reserved", bytes_per_rank=spec.shm_reserve_bytes, ranks=len(ranks), **rec)
+
     def run(self) -> None:
         job, spec = self.job, self.job.spec
         w0 = self.nproc_of(spec.argv)
         if w0 is not None:
             job.world_history.append(w0)
+        if self._first is None:
+            self.reserve_shm()
         proc = self._first if self._first is not None else self._start(resume=False)
         failure_t: Optional[float] = None
         step_at_failure = -1
@@ -485,14 +532,22 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--max-world", type=int, default=0)
     ap.add_argument("--global-batch", type=int, default=0)
     ap.add_argument("--micro-batch", type=int, default=1)
+    ap.add_argument("--shm-reserve", default="off",
+                    help="reserve the ranks' /dev/shm snapshot files before the first launch: 'auto' (planner size "
+                         "from the training command), 'off', or GiB per rank")
     a = ap.parse_args(argv[:cut])
     cmd = argv[cut + 1:]
+    shm_bytes = 0
+    if a.shm_reserve == "auto":
+        shm_bytes = planned_snapshot_bytes(cmd, Supervisor.nproc_of(cmd))
+    elif a.shm_reserve != "off":
+        shm_bytes = int(float(a.shm_reserve) * (1 << 30))
     spec = JobSpec(job_id=a.job_id, argv=cmd, auto_resume=not a.no_auto_resume, max_restarts=a.max_restarts,
                    save_dir=a.save_dir, run_dir=a.run_dir, heartbeat_timeout_s=a.heartbeat_timeout,
                    heartbeat_min_s=a.heartbeat_min, startup_timeout_s=a.startup_timeout,
                    restart_on_preempt=a.restart_on_preempt, max_nan_restarts=a.max_nan_restarts,
                    elastic=a.elastic, min_world=a.min_world, max_world=a.max_world, global_batch=a.global_batch,
-                   micro_batch=a.micro_batch)
+                   micro_batch=a.micro_batch, shm_reserve_bytes=shm_bytes)
     job = Job(spec)
     sup = Supervisor(job)
     for sig in (signal.SIGTERM, signal.SIGINT):

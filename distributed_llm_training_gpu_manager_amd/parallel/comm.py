@@ -262,21 +262,39 @@ class ShadowComm(Comm):
     too early corrupts the collective, every time instead of by timing luck.
 
     Step times measured this way exclude xGMI transfer time; they are per-rank compute + local
-    memory traffic, reported as such (never as a headline number).
+    memory traffic, reported as such (never as a headline number) -- unless ``link_gbps`` models it:
+
+    ``link_gbps`` (async mode): every collective first holds its comm stream for the time RCCL's ring needs on
+    an xGMI link of that bus bandwidth (all-gather / reduce-scatter: (W-1)/W of the full buffer, all-reduce twice
+    that, all-to-all (W-1)/W of what this rank sends, at ``a2a_gbps``), with a wall-clock spin kernel
+    (csrc/kernels/spin.hip, one wave). The consumer's wait then sees that latency, so whether the engine's prefetch
+    and bucketing hide the communication behind compute is measured on one GPU. Not modelled:
+    the compute units RCCL's channels occupy, and contention between concurrent collectives on one link.
     """
 
-    def __init__(self, world: int, rank: int, async_mode: bool = False, delay_cycles: int = 0):
+    def __init__(self, world: int, rank: int, async_mode: bool = False, delay_cycles: int = 0,
+                 link_gbps: float = 0.0, a2a_gbps: float = 0.0):
         self.group = None
         self.world, self.rank = int(world), int(rank)
         self.backend, self.is_gloo = "shadow", False
         self.async_mode, self.delay_cycles = bool(async_mode), int(delay_cycles)
+        self.link_gbps, self.a2a_gbps = float(link_gbps), float(a2a_gbps or link_gbps)
         self._stream = None
         self.issued = 0  # collectives run on the comm stream (async mode)
+        self.modelled_s = 0.0  # link time queued on the comm stream by the link model
 
     def _sibling(self, world: int, rank: int) -> "ShadowComm":
-        return ShadowComm(world, rank, self.async_mode, self.delay_cycles)
+        return ShadowComm(world, rank, self.async_mode, self.delay_cycles, self.link_gbps, self.a2a_gbps)
 
-    def _run(self, fn: Callable[[], None], tensors: List[torch.Tensor], async_op: bool) -> Handle:
+    def _link_ns(self, nbytes: float, a2a: bool = False) -> int:
+        bw = self.a2a_gbps if a2a else self.link_gbps
+        if bw <= 0 or self.world <= 1:
+            return 0
+        s = nbytes * (self.world - 1) / self.world / (bw * 1e9)
+        self.modelled_s += s
+        return int(s * 1e9)
+
+    def _run(self, fn: Callable[[], None], tensors: List[torch.Tensor], async_op: bool, link_ns: int = 0) -> Handle:
         """Run `fn` (the local stand-in of a collective over `tensors`) as RCCL would: on this communicator's
         stream, ordered after the issuing stream's queued work, completion awaited by Handle.wait()."""
         if not self.async_mode or not tensors or not tensors[0].is_cuda:
@@ -291,6 +309,9 @@ class ShadowComm(Comm):
         with torch.cuda.stream(s):
             if self.delay_cycles:
                 torch.cuda._sleep(self.delay_cycles)
+            if link_ns:
+                from .._native import hip_ops
+                hip_ops().spin_ns(link_ns)
             fn()
             ev = torch.cuda.Event()
             ev.record(s)
@@ -309,7 +330,7 @@ class ShadowComm(Comm):
                 out.copy_(inp)
             return DONE
         return self._run(lambda: out.view(self.world, -1).copy_(inp.reshape(1, -1).expand(self.world, -1)),
-                         [out, inp], async_op)
+                         [out, inp], async_op, self._link_ns(out.numel() * out.element_size()))
 
     def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, avg: bool = True,
                        async_op: bool = True) -> Handle:
@@ -321,12 +342,13 @@ class ShadowComm(Comm):
         def fn():
             red = inp.view(self.world, -1).float().sum(0)
             out.copy_(red / self.world if avg else red)
-        return self._run(fn, [out, inp], async_op)
+        return self._run(fn, [out, inp], async_op, self._link_ns(inp.numel() * inp.element_size()))
 
     def all_reduce(self, t: torch.Tensor, avg: bool = False, async_op: bool = True) -> Handle:
+        ns = self._link_ns(2 * t.numel() * t.element_size()) if self.world > 1 else 0
         if self.world > 1 and not avg:
-            return self._run(lambda: t.mul_(self.world), [t], async_op)
-        return self._run(lambda: None, [t], async_op) if self.world > 1 else DONE
+            return self._run(lambda: t.mul_(self.world), [t], async_op, ns)
+        return self._run(lambda: None, [t], async_op, ns) if self.world > 1 else DONE
 
     def all_reduce_max(self, t: torch.Tensor) -> None:
         return None
@@ -349,7 +371,7 @@ class ShadowComm(Comm):
                 else:  # a return leg of another size (combine): any rows of the right count will do
                     idx = torch.arange(o.shape[0], device=inp.device) % inp.shape[0]
                     o.copy_(inp.index_select(0, idx))
-        return self._run(fn, [out, inp], async_op)
+        return self._run(fn, [out, inp], async_op, self._link_ns(inp.numel() * inp.element_size(), a2a=True))
 
     def broadcast(self, t: torch.Tensor, src: int = 0) -> None:
         return None

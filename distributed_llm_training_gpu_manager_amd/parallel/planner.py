@@ -109,6 +109,23 @@ def zero3_budgets(hbm_bytes: float, committed_bytes: float, live_hbm_fraction: f
     return live_bytes / 2.0, tcache_budget
 
 
+def snapshot_bytes(m: ModelConfig, *, world: int, zero_stage: int = 3, ep_size: int = 1) -> int:
+    """Bytes of one rank's checkpoint snapshot (ckpt/checkpoint.py: fp32 master | exp_avg | exp_avg_sq | 16-bit
+    params = 14 B per element of the rank's partition), from the same group layout the engine builds; the largest
+    rank (shards differ by at most one padding unit) plus 64 MiB of slack."""
+    from .zero import FlatGroup
+
+    ep = max(1, ep_size) if m.n_experts else 1
+    P = 1 if zero_stage == 0 else world
+    groups_spec, _ = build_model(m, 0, ep)
+    shard = 0
+    for i, grp in enumerate(groups_spec):
+        kind = grp[2] if len(grp) > 2 else "dense"
+        Pg = (1 if zero_stage == 0 else world // ep) if kind == "expert" else P
+        shard += FlatGroup(i, grp[0], grp[1], Pg, kind).shard_numel
+    return int(14 * shard + (64 << 20))
+
+
 def plan_rank(m: ModelConfig, *, world: int, zero_stage: int = 3, micro_batch: int = 1, seq_len: int = 8192,
               grad_accum: int = 8, activation_checkpointing: bool = False, ep_size: int = 1,
               local_grad_accum="hbm", local_grad_hbm_fraction: float = 0.15, max_live_parameters="hbm",

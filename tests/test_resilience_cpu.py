@@ -260,3 +260,42 @@ def test_checkpointer_reports_prepared_after_background_preparation(tmp_path):
     ck.save(1, {"step": 1}, blocking=True)
     assert ck.prepared
     ck.close(discard_shm=True)
+
+
+def test_supervisor_reserves_shm_snapshots_before_the_first_launch(tmp_path):
+    """the supervisor (which outlives the ranks) reserves each rank's /dev/shm snapshot file before
+    the first launch, sized by the planner from the training command; the checkpointer then finds every page reserved
+    (prep_stats.pre_reserved: only mapping / page-locking left for an early spot notice), and a second reservation
+    never touches a snapshot that is already there (it is the restore source of a relaunch)."""
+    from distributed_llm_training_gpu_manager_amd.ckpt.checkpoint import reserve_snapshot_files, shm_snapshot_path
+    from distributed_llm_training_gpu_manager_amd.launcher.supervisor import (Job, JobSpec, Supervisor,
+                                                                               planned_snapshot_bytes)
+    save = str(tmp_path / "ck")
+    cmd = [sys.executable, "-c", "pass", "--model", "llama-tiny", "--zero-stage", "3"]
+    nb = planned_snapshot_bytes(cmd, 1)
+    eng = ZeroEngine(get_config("llama-tiny"), EngineConfig(zero_stage=3, micro_batch_size=1, seq_len=16,
+                                                            init_device="cpu"), torch.device("cpu"))
+    assert 14 * eng.shard_total <= nb <= 14 * eng.shard_total + (64 << 20)
+    job = Job(JobSpec(job_id="shm", argv=cmd, save_dir=save, run_dir=str(tmp_path / "run"), shm_reserve_bytes=nb))
+    sup = Supervisor(job)
+    sup.start()
+    sup.join(60)
+    ev = [e for e in job.events if e["event"] == "shm_reserved"]
+    path = shm_snapshot_path(save, 0)
+    try:
+        assert ev and ev[0]["bytes_added"] == nb and os.path.exists(path), job.events
+        st = os.stat(path)
+        assert st.st_blocks * 512 >= nb
+        ck = AsyncCheckpointer(eng, save, shm=True, disk=False)
+        assert ck.mode == "shm" and ck.shm_path == path
+        ck._alloc_snapshot()
+        assert ck.prep_stats.get("pre_reserved") and ck._falloc_done == ck.snap_bytes
+        ck.save(1, {"step": 1}, blocking=True)
+        before, size = open(path, "rb").read(4096), os.path.getsize(path)  # the checkpointer trimmed the slack
+        again = reserve_snapshot_files(save, [0], nb)
+        assert again["bytes_added"] == nb - size and open(path, "rb").read(4096) == before
+        ck.close()
+    finally:
+        for p in (path, path[:-5] + ".json"):
+            if os.path.exists(p):
+                os.unlink(p)

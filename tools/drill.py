@@ -107,6 +107,38 @@ def drill_spot(a, work, warm=False):
             "tail": (out[-300:], out2[-300:])}
 
 
+def drill_spot_reserved(a, work):
+    """spot_reserved: the job runs under the supervisor, which reserves this rank's /dev/shm
+    snapshot file (planner size from the command) BEFORE the first launch; the spot notice lands at step 1 -- before
+    the trainer's own background preparation could have prepared a fresh file -- and the emergency checkpoint must
+    finish inside the 120 s notice window (/root/reference/ai_engine/spot_resiliency.py:8-10) with a wide margin.
+    Then a fresh process restores from it."""
+    from distributed_llm_training_gpu_manager_amd.launcher.supervisor import planned_snapshot_bytes
+    ck = os.path.join(work, "ck_spot_res")
+    argv = train_argv(a, ["--steps", "6", "--save-dir", ck, "--preempt-at-step", "1"])
+    nb = planned_snapshot_bytes(argv, 1)
+    t0 = time.time()
+    job = JobRegistry().submit(JobSpec(job_id="spot-reserved-drill", argv=argv, env={"PYTHONPATH": ROOT}, save_dir=ck,
+                                       run_dir=os.path.join(work, "run_spot_res"), auto_resume=False,
+                                       shm_reserve_bytes=nb))
+    while job.status not in ("succeeded", "failed", "preempted") and time.time() - t0 < a.timeout:
+        time.sleep(0.2)
+    log = open(job.log_path).read()
+    em = re.findall(r"emergency checkpoint at step (\d+) in ([0-9.]+)s", log)
+    rc2, out2, dt2 = run(train_argv(a, ["--steps", "2", "--save-dir", ck, "--resume", "auto"]), a.timeout)
+    res = re.findall(r"resumed from step (\d+) in ([0-9.]+)s", out2)
+    ck_s = float(em[0][1]) if em else None
+    return {"drill": "spot_reserved", "status": job.status, "exit_codes": job.exit_codes,
+            "shm_reserved": [e for e in job.events if e["event"] == "shm_reserved"],
+            "planned_snapshot_bytes": nb, "emergency_ckpt": em,
+            "notice_window_s": 120.0, "margin_to_notice_window_s": None if ck_s is None else round(120.0 - ck_s, 2),
+            "emergency_record": [json.loads(x) for x in re.findall(r"emergency checkpoint record: (\{.*?\})\n", log)],
+            "ckpt_prepare": [json.loads(x) for x in re.findall(r"ckpt prepare: (\{.*?\})", log + out2)],
+            "startup_timeline": [json.loads(x) for x in re.findall(r"\[train\] startup: (\{.*?\})", log)],
+            "restore_exit": rc2, "restore": res, "restore_process_wall_s": round(dt2, 2),
+            "events": job.events, "tail": (log[-600:], out2[-300:])}
+
+
 def _drop_shm(save_dir: str) -> None:
     """Remove the /dev/shm snapshot tier a drill's save dir left behind (failed runs keep it for resume)."""
     import glob
@@ -144,14 +176,14 @@ def main():
            "data": "synthetic token ids, random-init weights"}
     for d in a.drills.split(","):
         t0 = time.time()
-        res[d] = {"nan": drill_nan, "sigkill": drill_sigkill, "spot": drill_spot,
+        res[d] = {"nan": drill_nan, "sigkill": drill_sigkill, "spot": drill_spot, "spot_reserved": drill_spot_reserved,
                   "spot_warm": lambda a_, w_: drill_spot(a_, w_, warm=True)}[d](a, work)
         res[d]["wall_s"] = round(time.time() - t0, 1)
         print(json.dumps({k: v for k, v in res[d].items() if k != "tail"})[:2000], flush=True)
         os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
         with open(a.out, "w") as f:
             json.dump(res, f, indent=1)
-        for sub in ("ck", "ck_spot"):  # the box's scratch disk holds one drill's checkpoints at a time
+        for sub in ("ck", "ck_spot", "ck_spot_res"):  # the box's scratch disk holds one drill's checkpoints at a time
             shutil.rmtree(os.path.join(work, sub), ignore_errors=True)
             _drop_shm(os.path.join(work, sub))
     shutil.rmtree(work, ignore_errors=True)

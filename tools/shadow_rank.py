@@ -26,6 +26,19 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+def _knob(v: str):
+    return v if v in ("hbm", "auto") else float(v)
+
+
+def _comms(eng):
+    seen = {}
+    for c in [eng.comm, getattr(eng, "gather_comm", None), getattr(eng, "ep_comm", None),
+              getattr(eng, "edp_comm", None)] + [x for g in eng.groups for x in (g.comm, getattr(g, "gcomm", None))]:
+        if c is not None:
+            seen[id(c)] = c
+    return list(seen.values())
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="llama3-70b")
@@ -44,6 +57,12 @@ def main(argv=None) -> int:
     ap.add_argument("--out", default=None)
     ap.add_argument("--async-comm", action="store_true",
                     help="collectives on per-communicator HIP streams, ordered like RCCL's (ShadowComm async_mode)")
+    ap.add_argument("--link-gbps", type=float, default=0.0,
+                    help="async comm: hold each collective's stream for its ring time at this xGMI bus bandwidth")
+    ap.add_argument("--a2a-gbps", type=float, default=0.0, help="all-to-all bandwidth of the link model (default: link)")
+    ap.add_argument("--live-params", default="hbm", help="stage3_max_live_parameters: 'hbm' or a number (1e9: reference)")
+    ap.add_argument("--reuse-distance", default="hbm", help="stage3_max_reuse_distance: 'hbm' or a number")
+    ap.add_argument("--local-grads", default="hbm", help="'hbm', 'on' or 'off' (off: reduce-scatter every micro-batch)")
     a = ap.parse_args(argv)
 
     import torch
@@ -60,9 +79,12 @@ def main(argv=None) -> int:
     mcfg = get_config(a.model, **({"n_layers": a.n_layers} if a.n_layers else {}))
     ecfg = EngineConfig(zero_stage=a.zero, micro_batch_size=a.mbs, seq_len=a.seq, grad_accum=a.ga, lr=3e-5,
                         warmup_steps=100, total_steps=10000, grad_clip=1.0, activation_checkpointing=a.ckpt,
-                        max_live_parameters="hbm", max_reuse_distance="hbm", expert_parallel_size=a.ep)
+                        max_live_parameters=_knob(a.live_params), max_reuse_distance=_knob(a.reuse_distance),
+                        local_grad_accum={"on": True, "off": False}.get(a.local_grads, a.local_grads),
+                        expert_parallel_size=a.ep)
     t0 = time.time()
-    comm = ShadowComm(a.world, a.rank, async_mode=a.async_comm)
+    comm = ShadowComm(a.world, a.rank, async_mode=a.async_comm or a.link_gbps > 0, link_gbps=a.link_gbps,
+                      a2a_gbps=a.a2a_gbps)
     eng = ZeroEngine(mcfg, ecfg, dev, comm)
     torch.cuda.synchronize()
     init_s = time.time() - t0
@@ -108,8 +130,14 @@ def main(argv=None) -> int:
         "step_s": [round(x, 3) for x in times], "per_micro_batch_s": round(sum(timed) / len(timed) / a.ga, 3),
         "tokens_per_s_per_rank_compute_only": round(a.mbs * a.seq * a.ga * len(timed) / sum(timed), 1),
         "init_s": round(init_s, 1),
-        "comm": "async (per-communicator HIP streams, RCCL ordering)" if a.async_comm else "sync (compute stream)",
-        "async_collectives_issued": comm.issued,
+        "comm": "async (per-communicator HIP streams, RCCL ordering)" if (a.async_comm or a.link_gbps > 0)
+        else "sync (compute stream)",
+        "async_collectives_issued": sum(getattr(c, "issued", 0) for c in _comms(eng)),
+        "link_model": {"link_gbps": a.link_gbps, "a2a_gbps": a.a2a_gbps or a.link_gbps,
+                       "modelled_link_s_total": round(sum(getattr(c, "modelled_s", 0.0) for c in _comms(eng)), 3),
+                       "steps_in_run": total} if a.link_gbps > 0 else None,
+        "knobs": {"stage3_max_live_parameters": a.live_params, "stage3_max_reuse_distance": a.reuse_distance,
+                  "local_grads": eng.local_grads, "gathers_per_step": eng.live_plan.gathers_per_step(a.ga)},
     }
     print(json.dumps(out), flush=True)
     if a.out:
