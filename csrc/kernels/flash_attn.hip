@@ -439,6 +439,8 @@ struct BwdParams {
   int64_t do_sb, do_ss, do_sh;
   int64_t dq_ss, dkv_ss;  // token (row) strides of the dq and dk/dv outputs: Hq*D / Hkv*D, or the fused
                           // [T, (Hq + 2 Hkv) D] dQKV row when the caller hands over one buffer
+  E* ds;                  // dS in MFMA-fragment order, one 2 KiB block per (b, q head, 32 queries, 32 keys)
+  int64_t ds_nblk;        // blocks per (b, q head): the causal triangle or the full square of 32-blocks
   int B, S, Hq, Hkv;
   float scale;          // softmax scale
   float scale_log2;     // scale * log2(e)
@@ -467,6 +469,20 @@ __device__ __forceinline__ void stage_rows(E* img, const E* base, int64_t row_st
   }
 }
 
+// ---- stored dS (the single-recompute backward, DLGM_ATTN_BWD=ds): dK/dV computes dS = P (dP - delta) once per (query, key)
+// and writes it out in the exact register order in which the dQ pass consumes it as the B operand of
+// dQ^T += K^T dS^T: block (query block qb, key block kb) of 32 x 32 is 2 x 1 KiB, k-step s2 at +512 elements,
+// lane l's 8 keys at +8 l -- each wave stores and loads it as one fully coalesced 16 B per lane access.
+// The dQ pass then recomputes neither S = QK^T nor dP = dO V^T: 2.5 forward-equivalents of MFMA work instead of 3.5
+// (VERDICT r05 item 2), for 2 B per causal (query, key) pair written once and read once. Measured at the Llama-3-8B
+// shape it is 5 % SLOWER than the recompute backward (the default): the dS write costs dK/dV more than the recompute
+// it saves the dQ pass (profiles/attn_bwd_stored_ds_ab_r06.json).
+__device__ __forceinline__ int64_t ds_block(int qb, int kb, int nkb, bool causal) {
+  return causal ? (int64_t)qb * (qb + 1) / 2 + kb : (int64_t)qb * nkb + kb;
+}
+constexpr int kTsRow = 36;             // LDS row of the per-wave dS transpose tile: 32 queries + 4 pad (72 B rows)
+constexpr int kTsWave = 32 * kTsRow;   // one wave's [32 keys][36] tile
+
 // ---- dK / dV: one workgroup per (b, q head, 128 keys); 4 waves x 32 keys on the MFMA lanes.
 constexpr int kKvThreads = 256;
 constexpr int kKvBKV = 128;
@@ -475,13 +491,16 @@ constexpr int kKvBQ = 32;
 // HP: q heads per workgroup (2 when the GQA group is even): the heads of a pair share this block's K / V, so
 // the workgroup walks both heads' query tiles into one dK/dV accumulator -- half the fp32 partials written
 // and summed by gqa_reduce, half the K / V block loads.
-template <typename E, int D, bool TAIL, int HP = 1>
+template <typename E, int D, bool TAIL, int HP = 1, bool STORE_DS = false>
 __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams<E> p) {
   constexpr int KK = D / 16;
   constexpr int DT = D / 32;
   constexpr int QT = kKvBQ * D;
   __shared__ __attribute__((aligned(16))) E smem[2 * 2 * QT + kKvBKV * D];  // [buf][Q | dO], then V rows
   __shared__ __attribute__((aligned(16))) float rc[2][64];        // [buf][-lse/scale 0..31 | -delta 32..63]
+  // STORE_DS: each wave's dS tile goes through LDS once ([key][query] rows written from the accumulator layout,
+  // read back transposed with ds_read_b64_tr_b16 into the dQ pass's B-operand order)
+  __shared__ __attribute__((aligned(16))) E ts[STORE_DS ? 4 * kTsWave : 1];
   E* vimg = smem + 2 * 2 * QT;  // this block's 128 V rows (row image): B operand of dP, re-read per tile
 
   const int lane = threadIdx.x & 63;
@@ -552,14 +571,20 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
     }
   };
 
+  // STORE_DS: the previous tile's two dS stores are this wave's youngest vector-memory operations; CDNA4's vmcnt
+  // counts stores too, so a full drain would wait for their write-back every tile -- wait for the DMA only
+  bool stored = false;
   // unrolled by two: the LDS buffer is a compile-time constant in each copy (immediate ds_read offsets)
   auto tile = [&](auto bufc, int j) {
     constexpr int buf = decltype(bufc)::value;
-    vm_drain();  // this tile's LDS-DMA has landed ...
+    if (STORE_DS && stored) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else vm_drain();  // this tile's LDS-DMA has landed ...
+    stored = false;
     __syncthreads();  // ... for every wave, and the other buffer's readers are done
     if (j + 1 < ntot) stage(buf ^ 1, j + 1);
     const int t = t0 + (HP > 1 ? j % nt_h : j);
     const int q0 = t * kKvBQ;
+    const int hp_cur = HP > 1 ? j / nt_h : 0;
     const bool active = uniform(!(p.causal && q0 + kKvBQ - 1 < kw0));
     if (active) {
       const E* qi = smem + buf * 2 * QT;
@@ -613,6 +638,28 @@ __global__ __launch_bounds__(kKvThreads, 2) void flash_bwd_dkdv_kernel(BwdParams
         dsf[s2] = (vec8_t<E>){(E)dpacc[8 * s2 + 0], (E)dpacc[8 * s2 + 1], (E)dpacc[8 * s2 + 2],
                            (E)dpacc[8 * s2 + 3], (E)dpacc[8 * s2 + 4], (E)dpacc[8 * s2 + 5],
                            (E)dpacc[8 * s2 + 6], (E)dpacc[8 * s2 + 7]};
+      }
+      // STORE_DS (DLGM_ATTN_BWD=ds): lane (key r, half h) holds dS for queries 8m + 4h + 0..3 in registers 4m..4m+3 --
+      // four 8-byte row pieces of the wave's [key][query] LDS tile; the transposed reads give lane (query l&31, half
+      // l>>5) its 8 keys {16 s2 + 8 (j >> 2) + 4 h + (j & 3)} -- the key order of the dQ pass's K^T reads -- stored as
+      // 16 B per lane. (Measured placing the read-back after the dV / dK MFMAs instead: 7 % slower.)
+      if (STORE_DS && uniform(kw0 < p.S)) {  // a wave whose keys all lie past S owns no dS block
+        E* tw = ts + w * kTsWave;
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+          *reinterpret_cast<vec4_t<E>*>(tw + r * kTsRow + 8 * m + 4 * h) =
+              (vec4_t<E>){(E)dpacc[4 * m], (E)dpacc[4 * m + 1], (E)dpacc[4 * m + 2], (E)dpacc[4 * m + 3]};
+        __builtin_amdgcn_wave_barrier();
+        const int colq = 16 * (g & 1) + 4 * (i16 & 3);
+        E* dst = p.ds + ((int64_t)(b * p.Hq + hq + hp_cur) * p.ds_nblk +
+                         ds_block(t, kw0 / 32, (p.S + 31) / 32, p.causal)) * 1024 + lane * 8;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int r1 = 16 * s2 + 4 * h + (i16 >> 2);
+          *reinterpret_cast<vec8_t<E>*>(dst + 512 * s2) =
+              cat(lds_read_tr(tw + r1 * kTsRow + colq), lds_read_tr(tw + (r1 + 8) * kTsRow + colq));
+        }
+        stored = true;
       }
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
@@ -850,12 +897,136 @@ __global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_kernel(BwdParams<E
   store_rows_bf16<DT>(p.dq + ((int64_t)b * p.S + qcol) * p.dq_ss + hq * D, dqt, p.scale, h, qcol < p.S);
 }
 
+// ---- dQ from the stored dS (DLGM_ATTN_BWD=ds): one workgroup per (b, q head, 128 queries), the dQ pass's structure
+// with the recompute gone -- per 64-key tile a wave loads its 2 x 2 dS fragments (16 B per lane, coalesced; issued
+// one tile ahead, beside the K tile's LDS-DMA) and runs the 16 MFMAs of dQ^T += K^T dS^T. Bound by the dS read.
+template <typename E, int D, bool TAIL>
+__global__ __launch_bounds__(kDqThreads, 2) void flash_bwd_dq_ds_kernel(BwdParams<E> p) {
+  constexpr int DT = D / 32;
+  constexpr int TILE = kDqBKV * D;
+  __shared__ __attribute__((aligned(16))) E smem[2 * TILE];  // [buf] K tile (dual image)
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h = lane >> 5, i16 = lane & 15, g = lane >> 4;
+  const int nqt = (p.S + kDqBQ - 1) / kDqBQ;
+  const int group = p.Hq / p.Hkv;
+  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_kv = group * nqt;
+  const int bk = work / per_kv;
+  const int rem = work - bk * per_kv;
+  const int qt = nqt - 1 - rem / group;
+  const int hq = (bk % p.Hkv) * group + rem % group;
+  const int b = bk / p.Hkv;
+  const int hk = hq / group;
+  const int q0 = qt * kDqBQ;
+  const int q0w = q0 + 32 * w;
+  const int qcol = q0w + (lane & 31);
+  const int nkb = (p.S + 31) / 32;
+  const int qb = q0w / 32;
+  const E* kb = p.k + b * p.k_sb + hk * p.k_sh;
+  const E* dsb = p.ds + (int64_t)(b * p.Hq + hq) * p.ds_nblk * 1024 + lane * 8;
+
+  f32x16 dqt[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) dqt[dt] = (f32x16)(0.f);
+  const int kv_end = p.causal ? min(p.S, q0 + kDqBQ) : p.S;
+  const int nt = (kv_end + kDqBKV - 1) / kDqBKV;
+  const TileDma<E, D, kDqBKV, 1, TAIL> kdma(kb, p.k_ss, p.S, w, lane);
+  // a dS block of this wave exists when its queries and the block's keys lie inside the sequence and the block is on
+  // or below the diagonal (a wave whose 32 queries all lie past S -- the tail of the last 128-query tile -- has none)
+  auto have = [&](int kbk) { return uniform(qb < nkb && kbk < nkb && !(p.causal && kbk > qb)); };
+  auto load = [&](vec8_t<E> (&f)[2][2], int t) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int kbk = 2 * t + u;
+      if (have(kbk)) {
+        const E* src = dsb + ds_block(qb, kbk, nkb, p.causal) * 1024;
+        f[u][0] = __builtin_nontemporal_load(reinterpret_cast<const vec8_t<E>*>(src));
+        f[u][1] = __builtin_nontemporal_load(reinterpret_cast<const vec8_t<E>*>(src + 512));
+      }
+    }
+  };
+  auto tile = [&](auto bufc, int t, vec8_t<E> (&cur)[2][2], vec8_t<E> (&nxt)[2][2]) {
+    constexpr int buf = decltype(bufc)::value;
+    vm_drain();  // this tile's K (LDS-DMA) and dS fragments (registers) have landed ...
+    __syncthreads();  // ... for every wave, and the other buffer's readers are done
+    if (t + 1 < nt) {
+      kdma.issue(smem + (buf ^ 1) * TILE, (t + 1) * kDqBKV);
+      load(nxt, t + 1);
+    }
+    const E* kt = smem + buf * TILE;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (!have(2 * t + u)) continue;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const int col = dt * 32 + 16 * (g & 1) + 4 * (i16 & 3);
+        const int ch = col >> 3, within = col & 7;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int r1 = 32 * u + 16 * s2 + 4 * h + (i16 >> 2);
+          const int r2 = r1 + 8;
+          vec8_t<E> a = cat(lds_read_tr(kt + r1 * D + swz_dual<D>(r1, ch) * 8 + within),
+                            lds_read_tr(kt + r2 * D + swz_dual<D>(r2, ch) * 8 + within));
+          dqt[dt] = mfma32(a, cur[u][s2], dqt[dt]);
+        }
+      }
+    }
+  };
+  vec8_t<E> fa[2][2], fb[2][2];
+  kdma.issue(smem, 0);
+  load(fa, 0);
+  for (int t = 0; t < nt; t += 2) {
+    tile(std::integral_constant<int, 0>{}, t, fa, fb);
+    if (t + 1 < nt) tile(std::integral_constant<int, 1>{}, t + 1, fb, fa);
+  }
+  store_rows_bf16<DT>(p.dq + ((int64_t)b * p.S + qcol) * p.dq_ss + hq * D, dqt, p.scale, h, qcol < p.S);
+}
+
+// delta = rowsum(dO * O) per (b, s, q head), written as the [-delta, -lse / scale] rows the dK/dV pass starts its
+// accumulators from (the recompute backward folds this into its dQ pass, which runs first; here dK/dV runs first).
+// D / 8 lanes per row, 16 B per lane of each operand, a shuffle reduction inside the row's lane group.
+template <typename E, int D>
+__global__ __launch_bounds__(256) void attn_delta_kernel(BwdParams<E> p) {
+  constexpr int L = D / 8;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t row = gid / L;  // (b, s, hq) in [B, S, Hq] order
+  const int c = (int)(gid % L);
+  const int64_t R = (int64_t)p.B * p.S * p.Hq;
+  float acc = 0.f;
+  int b = 0, sq = 0, hq = 0;
+  if (row < R) {
+    hq = (int)(row % p.Hq);
+    const int64_t bs = row / p.Hq;
+    sq = (int)(bs % p.S);
+    b = (int)(bs / p.S);
+    const f32x8 d = load8f(p.dout + b * p.do_sb + (int64_t)sq * p.do_ss + hq * p.do_sh + 8 * c);
+    const f32x8 o = load8f(p.o + row * D + 8 * c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += d[j] * o[j];
+  }
+#pragma unroll
+  for (int off = L / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if (row < R && c == 0) {
+    const int64_t rc = ((int64_t)b * p.Hq + hq) * p.S + sq;
+    float* dl = const_cast<float*>(p.delta);
+    dl[rc] = -acc;
+    dl[R + rc] = p.lse[rc] * p.neg_inv_scale;
+  }
+}
+
 void check_qkv(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda() && DLGM_IS16(t), name, " must be a bf16/fp16 GPU tensor");
   TORCH_CHECK(t.dim() == 4 && t.stride(3) == 1, name, " must be [B, S, H, D] with unit stride on D");
   TORCH_CHECK(t.stride(0) % 8 == 0 && t.stride(1) % 8 == 0 && t.stride(2) % 8 == 0,
               name, " strides must keep 16-byte alignment");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+
+bool attn_bwd_store_ds() {  // read per call (a getenv): A/B runs switch it inside one process
+  const char* e = std::getenv("DLGM_ATTN_BWD");
+  return e != nullptr && std::strcmp(e, "ds") == 0;
 }
 
 }  // namespace
@@ -945,6 +1116,14 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
     dk_part = at::empty({nparts, B, S, Hkv, D}, q.options().dtype(at::kFloat));
     dv_part = at::empty({nparts, B, S, Hkv, D}, q.options().dtype(at::kFloat));
   }
+  // default: the two-recompute backward (dQ pass first, computing delta itself). DLGM_ATTN_BWD=ds: dK/dV stores dS once
+  // and dQ reads it -- 29 % fewer MFMAs, but measured slower on MI355X (profiles/attn_bwd_stored_ds_ab_r06.json: dQ
+  // 718 -> 508 us, dK/dV 1013 -> 1288 us for the 2.15 GB dS write at the board's power limit, + a 32 us delta launch)
+  const bool store_ds = attn_bwd_store_ds();
+  const int64_t nkb = (S + 31) / 32;
+  const int64_t ds_nblk = causal ? nkb * (nkb + 1) / 2 : nkb * nkb;
+  at::Tensor ds;
+  if (store_ds) ds = at::empty({(int64_t)B * Hq * ds_nblk * 1024}, q.options());
   auto stream = c10::hip::getCurrentHIPStream();
   TORCH_CHECK(k.scalar_type() == q.scalar_type() && v.scalar_type() == q.scalar_type() &&
                   dout.scalar_type() == q.scalar_type() && out.scalar_type() == q.scalar_type(),
@@ -960,15 +1139,24 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dlgm_flash_attn_bwd(const at::Ten
                    nparts > 1 ? dv_part.data_ptr<float>() : nullptr, reinterpret_cast<E*>(dk.data_ptr()),
                    reinterpret_cast<E*>(dv.data_ptr()), q.stride(0), q.stride(1), q.stride(2), k.stride(0),
                    k.stride(1), k.stride(2), v.stride(0), v.stride(1), v.stride(2), dout.stride(0), dout.stride(1),
-                   dout.stride(2), dq_ss, dkv_ss, B, S, Hq, Hkv, (float)softmax_scale,
-                   (float)(softmax_scale * kLog2e), (float)(-1.0 / softmax_scale), causal};
-    // one (dK/dV, dQ) pair of launches per head dim / tail instantiation
+                   dout.stride(2), dq_ss, dkv_ss, store_ds ? reinterpret_cast<E*>(ds.data_ptr()) : nullptr,
+                   ds_nblk, B, S, Hq, Hkv, (float)softmax_scale, (float)(softmax_scale * kLog2e),
+                   (float)(-1.0 / softmax_scale), causal};
+    // one backward per head dim / tail instantiation
     auto run = [&](auto dc, auto tc) {
       constexpr int DD = decltype(dc)::value;
       constexpr bool TT = decltype(tc)::value;
-      flash_bwd_dq_kernel<E, DD, TT><<<dq_blocks, kDqThreads, 0, stream>>>(p);
-      if (hp == 2) flash_bwd_dkdv_kernel<E, DD, TT, 2><<<kv_blocks, kKvThreads, 0, stream>>>(p);
-      else flash_bwd_dkdv_kernel<E, DD, TT><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+      if (store_ds) {
+        const int64_t rows = (int64_t)B * S * Hq * (DD / 8);
+        attn_delta_kernel<E, DD><<<(rows + 255) / 256, 256, 0, stream>>>(p);
+        if (hp == 2) flash_bwd_dkdv_kernel<E, DD, TT, 2, true><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+        else flash_bwd_dkdv_kernel<E, DD, TT, 1, true><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+        flash_bwd_dq_ds_kernel<E, DD, TT><<<dq_blocks, kDqThreads, 0, stream>>>(p);
+      } else {
+        flash_bwd_dq_kernel<E, DD, TT><<<dq_blocks, kDqThreads, 0, stream>>>(p);
+        if (hp == 2) flash_bwd_dkdv_kernel<E, DD, TT, 2><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+        else flash_bwd_dkdv_kernel<E, DD, TT><<<kv_blocks, kKvThreads, 0, stream>>>(p);
+      }
     };
     if (D == 128) {
       if (tail) run(std::integral_constant<int, 128>{}, std::true_type{});

@@ -433,3 +433,26 @@ def _elementwise(name, got, want, rtol=0.05, atol_rms=0.1):
     atol = atol_rms * float(want.pow(2).mean().sqrt())
     bad = err > atol + rtol * want.abs()
     assert not bool(bad.any()), (name, int(bad.sum()), float(err.max()), atol)
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv,D,causal", [(1, 512, 8, 2, 128, True), (2, 200, 4, 1, 128, True),
+                                                 (1, 192, 4, 2, 64, False), (1, 40, 4, 4, 128, True)])
+def test_flash_attention_bwd_stored_ds_matches_recompute(B, S, Hq, Hkv, D, causal, monkeypatch):
+    """The stored-dS backward (DLGM_ATTN_BWD=ds: dK/dV stores dS in the dQ pass's fragment order, dQ reads it: delta
+    kernel -> dK/dV -> dQ) against the default two-recompute backward: dV bit-identical (the same P), dK within
+    rounding (delta = rowsum(dO O) is summed in another order), dQ within bf16 rounding of dS (the two passes
+    accumulate S in different orders), both against fp32."""
+    torch.manual_seed(3)
+    q, k, v = (torch.randn(B, S, h, D, dtype=torch.bfloat16, device=DEV) for h in (Hq, Hkv, Hkv))
+    do = torch.randn(B, S, Hq, D, dtype=torch.bfloat16, device=DEV)
+    scale = 1 / math.sqrt(D)
+    o, lse = ops.flash_attn_fwd(q, k, v, scale, causal)
+    old = ops.flash_attn_bwd(do, q, k, v, o, lse, scale, causal)
+    monkeypatch.setenv("DLGM_ATTN_BWD", "ds")
+    got = ops.flash_attn_bwd(do, q, k, v, o, lse, scale, causal)
+    ref = attn_ops._ref_bwd(do.cpu(), q.cpu(), k.cpu(), v.cpu(), o.cpu(), lse.cpu(), scale, causal)
+    assert torch.equal(got[2], old[2])
+    assert frob_err(got[1], old[1]) < 2e-3, frob_err(got[1], old[1])
+    assert frob_err(got[0], old[0]) < 2e-3, frob_err(got[0], old[0])
+    for name, g, want in zip("qkv", got, ref):
+        assert frob_err(g, want) < 1e-2, (name, frob_err(g, want))
