@@ -90,7 +90,7 @@ void dlgm_mesh_rs_reduce(at::Tensor out, double scale, bool accumulate, const at
                          int64_t me, int64_t ch, int64_t region_off, int64_t slot_bytes, int64_t rank_stride,
                          int64_t slots, int64_t heap_bytes, bool fp32_slots);
 std::vector<int64_t> dlgm_mesh_plan_layout(int64_t W, int64_t E);
-void dlgm_spin_ns(int64_t ns);
+void dlgm_stream_delay_ns(int64_t ns);
 void dlgm_mesh_ep_plan(const at::Tensor& offsets, at::Tensor plan, int64_t capacity, const at::Tensor& peers,
                        at::Tensor state, int64_t me, int64_t ch, int64_t region_off, int64_t slot_bytes,
                        int64_t slots, int64_t heap_bytes, int64_t timeout);
@@ -128,7 +128,7 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("gemm_lt(Tensor(a!) out, Tensor a, Tensor b, float beta, int algo) -> int");
   m.def("gemm_lt_tune(Tensor out, Tensor a, Tensor b, float beta, int n_heuristic, bool all_algos, int reps) -> Tensor");
   m.def("gemm_lt_version() -> int", &dlgm_gemm_lt_version);
-  m.def("spin_ns(int ns) -> ()", &dlgm_spin_ns);
+  m.def("stream_delay_ns(int ns) -> ()", &dlgm_stream_delay_ns);
   m.def("ipc_alloc(int nbytes, int mode=0) -> Tensor", &dlgm_ipc_alloc);
   m.def("ipc_handle(Tensor buf) -> Tensor", &dlgm_ipc_handle);
   m.def("ipc_open(Tensor handle) -> int", &dlgm_ipc_open);

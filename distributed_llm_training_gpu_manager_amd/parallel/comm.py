@@ -266,8 +266,9 @@ class ShadowComm(Comm):
 
     ``link_gbps`` (async mode): every collective first holds its comm stream for the time RCCL's ring needs on
     an xGMI link of that bus bandwidth (all-gather / reduce-scatter: (W-1)/W of the full buffer, all-reduce twice
-    that, all-to-all (W-1)/W of what this rank sends, at ``a2a_gbps``), with a wall-clock spin kernel
-    (csrc/kernels/spin.hip, one wave). The consumer's wait then sees that latency, so whether the engine's prefetch
+    that, all-to-all (W-1)/W of what this rank sends, at ``a2a_gbps``), with a host function on the stream that sleeps
+    that long (csrc/kernels/spin.hip: no compute unit taken). The consumer's wait then sees that latency, so whether
+    the engine's prefetch
     and bucketing hide the communication behind compute is measured on one GPU. Not modelled:
     the compute units RCCL's channels occupy, and contention between concurrent collectives on one link.
     """
@@ -311,7 +312,7 @@ class ShadowComm(Comm):
                 torch.cuda._sleep(self.delay_cycles)
             if link_ns:
                 from .._native import hip_ops
-                hip_ops().spin_ns(link_ns)
+                hip_ops().stream_delay_ns(link_ns)
             fn()
             ev = torch.cuda.Event()
             ev.record(s)

@@ -162,3 +162,29 @@ def test_dsconfig_auto_micro_batch():
     # without the model the request degrades to micro-batch 1 with a note
     cfg3, notes3 = engine_config_from_ds(ds, 8192)
     assert cfg3.micro_batch_size == 1 and any("needs the model" in n for n in notes3)
+
+
+def test_shadow_comm_link_model_accounts_ring_time():
+    """ShadowComm's link model: each collective is charged its ring time at the modelled xGMI bus
+    bandwidth -- (W-1)/W of the full buffer for all-gather / reduce-scatter, twice that for all-reduce, (W-1)/W of the
+    sent rows at the all-to-all bandwidth; siblings (sub-communicators) inherit the model."""
+    import torch
+    from distributed_llm_training_gpu_manager_amd.parallel.comm import ShadowComm
+    c = ShadowComm(8, 0, async_mode=True, link_gbps=100.0, a2a_gbps=50.0)
+    full = torch.zeros(8 * 1024 * 1024, dtype=torch.bfloat16)
+    c.all_gather(full, full[:1024 * 1024])
+    assert abs(c.modelled_s - 16 * 2 ** 20 * 7 / 8 / 100e9) < 1e-12
+    c.modelled_s = 0.0
+    out = torch.zeros(1024 * 1024, dtype=torch.float32)
+    c.reduce_scatter(out, torch.zeros(8 * 1024 * 1024, dtype=torch.float32))
+    assert abs(c.modelled_s - 32 * 2 ** 20 * 7 / 8 / 100e9) < 1e-12
+    c.modelled_s = 0.0
+    c.all_reduce(torch.zeros(1024, dtype=torch.float32))
+    assert abs(c.modelled_s - 2 * 4096 * 7 / 8 / 100e9) < 1e-15
+    c.modelled_s = 0.0
+    x = torch.zeros(64, 16, dtype=torch.bfloat16)
+    c.all_to_all_single(torch.zeros_like(x), x)
+    assert abs(c.modelled_s - 64 * 16 * 2 * 7 / 8 / 50e9) < 1e-15
+    sib = c.new_group(list(range(4)))
+    assert sib.link_gbps == 100.0 and sib.world == 4
+    assert ShadowComm(8, 0).modelled_s == 0.0 and ShadowComm(8, 0)._link_ns(1e9) == 0

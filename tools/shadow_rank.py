@@ -63,6 +63,7 @@ def main(argv=None) -> int:
     ap.add_argument("--live-params", default="hbm", help="stage3_max_live_parameters: 'hbm' or a number (1e9: reference)")
     ap.add_argument("--reuse-distance", default="hbm", help="stage3_max_reuse_distance: 'hbm' or a number")
     ap.add_argument("--local-grads", default="hbm", help="'hbm', 'on' or 'off' (off: reduce-scatter every micro-batch)")
+    ap.add_argument("--engine-kw", default="", help="more EngineConfig fields, 'name=value,...' (numbers parsed)")
     a = ap.parse_args(argv)
 
     import torch
@@ -82,6 +83,13 @@ def main(argv=None) -> int:
                         max_live_parameters=_knob(a.live_params), max_reuse_distance=_knob(a.reuse_distance),
                         local_grad_accum={"on": True, "off": False}.get(a.local_grads, a.local_grads),
                         expert_parallel_size=a.ep)
+    for kv in filter(None, a.engine_kw.split(",")):
+        k, v = kv.split("=", 1)
+        try:
+            v = float(v) if "." in v or "e" in v else int(v)
+        except ValueError:
+            pass
+        setattr(ecfg, k, v)
     t0 = time.time()
     comm = ShadowComm(a.world, a.rank, async_mode=a.async_comm or a.link_gbps > 0, link_gbps=a.link_gbps,
                       a2a_gbps=a.a2a_gbps)
