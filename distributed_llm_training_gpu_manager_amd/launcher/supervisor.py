@@ -424,8 +424,11 @@ class JobRegistry:
 
     def submit(self, spec: JobSpec) -> Job:
         job = Job(spec)
-        # start the first attempt synchronously so launch errors (missing binary) surface to the caller
-        proc = Supervisor(job)._start(resume=False)
+        # start the first attempt synchronously so launch errors (missing binary) surface to the caller -- after the
+        # shm snapshot files are reserved (Supervisor.run skips that for a job whose first attempt is already running)
+        first = Supervisor(job)
+        first.reserve_shm()
+        proc = first._start(resume=False)
         sup = Supervisor(job, first_proc=proc)
         with self._lock:
             self._jobs[spec.job_id] = job

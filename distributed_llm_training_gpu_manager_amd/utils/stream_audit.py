@@ -12,7 +12,9 @@ the edges themselves, independent of timing, the way ThreadSanitizer checks thre
   blocking device-to-host copy, ``.item()``) joins into a host clock that every later op inherits;
 * each access to device memory is recorded per storage and byte range with the stream and tick that made it. An access
   on stream T conflicts with an earlier access on stream S to overlapping bytes (at least one a write) unless
-  ``vc[T][S]`` has reached that tick: a read-after-write, write-after-read or write-after-write **race**;
+  ``vc[T][S]`` has reached that tick: a read-after-write, write-after-read or write-after-write **race**. Page-locked
+  host memory is tracked as well: H2D / D2H copies access it on their stream, CPU ops on it run on a ``host`` key
+  that is complete when the op returns (a CPU write into a buffer an earlier async D2H / H2D still uses is a race);
 * the caching allocator hands a freed block back to the stream that allocated it without waiting for other streams,
   unless the tensor was ``record_stream``-ed to them. When a new storage occupies bytes of a dead one, the dead
   storage's accesses on other streams (not covered by ``record_stream``) must be ordered before every access to the
@@ -45,7 +47,9 @@ from typing import Any, Callable, Dict, Hashable, List, Optional, Tuple
 
 Clock = Dict[Hashable, int]
 
-MAX_RECORDS = 48  # access records kept per storage (oldest dropped first: a bounded detector, never a false report)
+# access records kept per storage (oldest dropped first: a bounded detector, never a false report); raise it with
+# DLGM_STREAM_AUDIT_RECORDS for a deeper (slower) pass over buffers touched through many views
+MAX_RECORDS = int(os.environ.get("DLGM_STREAM_AUDIT_RECORDS", "48"))
 
 
 def enabled() -> bool:
@@ -148,8 +152,10 @@ class HazardModel:
 
     # ---------------------------------------------------------------- storages
     def storage(self, key: Hashable, base: int, nbytes: int, stream: Hashable, alive: Callable[[], bool],
-                name: str = "") -> StorageRec:
-        """The record of a storage, created (with the reuse check armed) the first time it is seen."""
+                name: str = "", reuse: bool = True) -> StorageRec:
+        """The record of a storage, created (with the reuse check armed unless `reuse` is False: pinned host blocks,
+        which the host caching allocator hands out again only after the streams that copied them are done) the first
+        time it is seen."""
         rec = self.recs.get(key)
         if rec is not None and rec.alive() and rec.base == base:
             return rec
@@ -162,7 +168,7 @@ class HazardModel:
         for k, old in cands:
             if old.alive() or old.base >= base + nbytes or old.base + old.nbytes <= base:
                 continue
-            for s, t in old.last_by_stream.items():
+            for s, t in (old.last_by_stream.items() if reuse else ()):
                 if s in old.record_streams:
                     continue  # the allocator itself waited for these before handing the block out again
                 new.pending.append((s, t, old.name))
@@ -251,6 +257,7 @@ class HazardModel:
             "\n".join(f"  [{i}] {h}" for i, h in enumerate(self.hazards))
 
 
+HOST = "host"  # the stream key of CPU ops on page-locked host memory
 _NAMES: Dict[Hashable, str] = {}  # stream key -> name (utils/streams.py registers every named stream here)
 # storage base pointer -> why: memory whose cross-stream accesses are ordered by a device-side protocol (atomics,
 # flags polled by the kernels themselves) rather than by stream edges; the audit does not track it
@@ -280,7 +287,15 @@ def _make_mode(model: HazardModel, fake_stream: Optional[Callable[[], Hashable]]
     syncing = {aten._local_scalar_dense.default, aten.nonzero.default, aten.equal.default,
                aten.is_nonzero.default}
     schema_cache: Dict[Any, Tuple[List[bool], List[bool]]] = {}
-    dev_ok = (lambda t: not t.is_cuda) if fake_stream is not None else (lambda t: t.is_cuda)
+
+    def pinned(t: "torch.Tensor") -> bool:
+        try:
+            return t.device.type == "cpu" and t.is_pinned()
+        except Exception:
+            return False
+    # page-locked host memory is tracked too: copies to / from it are accesses on their stream, CPU ops on it are
+    # accesses by the host (HOST), complete when they return (e.g. a D2H into a pinned buffer that the next H2D reads)
+    dev_ok = (lambda t: not t.is_cuda) if fake_stream is not None else (lambda t: t.is_cuda or pinned(t))
 
     def flags(func):
         f = schema_cache.get(func)
@@ -307,11 +322,13 @@ def _make_mode(model: HazardModel, fake_stream: Optional[Callable[[], Hashable]]
     def tracked(t: "torch.Tensor") -> bool:
         return dev_ok(t) and int(t.untyped_storage().data_ptr()) not in _PROTOCOL
 
-    def rec_of(t: "torch.Tensor", s: int):
+    def rec_of(t: "torch.Tensor", s: Hashable):
         st = t.untyped_storage()
         ref = StorageWeakRef(st)
+        host = fake_stream is None and not t.is_cuda
         return model.storage(ref.cdata, st.data_ptr(), st.nbytes(), s, lambda r=ref: not r.expired(),
-                             f"{tuple(t.shape)} {str(t.dtype)[6:]} storage@{st.data_ptr():#x}")
+                             f"{tuple(t.shape)} {str(t.dtype)[6:]} {'pinned ' if host else ''}storage@{st.data_ptr():#x}",
+                             reuse=not host)
 
     def span(t: "torch.Tensor") -> Tuple[int, int]:
         es = t.element_size()
@@ -342,8 +359,11 @@ def _make_mode(model: HazardModel, fake_stream: Optional[Callable[[], Hashable]]
             outs = [t for t in tensors(out) if isinstance(t, torch.Tensor) and dev_ok(t)]
             if not cuda_in and not outs:
                 return
-            dev = (cuda_in or outs)[0].device
-            s = fake_stream() if fake_stream is not None else int(torch.cuda.current_stream(dev).cuda_stream)
+            if fake_stream is not None:
+                s: Hashable = fake_stream()
+            else:
+                gpu = [t for t in cuda_in + outs if t.is_cuda]
+                s = int(torch.cuda.current_stream(gpu[0].device).cuda_stream) if gpu else HOST
             if func is aten.record_stream.default:
                 model.record_stream(rec_of(args[0], s), stream_key(args[1]))
                 return
@@ -389,8 +409,10 @@ def _make_mode(model: HazardModel, fake_stream: Optional[Callable[[], Hashable]]
                 any(isinstance(a, torch.Tensor) and not a.is_cuda for a in args[:1]))
             nb = bool(kwargs.get("non_blocking", False)) or (len(args) > 2 and args[2] is True and
                                                             func is aten.copy_.default)
-            if func in syncing or (cuda_in and host_out and not nb and func in (aten._to_copy.default,
-                                                                                 aten.copy_.default)):
+            if s == HOST:  # a CPU op on pinned memory has completed when it returns
+                model.host_sync({HOST: tick})
+            elif func in syncing or (cuda_in and host_out and not nb and func in (aten._to_copy.default,
+                                                                                   aten.copy_.default)):
                 model.host_sync(model.snapshot(s))
 
     return Mode()

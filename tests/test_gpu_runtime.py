@@ -119,18 +119,23 @@ def test_shm_save_falls_back_to_host_when_the_reservation_fails(tmp_path, monkey
     e.train_step([(t[:, :-1], t[:, 1:])])
     ck = C.AsyncCheckpointer(e, str(tmp_path), shm=True, disk=False)
     assert ck.mode == "shm" and ck.snap_bytes > 4 * (64 << 20)
-    ck.prepare_async()
-    time.sleep(0.12)  # a few pieces prepared, most not
     real, calls = ck._reserve, []
 
-    def full_after_two(fd, off, ln):
-        calls.append(off)
-        if len(calls) > 2:
+    def slow_then_full(fd, off, ln):
+        # the background preparation reserves slowly (a tmpfs reserves ~17 GB/s: unthrottled, the whole file would be
+        # reserved before the save arrives); the save's own reservation of the rest finds the tmpfs full. (The save
+        # joins the preparation thread and clears ck._prep before it reserves anything itself.)
+        calls.append((off, ck._prep is not None))
+        if ck._prep is None:
             ck.tier_notes.append("No space left on device (simulated)")
             return False
+        time.sleep(0.03)
         return real(fd, off, ln)
-    monkeypatch.setattr(ck, "_reserve", full_after_two)
+    monkeypatch.setattr(ck, "_reserve", slow_then_full)
+    ck.prepare_async()
+    time.sleep(0.12)  # a few pieces prepared, most not
     ck.save(1, {"step": 1}, blocking=True)
+    assert any(not prep for _, prep in calls), calls  # the save itself hit the full tmpfs
     rec = ck.history[-1]
     assert ck.mode == "host" and rec["mode"] == "host", rec
     assert any("snapshot tier -> host memory" in n for n in ck.tier_notes), ck.tier_notes
@@ -200,6 +205,7 @@ def _trainer(tmp, *extra):
                                "--log-interval", "100", "--telemetry-interval", "0", *extra]))
 
 
+@pytest.mark.no_stream_audit  # asserts host run-ahead: the audit's per-op Python work lets the GPU catch up
 def test_trainer_runs_ahead_and_nan_latch_keeps_pre_nan_state(tmp_path):
     from distributed_llm_training_gpu_manager_amd.launcher.supervisor import EXIT_NAN_HALT
 

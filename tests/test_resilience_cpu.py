@@ -262,13 +262,14 @@ def test_checkpointer_reports_prepared_after_background_preparation(tmp_path):
     ck.close(discard_shm=True)
 
 
-def test_supervisor_reserves_shm_snapshots_before_the_first_launch(tmp_path):
+@pytest.mark.parametrize("via", ["supervisor", "registry"])
+def test_supervisor_reserves_shm_snapshots_before_the_first_launch(tmp_path, via):
     """the supervisor (which outlives the ranks) reserves each rank's /dev/shm snapshot file before
     the first launch, sized by the planner from the training command; the checkpointer then finds every page reserved
     (prep_stats.pre_reserved: only mapping / page-locking left for an early spot notice), and a second reservation
     never touches a snapshot that is already there (it is the restore source of a relaunch)."""
     from distributed_llm_training_gpu_manager_amd.ckpt.checkpoint import reserve_snapshot_files, shm_snapshot_path
-    from distributed_llm_training_gpu_manager_amd.launcher.supervisor import (Job, JobSpec, Supervisor,
+    from distributed_llm_training_gpu_manager_amd.launcher.supervisor import (Job, JobRegistry, JobSpec, Supervisor,
                                                                                planned_snapshot_bytes)
     save = str(tmp_path / "ck")
     cmd = [sys.executable, "-c", "pass", "--model", "llama-tiny", "--zero-stage", "3"]
@@ -276,10 +277,17 @@ def test_supervisor_reserves_shm_snapshots_before_the_first_launch(tmp_path):
     eng = ZeroEngine(get_config("llama-tiny"), EngineConfig(zero_stage=3, micro_batch_size=1, seq_len=16,
                                                             init_device="cpu"), torch.device("cpu"))
     assert 14 * eng.shard_total <= nb <= 14 * eng.shard_total + (64 << 20)
-    job = Job(JobSpec(job_id="shm", argv=cmd, save_dir=save, run_dir=str(tmp_path / "run"), shm_reserve_bytes=nb))
-    sup = Supervisor(job)
-    sup.start()
-    sup.join(60)
+    spec = JobSpec(job_id="shm", argv=cmd, save_dir=save, run_dir=str(tmp_path / "run"), shm_reserve_bytes=nb)
+    if via == "supervisor":
+        job = Job(spec)
+        sup = Supervisor(job)
+        sup.start()
+        sup.join(60)
+    else:  # the API / drill path: JobRegistry.submit starts the first attempt itself, synchronously
+        job = JobRegistry().submit(spec)
+        t0 = time.time()
+        while job.status not in ("succeeded", "failed", "preempted") and time.time() - t0 < 60:
+            time.sleep(0.05)
     ev = [e for e in job.events if e["event"] == "shm_reserved"]
     path = shm_snapshot_path(save, 0)
     try:

@@ -183,3 +183,44 @@ def test_audit_names_a_missing_wait_and_a_missing_record_stream_on_the_gpu():
         torch.cuda.current_stream(dev).wait_stream(side)
         float(s)
     assert not c.hazards, c.report()
+
+
+def test_host_key_ops_complete_on_return():
+    """CPU ops on pinned memory (stream key HOST) are complete when they return: a later device copy on any stream is
+    ordered after them; but a host write over bytes an earlier async copy still reads is a WAR race."""
+    from distributed_llm_training_gpu_manager_amd.utils.stream_audit import HOST
+    m = HazardModel()
+    r = _rec(m, 1, 0x9000, 256, HOST, Box())
+    t = m.enqueue(HOST)
+    m.access(r, 0, 256, HOST, t, True, "host_fill")
+    m.host_sync({HOST: t})
+    _acc(m, r, S, False, what="h2d_read")  # queued after the host wrote: ordered
+    assert not m.hazards
+    t = m.enqueue(HOST)
+    m.access(r, 0, 64, HOST, t, True, "host_overwrite")  # the H2D may not have run yet
+    assert [h.kind for h in m.hazards] == ["WAR"] and "h2d_read" in m.hazards[0].first
+
+
+@pytest.mark.gpu
+@pytest.mark.no_stream_audit
+def test_audit_tracks_pinned_host_buffers_on_the_gpu():
+    """A D2H into a pinned buffer on one stream and an H2D out of it on another, without an event between them: the
+    RAW on page-locked host memory is named; with the event it is clean."""
+    dev = torch.device("cuda", 0)
+    side = torch.cuda.Stream(dev)
+    host = torch.empty(1 << 16, pin_memory=True)
+    for ordered in (False, True):
+        with stream_audit() as a:
+            x = torch.randn(1 << 16, device=dev)
+            host.copy_(x, non_blocking=True)  # D2H on compute
+            ev = torch.cuda.Event()
+            ev.record()
+            with torch.cuda.stream(side):
+                if ordered:
+                    side.wait_event(ev)
+                y = torch.empty(1 << 16, device=dev)
+                y.copy_(host, non_blocking=True)  # H2D on the side stream
+            torch.cuda.synchronize()
+        kinds = [h.kind for h in a.hazards]
+        assert kinds == ([] if ordered else ["RAW"]), a.report()
+        assert ordered or "pinned" in a.hazards[0].storage

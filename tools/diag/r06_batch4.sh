@@ -17,3 +17,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d /tmp/ovl -o ov
     --reuse-distance 1e9 --local-grads on --link-gbps 350 > gpurun_out/r06/ovl_trace.log 2>&1
 chk $? ovl_trace
 python tools/trace_overlap.py /tmp/ovl/ovl_kernel_trace.csv --skip-s 0 --out gpurun_out/r06/ovl_trace_summary.json | head -40
+# the corrected audit over the round-4 tree's shadow-async suite (the mesh cases need the protocol exemption HEAD has)
+(cd _bisect/r04 && DLGM_STREAM_AUDIT=1 timeout -k 10 400 python -u -m pytest -v --timeout 250 --timeout-method thread \
+    -p no:cacheprovider -m gpu tests/test_shadow_async_gpu.py -k "not mesh" > $GRAFT_REPO_ROOT/gpurun_out/r06/audit_r04_v3.log 2>&1)
+chk $? audit_r04; tail -1 gpurun_out/r06/audit_r04_v3.log
