@@ -12,6 +12,7 @@ eager PyTorch path.
 from __future__ import annotations
 
 import os
+import sys
 import threading
 from pathlib import Path
 
@@ -61,5 +62,14 @@ def hip_available() -> bool:
 
 
 def use_native(t: torch.Tensor) -> bool:
-    """True when `t` lives on the GPU (and therefore must use the HIP kernel)."""
-    return t.is_cuda and os.environ.get("DLGM_FORCE_REFERENCE", "0") != "1"
+    """True when `t` lives on the GPU (and therefore must use the HIP kernel). DLGM_FORCE_REFERENCE=1 sends every op
+    to its torch reference; a comma list of ops modules (e.g. ``attention,norm``) only those (a diagnostic bisect)."""
+    if not t.is_cuda:
+        return False
+    force = os.environ.get("DLGM_FORCE_REFERENCE", "0")
+    if force in ("", "0"):
+        return True
+    if force == "1":
+        return False
+    caller = sys._getframe(1).f_globals.get("__name__", "").rsplit(".", 1)[-1]
+    return caller not in force.split(",")

@@ -19,16 +19,16 @@ def grad_stats(grads: Sequence[torch.Tensor], out: torch.Tensor, accumulate: boo
     if use_native(out):
         hip_ops().grad_stats(list(grads), out, accumulate)
         return out
-    ss = torch.zeros((), dtype=torch.float64)
-    bad = torch.zeros((), dtype=torch.float64)
+    ss = torch.zeros((), dtype=torch.float64, device=out.device)
+    bad = torch.zeros((), dtype=torch.float64, device=out.device)
     for g in grads:
         gf = g.detach().float()
         fin = torch.isfinite(gf)
         bad += (~fin).sum()
         ss += torch.where(fin, gf, torch.zeros_like(gf)).double().pow(2).sum()
     if accumulate:
-        out[0] += ss.float().to(out.device)
-        out[1] += bad.float().to(out.device)
+        out[0] += ss.float()
+        out[1] += bad.float()
     else:
         out[0] = ss.float()
         out[1] = bad.float()

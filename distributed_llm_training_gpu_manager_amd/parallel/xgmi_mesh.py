@@ -36,6 +36,8 @@ workgroups and the data-moving kernels never wait.
 from __future__ import annotations
 
 import math
+import threading
+import weakref
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -67,6 +69,38 @@ class Region:
 
 def _round(x: int, m: int = ALIGN) -> int:
     return (int(x) + m - 1) // m * m
+
+
+# Heaps are kept for the life of the process and handed to the next mesh of the same device and memory kind: an
+# uncached heap is never returned to the driver. Freeing one and letting the caching allocator map the memory again
+# made later, unrelated engines compute different bits (round 6: synchronous shadow runs after mesh runs in one
+# process diverged from the first run in 2-30 of 35 repetitions, and a gather faulted after empty_cache; kept heaps,
+# fine-grained or plain heaps: 0 -- tools/diag/r06_stress.sh, README "Determinism"). Shadow meshes only (one process
+# builds many of them: the tests, the shadow-rank tools): a heap a peer process maps is exported over IPC, and a job
+# builds one mesh per communicator and frees it at exit.
+_HEAP_POOL: Dict[Tuple[int, int], List[torch.Tensor]] = {}
+_HEAP_LOCK = threading.Lock()
+
+
+def _pool_take(dev: int, mode: int, nbytes: int) -> Optional[torch.Tensor]:
+    with _HEAP_LOCK:
+        free = _HEAP_POOL.get((dev, mode), [])
+        fit = [h for h in free if h.numel() >= nbytes]
+        if not fit:
+            return None
+        h = min(fit, key=lambda t: t.numel())
+        free.remove(h)
+        return h
+
+
+def _pool_give(dev: int, mode: int, heap: torch.Tensor) -> None:
+    with _HEAP_LOCK:
+        _HEAP_POOL.setdefault((dev, mode), []).append(heap)
+
+
+def _release_heap(dev: int, mode: int, heap: torch.Tensor) -> None:
+    """weakref.finalize of a shadow mesh: its heap goes back to the pool."""
+    _pool_give(dev, mode, heap)
 
 
 class XgmiMesh:
@@ -102,6 +136,8 @@ class XgmiMesh:
             dist.all_gather_object(layouts, mine, group=comm.group)
             assert all(x == mine for x in layouts), f"mesh: heap layouts differ across ranks: {layouts}"
         self.heap, self.alloc_mode = self._alloc(ops, alloc_mode)
+        if self.shadow:
+            weakref.finalize(self, _release_heap, self._dev_index(), ALLOC_MODES.index(self.alloc_mode), self.heap)
         self._opened: List[int] = []
         ptrs = [0] * self.W
         ptrs[self.rank] = int(self.heap.data_ptr())
@@ -134,12 +170,22 @@ class XgmiMesh:
             self.host_barrier()
 
     # ------------------------------------------------------------------ setup
+    def _dev_index(self) -> int:
+        return self.device.index if self.device.index is not None else torch.cuda.current_device()
+
     def _alloc(self, ops, mode: str):
-        """Uncached heap if the driver exports it over IPC; else fine-grained, else plain (recorded)."""
+        """Uncached heap if the driver exports it over IPC; else fine-grained, else plain (recorded). A shadow mesh
+        reuses a pooled heap of the kind (a dead shadow mesh's, at least this large), zeroed, when there is one."""
         order = {"auto": (0, 1, 2), "uncached": (0,), "fine-grained": (1,), "coarse-grained": (2,)}[mode]
         err = None
         with torch.cuda.device(self.device):
             for m in order:
+                pooled = _pool_take(self._dev_index(), m, self.heap_bytes) if self.shadow else None
+                if pooled is not None:
+                    torch.cuda.synchronize(self.device)  # the previous owner's kernels are done with it
+                    pooled[:self.heap_bytes].zero_()
+                    torch.cuda.synchronize(self.device)
+                    return pooled, ALLOC_MODES[m]
                 try:
                     buf = ops.ipc_alloc(self.heap_bytes, m)
                     if self.W > 1 and not self.shadow:

@@ -536,8 +536,8 @@ def poison_allocations(value: float = float("nan")):
     class Poison(TorchDispatchMode):
         def __torch_dispatch__(self, func, types, args=(), kwargs=None):
             out = func(*args, **(kwargs or {}))
-            if func in factories and isinstance(out, torch.Tensor) and out.is_cuda and out.is_floating_point() \
-                    and out.numel() > 0:
+            if func in factories and isinstance(out, torch.Tensor) and out.is_floating_point() and out.numel() > 0 \
+                    and (out.is_cuda or (out.device.type == "cpu" and out.is_pinned())):  # pinned staging too
                 out.fill_(value)
             return out
 
