@@ -16,6 +16,7 @@
 #include <omp.h>
 #include <stdint.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 #include <zlib.h>
@@ -231,6 +232,37 @@ uint64_t dlgm_touch_pages(const void* ptr, size_t n, int nthreads) {
   worker();
   for (auto& t : ts) t.join();
   return total.load();
+}
+
+// Map the pages of [ptr, ptr + n) (a shared /dev/shm file mapping) WRITABLE into this process on `nthreads`
+// threads: madvise(MADV_POPULATE_WRITE) over 64 MiB slices. On the MI355X host (24 GiB of a reserved snapshot
+// file) this maps at 64 GB/s on 8-16 threads where touching one byte per page ran at 13-14 GB/s on any number of
+// threads, and the page-lock (hipHostRegister) of pages mapped this way runs at 118-133 GB/s instead of 37-41 GB/s
+// (no write upgrade of read-mapped pages): profiles/shm_map_bench_r06.json. Returns 0, or the errno of the first
+// failed slice (EINVAL on kernels older than 5.14: the caller falls back to touching).
+int dlgm_populate_write(void* ptr, size_t n, int nthreads) {
+  constexpr size_t kSlice = 64u << 20;
+  constexpr int kPopulateWrite = 23;  // MADV_POPULATE_WRITE (Linux 5.14)
+  const size_t nslices = (n + kSlice - 1) / kSlice;
+  std::atomic<size_t> next{0};
+  std::atomic<int> err{0};
+  auto worker = [&]() {
+    for (;;) {
+      const size_t i = next.fetch_add(1);
+      if (i >= nslices || err.load()) break;
+      const size_t len = std::min(kSlice, n - i * kSlice);
+      if (madvise((char*)ptr + i * kSlice, len, kPopulateWrite) != 0) {
+        int e = errno, zero = 0;
+        err.compare_exchange_strong(zero, e);
+      }
+    }
+  };
+  nthreads = std::max(1, std::min<int>(nthreads, (int)std::max<size_t>(nslices, 1)));
+  std::vector<std::thread> ts;
+  for (int t = 1; t < nthreads; ++t) ts.emplace_back(worker);
+  worker();
+  for (auto& t : ts) t.join();
+  return err.load();
 }
 
 // dst <- src (n bytes) on `nthreads` threads in `chunk` pieces, with the CRC32C of every chunk of the copied

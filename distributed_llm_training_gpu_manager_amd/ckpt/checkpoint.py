@@ -60,6 +60,8 @@ MODEL0 = "mp_rank_00_model_states.pt"
 # 1 GiB pieces with 5 ms pauses kept the first step after a restore at 0.9 s (one whole-file registration: 6.4 s)
 REG_CHUNK = 1 << 30
 REG_PAUSE_S = 0.005
+# threads that map each piece (MADV_POPULATE_WRITE, _host.populate_pages) before it is page-locked
+MAP_THREADS = 16
 # pinned slots of the capture into a not-yet-page-locked part of the shm snapshot (_ring_capture)
 RING_SLOT = 256 << 20
 RING_SLOTS = 4
@@ -379,13 +381,14 @@ class AsyncCheckpointer:
     def _ready_pipeline(self, hi: int, stop=None, pause: float = 0.0, on_locked=None) -> int:
         """Snapshot pieces [_reg_done, hi) of REG_CHUNK bytes through three stages that run concurrently, one piece
         apart: a thread reserves (posix_fallocate: a full tmpfs is an error here, not a SIGBUS in a later copy),
-        a thread maps (reads one byte per 4 KiB page through the mapping: read faults map 16 pages at a time), and
-        the calling thread page-locks (hipHostRegister), then calls on_locked(off, ln). On the MI355X host, one
-        24 GiB pass each: reserve 17-19.5 GB/s, map 15-19 GB/s (16 threads were no faster), page-lock mapped pages
-        55-58 GB/s against 12.6 GB/s for reserved-but-unmapped ones and 8 GB/s for a sparse file
-        (profiles/shm_map_bench_r05.json) -- so the pipeline runs at about the reserve rate. Without a GPU it only
-        reserves. Returns the end of the page-locked range (< hi after a stop or a failed registration: the rest
-        then goes through the pinned slots)."""
+        a thread maps the pages writable (MADV_POPULATE_WRITE on MAP_THREADS threads; one byte read per page where
+        that is unavailable), and the calling thread page-locks (hipHostRegister), then calls on_locked(off, ln). On
+        the MI355X host, 24 GiB each: reserve 17-19.5 GB/s; map 64 GB/s by populate-write on 8-16 threads against
+        13-16 GB/s by touching (on any number of threads); page-lock 118-133 GB/s for populate-written pages, 37-41
+        for read-touched ones, 12.6 for reserved-but-unmapped ones (profiles/shm_map_bench_r05.json, _r06.json) -- so
+        a supervisor-reserved file is mapped and locked at ~40 GB/s. Without a GPU it only reserves. Returns the end
+        of the page-locked range (< hi after a stop or a failed registration: the rest then goes through the pinned
+        slots)."""
         fns = self._hip_register_fns() if self.cuda else None
         if self.cuda and fns is None:
             cr = torch.cuda.cudart()
@@ -414,7 +417,9 @@ class AsyncCheckpointer:
                 if self._falloc_done < off + ln:
                     time.sleep(0.0005)
                     continue
-                int(self._snap[off:off + ln][::4096].sum())  # one byte per page: map it
+                piece = self._snap[off:off + ln]
+                if not _host.populate_pages(piece, MAP_THREADS):  # writable, on threads (64 GB/s on MI355X host)
+                    int(piece[::4096].sum())  # one byte per page: map it (13-16 GB/s on one or more threads)
                 self._mapped_done = off + ln
 
         ths = [threading.Thread(target=reserve, daemon=True, name="ckpt-reserve")]

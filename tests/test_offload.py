@@ -177,3 +177,27 @@ def test_touch_pages_maps_a_shared_file_and_sums_one_byte_per_page(tmp_path):
     t[0], t[4096 * 7], t[4096 * 7 + 1], t[n - 4096] = 3, 5, 100, 11  # the +1 byte is not on a page start
     assert _host.touch_pages(t, 4) == 3 + 5 + 11
     assert _host.touch_pages(t[:8192], 16) == 3
+
+
+def test_populate_pages_maps_a_reserved_shm_file_writable_and_keeps_its_bytes(tmp_path):
+    """_host.populate_pages (MADV_POPULATE_WRITE on threads, csrc/host/ckpt_io.cpp): the snapshot pipeline's map
+    stage. It must not change any byte (a restore source may already be in the file) and must cover every slice,
+    the last partial one included."""
+    import os
+    n = (130 << 20) + 4096 * 3  # three 64 MiB slices, the last one short
+    path = "/dev/shm/dlgm-test-populate.snap" if os.path.isdir("/dev/shm") else str(tmp_path / "snap")
+    fd = os.open(path, os.O_RDWR | os.O_CREAT, 0o600)
+    try:
+        os.ftruncate(fd, n)
+        os.posix_fallocate(fd, 0, n)
+        os.close(fd)
+        t = torch.from_file(path, shared=True, size=n, dtype=torch.uint8)
+        t[0], t[(64 << 20) + 5], t[n - 1] = 7, 9, 11
+        ok = _host.populate_pages(t, 8)
+        assert ok or _host.lib() is None  # Linux >= 5.14 with the host library built
+        assert (int(t[0]), int(t[(64 << 20) + 5]), int(t[n - 1])) == (7, 9, 11)
+        assert int(t.sum()) == 7 + 9 + 11
+        del t
+    finally:
+        if os.path.exists(path):
+            os.unlink(path)
