@@ -60,8 +60,9 @@ MODEL0 = "mp_rank_00_model_states.pt"
 # 1 GiB pieces with 5 ms pauses kept the first step after a restore at 0.9 s (one whole-file registration: 6.4 s)
 REG_CHUNK = 1 << 30
 REG_PAUSE_S = 0.005
+REG_DUTY = 0.3  # background preparation: at most this fraction of the wall time inside hipHostRegister
 # threads that map each piece (MADV_POPULATE_WRITE, _host.populate_pages) before it is page-locked
-MAP_THREADS = 16
+MAP_THREADS = 8
 # pinned slots of the capture into a not-yet-page-locked part of the shm snapshot (_ring_capture)
 RING_SLOT = 256 << 20
 RING_SLOTS = 4
@@ -449,12 +450,16 @@ class AsyncCheckpointer:
                         break
                     self._reg.append((ptr + off, ln))
                     self._reg_done = off + ln
-                    self.prep_stats["register_s"] = round(self.prep_stats.get("register_s", 0.0) + time.time() - tr, 3)
+                    dt = time.time() - tr
+                    self.prep_stats["register_s"] = round(self.prep_stats.get("register_s", 0.0) + dt, 3)
                     if on_locked is not None:
                         on_locked(off, ln)
                     off += ln
                     if pause > 0 and off < hi:
-                        time.sleep(pause)
+                        # background preparation: hipHostRegister holds the HIP runtime, so the training thread's
+                        # launches wait while it runs -- keep it to REG_DUTY of the wall time (with populate-written
+                        # pages a 1 GiB piece locks in ~8 ms; back to back they held the first Mixtral step at 5.9 s)
+                        time.sleep(max(pause, dt * (1.0 / REG_DUTY - 1.0)))
         finally:
             halt.set()
             for t in ths:
