@@ -85,12 +85,11 @@ _HEAP_LOCK = threading.Lock()
 def _pool_take(dev: int, mode: int, nbytes: int) -> Optional[torch.Tensor]:
     with _HEAP_LOCK:
         free = _HEAP_POOL.get((dev, mode), [])
-        fit = [h for h in free if h.numel() >= nbytes]
+        fit = [i for i, h in enumerate(free) if h.numel() >= nbytes]
         if not fit:
             return None
-        h = min(fit, key=lambda t: t.numel())
-        free.remove(h)
-        return h
+        # by index: list.remove would compare tensors with ==
+        return free.pop(min(fit, key=lambda i: free[i].numel()))
 
 
 def _pool_give(dev: int, mode: int, heap: torch.Tensor) -> None:
