@@ -238,11 +238,11 @@ uint64_t dlgm_touch_pages(const void* ptr, size_t n, int nthreads) {
 // threads: madvise(MADV_POPULATE_WRITE) over 64 MiB slices. On the MI355X host (24 GiB of a reserved snapshot
 // file) this maps at 64 GB/s on 8-16 threads where touching one byte per page ran at 13-14 GB/s on any number of
 // threads, and the page-lock (hipHostRegister) of pages mapped this way runs at 118-133 GB/s instead of 37-41 GB/s
-// (no write upgrade of read-mapped pages): profiles/shm_map_bench_r06.json. Returns 0, or the errno of the first
-// failed slice (EINVAL on kernels older than 5.14: the caller falls back to touching).
-int dlgm_populate_write(void* ptr, size_t n, int nthreads) {
+// (no write upgrade of read-mapped pages): profiles/shm_map_bench_r06.json. write = 0: MADV_POPULATE_READ instead.
+// Returns 0, or the errno of the first failed slice (EINVAL on kernels older than 5.14: the caller touches instead).
+int dlgm_populate_pages(void* ptr, size_t n, int nthreads, int write) {
   constexpr size_t kSlice = 64u << 20;
-  constexpr int kPopulateWrite = 23;  // MADV_POPULATE_WRITE (Linux 5.14)
+  const int advice = write ? 23 : 22;  // MADV_POPULATE_WRITE / MADV_POPULATE_READ (Linux 5.14)
   const size_t nslices = (n + kSlice - 1) / kSlice;
   std::atomic<size_t> next{0};
   std::atomic<int> err{0};
@@ -251,7 +251,7 @@ int dlgm_populate_write(void* ptr, size_t n, int nthreads) {
       const size_t i = next.fetch_add(1);
       if (i >= nslices || err.load()) break;
       const size_t len = std::min(kSlice, n - i * kSlice);
-      if (madvise((char*)ptr + i * kSlice, len, kPopulateWrite) != 0) {
+      if (madvise((char*)ptr + i * kSlice, len, advice) != 0) {
         int e = errno, zero = 0;
         err.compare_exchange_strong(zero, e);
       }

@@ -52,9 +52,9 @@ def lib():
                                               ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)]
         L.dlgm_touch_pages.restype = ctypes.c_uint64
         L.dlgm_touch_pages.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-        if hasattr(L, "dlgm_populate_write"):
-            L.dlgm_populate_write.restype = ctypes.c_int
-            L.dlgm_populate_write.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        if hasattr(L, "dlgm_populate_pages"):
+            L.dlgm_populate_pages.restype = ctypes.c_int
+            L.dlgm_populate_pages.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
         L.dlgm_close_file.restype = ctypes.c_int
         L.dlgm_close_file.argtypes = [ctypes.c_int, ctypes.c_int]
         L.dlgm_aio_create.restype = ctypes.c_void_p
@@ -171,16 +171,16 @@ def touch_pages(t: torch.Tensor, threads: int = THREADS) -> int:
     return int(L.dlgm_touch_pages(ctypes.c_void_p(t.data_ptr()), n, int(threads)))
 
 
-def populate_pages(t: torch.Tensor, threads: int = 16) -> bool:
-    """Map the pages of a contiguous CPU tensor (a mapped /dev/shm file) writable into this process with
-    MADV_POPULATE_WRITE on `threads` threads (csrc/host/ckpt_io.cpp: 64 GB/s on the MI355X host, and the page-lock
-    after it 3x faster than after a read touch). False when unavailable (old kernel, library not built): the caller
-    touches the pages instead."""
+def populate_pages(t: torch.Tensor, threads: int = 16, write: bool = True) -> bool:
+    """Map the pages of a contiguous CPU tensor (a mapped /dev/shm file) into this process with MADV_POPULATE_WRITE
+    (or _READ) on `threads` threads (csrc/host/ckpt_io.cpp: 64 GB/s on the MI355X host, and the page-lock after a
+    populate-write 3x faster than after a read touch). False when unavailable (old kernel, library not built): the
+    caller touches the pages instead."""
     L = lib()
     n = t.numel() * t.element_size()
-    if L is None or not hasattr(L, "dlgm_populate_write") or n == 0:
+    if L is None or not hasattr(L, "dlgm_populate_pages") or n == 0:
         return False
-    return int(L.dlgm_populate_write(ctypes.c_void_p(t.data_ptr()), n, int(threads))) == 0
+    return int(L.dlgm_populate_pages(ctypes.c_void_p(t.data_ptr()), n, int(threads), int(bool(write)))) == 0
 
 
 def cpu_adamw_(p, m, v, g, p16, lr, b1, b2, eps, wd, bc1, bc2, gscale=1.0) -> None:

@@ -60,7 +60,8 @@ MODEL0 = "mp_rank_00_model_states.pt"
 # 1 GiB pieces with 5 ms pauses kept the first step after a restore at 0.9 s (one whole-file registration: 6.4 s)
 REG_CHUNK = 1 << 30
 REG_PAUSE_S = 0.005
-REG_DUTY = 0.3  # background preparation: at most this fraction of the wall time inside hipHostRegister
+# background preparation: at most this fraction of the wall time inside hipHostRegister (DLGM_SHM_REG_DUTY)
+REG_DUTY = float(os.environ.get("DLGM_SHM_REG_DUTY", "0.3"))
 # threads that map each piece (MADV_POPULATE_WRITE, _host.populate_pages) before it is page-locked
 MAP_THREADS = 8
 # pinned slots of the capture into a not-yet-page-locked part of the shm snapshot (_ring_capture)
@@ -124,13 +125,38 @@ def shm_snapshot_path(save_dir: str, rank: int) -> str:
     return f"/dev/shm/dlgm-ckpt-{key}-r{int(rank)}.snap"
 
 
+def _prefault(fd: int, lo: int, hi: int) -> None:
+    """Fault the reserved pages [lo, hi) of a tmpfs file in once, through a throw-away mapping (threaded
+    MADV_POPULATE_WRITE): tmpfs zeroes a fallocated page at its first fault, so after this a rank's own mapping only
+    builds page tables. Without it the ranks' first touch zeroed 82 GB beside the training loop (the first Mixtral
+    step of a fresh job: 5-9 s instead of 1.3-2 s). Best effort: a failure leaves the zeroing to the ranks."""
+    import ctypes
+    import mmap
+    if hi <= lo:
+        return
+    try:
+        mm = mmap.mmap(fd, hi, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+    except (OSError, ValueError):
+        return
+    try:
+        buf = (ctypes.c_char * hi).from_buffer(mm)
+        try:
+            L = _host.lib()
+            if L is not None and hasattr(L, "dlgm_populate_pages"):
+                L.dlgm_populate_pages(ctypes.c_void_p(ctypes.addressof(buf) + lo), hi - lo, 16, 1)
+        finally:
+            del buf
+    finally:
+        mm.close()
+
+
 def reserve_snapshot_files(save_dir: str, ranks, nbytes: int, threads: int = 8) -> Dict[str, Any]:
     """Reserve (posix_fallocate: tmpfs pages allocated and zeroed) the snapshot file of every rank in `ranks`, at
     least `nbytes` each, WITHOUT touching what a file already holds (a previous attempt's snapshot is the restore
     source): only missing bytes past its current allocation are added. Runs in the supervisor, which outlives the
     ranks, before the first launch: the ranks' own background preparation then finds every page
-    reserved, and a spot notice at step 1 pays only for mapping and page-locking (~15-55 GB/s) instead of the
-    3.5-6 GB/s of fresh tmpfs pages. Returns {files, bytes_added, seconds}."""
+    reserved and already faulted in once (zeroed, _prefault), and a spot notice at step 1 pays only for mapping and
+    page-locking instead of the 3.5-6 GB/s of fresh tmpfs pages. Returns {files, bytes_added, seconds}."""
     import concurrent.futures as cf
     t0 = time.time()
     if not os.path.isdir("/dev/shm") or nbytes <= 0:
@@ -160,6 +186,7 @@ def reserve_snapshot_files(save_dir: str, ranks, nbytes: int, threads: int = 8) 
             pieces = [(o, min(piece, nbytes - o)) for o in range(off - off % piece, nbytes, piece)]
             with cf.ThreadPoolExecutor(max(1, threads // max(1, len(jobs)))) as ex:
                 list(ex.map(lambda a: os.posix_fallocate(fd, a[0], a[1]), pieces))
+            _prefault(fd, off - off % piece, nbytes)
         finally:
             os.close(fd)
     with cf.ThreadPoolExecutor(max(1, min(len(jobs), threads))) as ex:
@@ -382,8 +409,9 @@ class AsyncCheckpointer:
     def _ready_pipeline(self, hi: int, stop=None, pause: float = 0.0, on_locked=None) -> int:
         """Snapshot pieces [_reg_done, hi) of REG_CHUNK bytes through three stages that run concurrently, one piece
         apart: a thread reserves (posix_fallocate: a full tmpfs is an error here, not a SIGBUS in a later copy),
-        a thread maps the pages writable (MADV_POPULATE_WRITE on MAP_THREADS threads; one byte read per page where
-        that is unavailable), and the calling thread page-locks (hipHostRegister), then calls on_locked(off, ln). On
+        a thread maps the pages (inside a save: writable, MADV_POPULATE_WRITE on MAP_THREADS threads; in the
+        background preparation, or where that is unavailable: one byte read per page, which leaves the training
+        loop alone), and the calling thread page-locks (hipHostRegister), then calls on_locked(off, ln). On
         the MI355X host, 24 GiB each: reserve 17-19.5 GB/s; map 64 GB/s by populate-write on 8-16 threads against
         13-16 GB/s by touching (on any number of threads); page-lock 118-133 GB/s for populate-written pages, 37-41
         for read-touched ones, 12.6 for reserved-but-unmapped ones (profiles/shm_map_bench_r05.json, _r06.json) -- so
@@ -419,7 +447,11 @@ class AsyncCheckpointer:
                     time.sleep(0.0005)
                     continue
                 piece = self._snap[off:off + ln]
-                if not _host.populate_pages(piece, MAP_THREADS):  # writable, on threads (64 GB/s on MI355X host)
+                # a save maps with MADV_POPULATE_WRITE on threads (64 GB/s); the background preparation touches one
+                # byte per page instead: populate threads running beside the training loop held the first Mixtral
+                # step at 5-9 s (touching: 1.3 s), profiles/drills_mixtral_8x7b_ep8_shadow_r06.json "map_ab"
+                mode = os.environ.get("DLGM_SHM_MAP") or ("touch" if pause > 0 else "write")
+                if mode == "touch" or not _host.populate_pages(piece, MAP_THREADS, write=mode != "read"):
                     int(piece[::4096].sum())  # one byte per page: map it (13-16 GB/s on one or more threads)
                 self._mapped_done = off + ln
 
