@@ -259,7 +259,7 @@ class AsyncCheckpointer:
         self._unreg = None
         self._restored_map: Optional[torch.Tensor] = None  # the shm file mapped by a restore (reused, see _load_shm)
         self._ring: List[torch.Tensor] = []
-        self._stream = owned_stream(self.dev, "ckpt") if self.cuda else None
+        self._stream = owned_stream(self.dev, "ckpt", owner=self) if self.cuda else None
         self.last_ring: Dict[str, Any] = {}
         self.defer_moments = True  # shm restore: Adam moments restored beside the first step (_load_shm)
         self._moments: Optional[threading.Thread] = None
@@ -1136,7 +1136,7 @@ class AsyncCheckpointer:
         if split < len(jobs):
             self.restore_stats["deferred_GiB"] = round(sum(j[2] for j in jobs[split:]) / 2 ** 30, 1)
             td = time.time()
-            stream = owned_stream(self.dev, "ckpt-restore")
+            stream = owned_stream(self.dev, "ckpt-restore", owner=self)
 
             def background():
                 try:

@@ -44,7 +44,7 @@ class NanTrap:
         self._pending: Deque = deque()
         self._lock = threading.Lock()
         self._done = threading.Condition(self._lock)
-        self._stream = owned_stream(device, "nan-trap") if self._cuda else None
+        self._stream = owned_stream(device, "nan-trap", owner=self) if self._cuda else None
         self._stop = threading.Event()
         self._poll_s = poll_s
         self._thread = threading.Thread(target=self._watch, daemon=True, name="nan-trap")

@@ -304,7 +304,7 @@ class ShadowComm(Comm):
         dev = tensors[0].device
         cur = torch.cuda.current_stream(dev)
         if self._stream is None:
-            self._stream = owned_stream(dev, "shadow-comm")
+            self._stream = owned_stream(dev, "shadow-comm", owner=self)
         s = self._stream
         s.wait_stream(cur)
         with torch.cuda.stream(s):

@@ -66,7 +66,7 @@ class HostOffloadOptimizer:
             mk = lambda: torch.zeros(numel, dtype=torch.float32, pin_memory=self.cuda)  # noqa: E731
             self.master, self.exp_avg, self.exp_avg_sq = mk(), mk(), mk()
         if self.cuda:
-            self.stream = owned_stream(device, "offload")
+            self.stream = owned_stream(device, "offload", owner=self)
             self.gslot = [torch.empty(self.chunk, dtype=torch.float32, pin_memory=True) for _ in range(2)]
             self.pslot = [torch.empty(self.chunk, dtype=dtype, pin_memory=True) for _ in range(2)]
 
@@ -377,7 +377,7 @@ class ActivationOffloader:
     def __init__(self, device: torch.device):
         self.device = device
         self.cuda = device.type == "cuda"
-        self.stream = owned_stream(device, "offload") if self.cuda else None
+        self.stream = owned_stream(device, "offload", owner=self) if self.cuda else None
         self._pool: dict = {}
 
     def _host_buf(self, t: torch.Tensor) -> torch.Tensor:

@@ -162,7 +162,7 @@ class XgmiMesh:
         self.timeout_ticks = int(timeout_s * 100e6)  # s_memrealtime runs at 100 MHz on MI355X
         # one stream per traffic class (parameter gathers / gradient reductions), like the engine's two RCCL
         # communicators: a prefetch gather and a reduce-scatter run concurrently
-        self._streams: Dict[str, torch.cuda.Stream] = {k: owned_stream(device, f"mesh-{k}") for k in ("ag", "rs")}
+        self._streams: Dict[str, torch.cuda.Stream] = {k: owned_stream(device, f"mesh-{k}", owner=self) for k in ("ag", "rs")}
         self.closed = False
         self.issued = 0
         if self.W > 1 and not self.shadow:  # nobody may write into a heap before every rank mapped every heap

@@ -632,11 +632,11 @@ class ZeroEngine:
                                              aio_threads=self.cfg.aio_threads,
                                              aio_block_size=self.cfg.aio_block_size)
             self.p16_shard = self.param_nvme.mapped  # cold paths (checkpoints, host optimizer) use the mapping
-            self._h2d = owned_stream(dev, "param-h2d") if self.is_cuda else None
+            self._h2d = owned_stream(dev, "param-h2d", owner=self) if self.is_cuda else None
             self._p16_ready = None
         elif self.param_host:
             self.p16_shard = torch.zeros(n, dtype=self.dtype, pin_memory=self.is_cuda)
-            self._h2d = owned_stream(dev, "param-h2d") if self.is_cuda else None
+            self._h2d = owned_stream(dev, "param-h2d", owner=self) if self.is_cuda else None
             self._p16_ready = None  # event: host bf16 partition final (after the device AdamW's D2H)
         elif self.mesh is not None:  # peers pull their gathers straight out of this rank's heap
             self.p16_shard = self.mesh.region_tensor("p16", self.dtype, n)
@@ -1306,7 +1306,7 @@ class ZeroEngine:
         GEMMs run at the board's power cap; profiles/optimizer_overlap_ab_r04.json)."""
         cfg = self.cfg
         if self._opt_stream is None:
-            self._opt_stream = owned_stream(self.device, "optimizer")
+            self._opt_stream = owned_stream(self.device, "optimizer", owner=self)
             self._opt_stats = torch.empty_like(self.stats)
             self._opt_sst = torch.empty_like(sst) if sst is not None else None
         self._opt_stats.copy_(self.stats)

@@ -20,6 +20,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
+import weakref
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -79,16 +80,40 @@ def dedicated_stream(device: torch.device, name: str) -> "torch.cuda.Stream":
     return s
 
 
-def owned_stream(device: torch.device, kind: str, slots: int = 16) -> "torch.cuda.Stream":
+_FREE: Dict[Tuple[int, str], list] = {}  # (device, kind) -> leased streams whose owner is gone
+
+
+def _give_back(key: Tuple[int, str], s) -> None:
+    with _LOCK:
+        _FREE.setdefault(key, []).append(s)
+
+
+def owned_stream(device: torch.device, kind: str, owner: Optional[object] = None,
+                 slots: int = 16) -> "torch.cuda.Stream":
     """A dedicated stream for an object that owns one for its lifetime (a communicator, a mesh, the optimizer /
-    checkpoint / NaN-trap copy streams): the next of `slots` streams of this kind, so the live objects of one
-    engine never share a HIP stream while a process that builds thousands of them (the test suite) reuses a few."""
+    checkpoint / NaN-trap copy streams). With `owner`, the stream is LEASED: no other live owner of any kind holds it
+    (a free one of this kind is reused, else a new one is created), and it returns to the kind's free list when the
+    owner is garbage-collected -- a process that builds thousands of owners (the test suite) creates only as many
+    streams as were ever live at once. Without an owner: the next of `slots` round-robin streams of this kind."""
     if _POOL:  # diagnostic A/B only: the round-4 behaviour (a fresh stream from torch's round-robin pool)
         return torch.cuda.Stream(device)
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if owner is None:
+        with _LOCK:
+            k = _KIND_NEXT.get(kind, 0)
+            _KIND_NEXT[kind] = k + 1
+        return dedicated_stream(device, f"{kind}#{k % slots}")
+    key = (idx, kind)
     with _LOCK:
-        k = _KIND_NEXT.get(kind, 0)
-        _KIND_NEXT[kind] = k + 1
-    return dedicated_stream(device, f"{kind}#{k % slots}")
+        free = _FREE.get(key)
+        s = free.pop() if free else None
+        if s is None:
+            k = _KIND_NEXT.get("lease:" + kind, 0)
+            _KIND_NEXT["lease:" + kind] = k + 1
+    if s is None:
+        s = dedicated_stream(device, f"{kind}@{k}")
+    weakref.finalize(owner, _give_back, key, s)
+    return s
 
 
 def side_stream(device: torch.device, name: str) -> Optional["torch.cuda.Stream"]:
