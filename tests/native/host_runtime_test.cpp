@@ -2,6 +2,7 @@
 // CRC32C against published check values, multi-threaded write/read round trips with per-chunk
 // CRCs (odd sizes, chunk tails), streamed pwrite_at pieces, and the AVX2 AdamW against a scalar
 // double-precision reference on a length that exercises the vector body and the scalar tail.
+#include <cerrno>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -9,6 +10,10 @@
 #include <cstring>
 #include <string>
 #include <vector>
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
 extern "C" {
 uint32_t dlgm_crc32c(const void* p, size_t n, uint32_t seed);
@@ -20,6 +25,8 @@ void dlgm_cpu_adamw(float* p, float* m, float* v, const float* g, uint16_t* p16,
 int dlgm_open_write(const char* path, size_t total);
 int dlgm_pwrite_at(int fd, const void* ptr, size_t n, size_t offset, size_t chunk, int nthreads, uint32_t* crcs);
 int dlgm_close_file(int fd, int do_fsync);
+uint64_t dlgm_touch_pages(const void* ptr, size_t n, int nthreads);
+int dlgm_populate_pages(void* ptr, size_t n, int nthreads, int write);
 }
 
 static int failures = 0;
@@ -74,6 +81,29 @@ int main(int argc, char** argv) {
   std::remove(path.c_str());
   // reading a missing file fails cleanly
   CHECK(dlgm_read_file((dir + "/does_not_exist.bin").c_str(), back.data(), 16, chunk, 1, rc.data()) != 0);
+
+  // a shared file mapping: populate (write and read advice) on threads keeps every byte, touch sums one per page;
+  // the length leaves a short last 64 MiB slice
+  {
+    const size_t fn = (130u << 20) + 3 * 4096;
+    const std::string fpath = dir + "/dlgm_host_selftest.map";
+    int mfd = open(fpath.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0600);
+    CHECK(mfd >= 0 && ftruncate(mfd, (off_t)fn) == 0);
+    uint8_t* mp = (uint8_t*)mmap(nullptr, fn, PROT_READ | PROT_WRITE, MAP_SHARED, mfd, 0);
+    CHECK(mp != MAP_FAILED);
+    if (mp != MAP_FAILED) {
+      mp[0] = 3;
+      mp[(64u << 20) + 4096] = 5;
+      mp[fn - 4096] = 11;
+      const int w = dlgm_populate_pages(mp, fn, 8, 1), r = dlgm_populate_pages(mp, fn, 3, 0);
+      CHECK((w == 0 && r == 0) || (w == EINVAL && r == EINVAL));  // EINVAL: a kernel older than 5.14
+      CHECK(mp[0] == 3 && mp[(64u << 20) + 4096] == 5 && mp[fn - 4096] == 11);
+      CHECK(dlgm_touch_pages(mp, fn, 4) == 3 + 5 + 11);
+      munmap(mp, fn);
+    }
+    if (mfd >= 0) close(mfd);
+    std::remove(fpath.c_str());
+  }
 
   // AdamW vs a double-precision scalar reference
   const size_t m = 8192 * 3 + 13;
