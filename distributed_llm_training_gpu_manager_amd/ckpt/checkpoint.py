@@ -125,7 +125,7 @@ def shm_snapshot_path(save_dir: str, rank: int) -> str:
     return f"/dev/shm/dlgm-ckpt-{key}-r{int(rank)}.snap"
 
 
-def _prefault(fd: int, lo: int, hi: int) -> None:
+def _prefault(fd: int, lo: int, hi: int, threads: int = 16) -> None:
     """Fault the reserved pages [lo, hi) of a tmpfs file in once, through a throw-away mapping (threaded
     MADV_POPULATE_WRITE): tmpfs zeroes a fallocated page at its first fault, so after this a rank's own mapping only
     builds page tables. Without it the ranks' first touch zeroed 82 GB beside the training loop (the first Mixtral
@@ -143,7 +143,7 @@ def _prefault(fd: int, lo: int, hi: int) -> None:
         try:
             L = _host.lib()
             if L is not None and hasattr(L, "dlgm_populate_pages"):
-                L.dlgm_populate_pages(ctypes.c_void_p(ctypes.addressof(buf) + lo), hi - lo, 16, 1)
+                L.dlgm_populate_pages(ctypes.c_void_p(ctypes.addressof(buf) + lo), hi - lo, int(threads), 1)
         finally:
             del buf
     finally:
@@ -186,7 +186,7 @@ def reserve_snapshot_files(save_dir: str, ranks, nbytes: int, threads: int = 8) 
             pieces = [(o, min(piece, nbytes - o)) for o in range(off - off % piece, nbytes, piece)]
             with cf.ThreadPoolExecutor(max(1, threads // max(1, len(jobs)))) as ex:
                 list(ex.map(lambda a: os.posix_fallocate(fd, a[0], a[1]), pieces))
-            _prefault(fd, off - off % piece, nbytes)
+            _prefault(fd, off - off % piece, nbytes, max(2, 16 // max(1, len(jobs))))  # ~16 threads in all
         finally:
             os.close(fd)
     with cf.ThreadPoolExecutor(max(1, min(len(jobs), threads))) as ex:

@@ -1,0 +1,22 @@
+#!/usr/bin/env python3
+"""Round 6: Mixtral 2-layer bench A/B -- VARIANT=nowt: no cached expert-weight transposes (the grouped dX GEMMs read
+the [E, out, in] weights MN-contiguous instead of a per-step rebuilt [E, in, out] copy). Runs bench.py's main."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+from distributed_llm_training_gpu_manager_amd.parallel import zero as Z  # noqa: E402
+
+v = os.environ.get("VARIANT", "")
+if v == "nowt":
+    orig = Z.ZeroEngine.__init__
+
+    def init(self, model_cfg, cfg, *a, **k):
+        cfg.expert_weight_cache = False
+        orig(self, model_cfg, cfg, *a, **k)
+    Z.ZeroEngine.__init__ = init
+import bench  # noqa: E402
+
+sys.argv = ["bench.py", "--model", "mixtral-8x7b", "--n-layers", "2", "--seq", "4096", "--ga", "4", "--steps", "15",
+            "--warmup", "3", "--no-telemetry"]
+sys.exit(bench.main())
