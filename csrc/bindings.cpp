@@ -69,7 +69,8 @@ int64_t dlgm_gemm_lt_version();
 // gemm_mfma.hip
 void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bool accumulate,
                     const c10::optional<at::Tensor>& offsets, int64_t mode, int64_t M, int64_t N, int64_t K,
-                    int64_t G, int64_t b_gstride, const c10::optional<at::Tensor>& stats_part);
+                    int64_t G, int64_t b_gstride, const c10::optional<at::Tensor>& stats_part,
+                    const c10::optional<at::Tensor>& glu);
 void dlgm_gemm_mfma_seg(at::Tensor out, const std::vector<at::Tensor>& a, const std::vector<at::Tensor>& b,
                         const at::Tensor& offsets, bool accumulate, bool kmajor);
 
@@ -143,7 +144,7 @@ TORCH_LIBRARY(dlgm, m) {
   m.def("mesh_ep_plan(Tensor offsets, Tensor(a!) plan, int capacity, Tensor peers, Tensor(b!) state, int me, int ch, int region_off, int slot_bytes, int slots, int heap_bytes, int timeout) -> ()");
   m.def("mesh_push_rows(Tensor x, Tensor plan, bool combine, Tensor peers, Tensor(a!) state, int me, int ch, int region_off, int slot_bytes, int hdr_bytes, int slots, int slot_rows, int heap_bytes, int n_experts) -> ()");
   m.def("mesh_copy_rows(Tensor(a!) out, Tensor? nrows, Tensor peers, Tensor(b!) state, int me, int ch, int region_off, int slot_bytes, int hdr_bytes, int slots, int heap_bytes) -> ()");
-  m.def("gemm_mfma(Tensor(a!) out, Tensor a, Tensor b, bool accumulate, Tensor? offsets, int mode, int M, int N, int K, int G, int b_gstride, Tensor(b!)? stats_part=None) -> ()");
+  m.def("gemm_mfma(Tensor(a!) out, Tensor a, Tensor b, bool accumulate, Tensor? offsets, int mode, int M, int N, int K, int G, int b_gstride, Tensor(b!)? stats_part=None, Tensor? glu=None) -> ()");
   m.def("gemm_mfma_seg(Tensor(a!) out, Tensor[] a, Tensor[] b, Tensor offsets, bool accumulate, bool kmajor=False) -> ()");
 }
 

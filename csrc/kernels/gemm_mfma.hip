@@ -68,6 +68,11 @@ struct GemmArgs {
   int nreal;           // grouped-K with the chunk remap: real blocks (the grid is rounded up to 8 * kChunk)
   float* stats_part;   // grouped-K fp32 epilogues: per-tile (sum of squares of the finite, #non-finite) of the
                        // FINAL C values, at [2 * tile] (deterministic: reduced later in a fixed order)
+  // bf16 epilogue fused with the SwiGLU backward (the MoE down projection's input gradient): the tile's values are
+  // dA = dY @ W_down; instead of storing dA, read gate / up of the same rows and columns from glu ([rows, 2 glu_f],
+  // row stride ldc) and store dgate at column c and dup at column glu_f + c of C ([rows, 2 glu_f])
+  const bf16* glu;
+  int glu_f;
 };
 
 
@@ -574,6 +579,31 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
     }
     __syncthreads();
     const int half = lane >> 5, c = lane & 31;
+    if (p.glu != nullptr) {
+      // SwiGLU backward on the rounded bf16 dA (the same values and the same fp32 math as swiglu_bwd_kernel)
+#pragma unroll 2
+      for (int it = 0; it < 16; ++it) {
+        const int r = 32 * w + 2 * it + half;
+        if (r >= rows_valid) break;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + r * 512 + ((c ^ (r & 31)) << 4));
+        const int64_t row = (int64_t)(m0 + r) * p.ldc;
+        const int col = n0 + c * 8;
+        const f32x8 g = load8f(p.glu + row + col), u = load8f(p.glu + row + p.glu_f + col);
+        const f32x8 d = __builtin_convertvector(v, f32x8);
+        f32x8 dg, du;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float sg_ = 1.f / (1.f + __expf(-g[j]));
+          const float gs = g[j] * sg_;
+          du[j] = d[j] * gs;
+          dg[j] = d[j] * u[j] * (sg_ + gs * (1.f - sg_));
+        }
+        bf16* out = reinterpret_cast<bf16*>(C) + row + col;
+        store8f(out, dg);
+        store8f(out + p.glu_f, du);
+      }
+      return;
+    }
 #pragma unroll 4
     for (int it = 0; it < 16; ++it) {
       const int r = 32 * w + 2 * it + half;
@@ -666,7 +696,8 @@ void launch_epi(int epi, dim3 grid, hipStream_t st, const GemmArgs& a) {
 // b_gstride elements per group; mode 2 grouped-K: offsets split the K rows, out is [G, M, N].
 void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bool accumulate,
                     const c10::optional<at::Tensor>& offsets, int64_t mode, int64_t M, int64_t N, int64_t K,
-                    int64_t G, int64_t b_gstride, const c10::optional<at::Tensor>& stats_part) {
+                    int64_t G, int64_t b_gstride, const c10::optional<at::Tensor>& stats_part,
+                    const c10::optional<at::Tensor>& glu) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda() && out.is_cuda(), "gemm_mfma: GPU tensors");
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16, "gemm_mfma: bf16 operands");
   TORCH_CHECK(a.dim() == 2 && b.dim() >= 2 && out.dim() >= 2, "gemm_mfma: 2-D operand views");
@@ -716,13 +747,23 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
   p.qskip = 1;
   p.chunk = 1;
   p.splitk = 1;
+  const bool fused_glu = glu.has_value() && glu->defined();
+  if (fused_glu) {  // out = dgu [rows, 2N] (dgate | dup), glu = gu [rows, 2N]: the SwiGLU backward in the epilogue
+    TORCH_CHECK(mode == kGroupM && !out32 && !accumulate, "gemm_mfma(glu): a grouped-M bf16 store");
+    TORCH_CHECK(glu->is_cuda() && glu->scalar_type() == at::kBFloat16 && glu->is_contiguous() && glu->dim() == 2 &&
+                    glu->size(1) == 2 * N && out.is_contiguous() && out.sizes() == glu->sizes() && glu->size(0) >= M,
+                "gemm_mfma(glu): gu and out must be contiguous bf16 [rows, 2N]");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(glu->data_ptr()) % 16 == 0, "gemm_mfma(glu): 16-byte aligned gu");
+    p.glu = reinterpret_cast<const bf16*>(glu->data_ptr());
+    p.glu_f = (int)N;
+  }
   // narrow grouped-M problems (<= 16 column tiles: the expert down projection and input gradients) fill only ~2.2
   // rounds of 256 CUs, so a third round runs ~20 % full: split the long K in two (fp32 partials + one reduce)
   at::Tensor part;
   at::Tensor out_final = out;
   // (round 4: splitting K >= 8192 in two and K >= 24576 in three measured 3-7 % slower on the Mixtral shapes than
   // this rule: the fp32 partial traffic outweighs the fuller last round; profiles/gemm_splitk_policy_ab_r04.jsonl)
-  if (mode == kGroupM && !out32 && out.is_contiguous() && ldc == N && p.tiles_n <= 16 && K >= 16384) {
+  if (mode == kGroupM && !out32 && !fused_glu && out.is_contiguous() && ldc == N && p.tiles_n <= 16 && K >= 16384) {
     p.splitk = 2;
     part = at::empty({p.splitk, M, N}, out.options().dtype(at::kFloat));
     p.c = part.data_ptr();

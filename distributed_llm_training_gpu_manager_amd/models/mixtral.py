@@ -143,9 +143,10 @@ class MixtralBlock(LlamaBlock):
         if self._grouped(x):
             offs = dctx.local_offsets
             dy = dy.contiguous()
-            da_all = self._grouped_dx(dy, p, "w_down", offs)
-            dgu_all = ops.swiglu_bwd(da_all, gu_all, dctx.nrows)
-            del da_all
+            # dA = dY @ W_down fused with the SwiGLU backward in the grouped GEMM's epilogue (dA never stored)
+            wt = p.get("w_down.T")
+            dgu_all = (gm.grouped_dx_swiglu(dy, wt, offs, gu_all) if wt is not None
+                       else gm.grouped_dx_swiglu(dy, p["w_down"], offs, gu_all, transpose_w=False))
             dx = self._grouped_dx(dgu_all, p, "w_gate_up", offs)
             if ctx is not None and ctx.defer_wgrad:
                 # dW once per step over the micro-batches' rows regrouped expert-major on the device

@@ -18,6 +18,7 @@ permitted when stream is capturing": it synchronises) and ran 117.5k tok/s again
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -94,6 +95,24 @@ def grouped_mm(x: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, transpos
             we = w[e].t() if transpose_w else w[e]
             out[lo:hi] = (x[lo:hi].float() @ we.float()).to(out.dtype)
     return out
+
+
+def grouped_dx_swiglu(dy: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, gu: torch.Tensor,
+                      transpose_w: bool = True) -> torch.Tensor:
+    """The MoE down projection's input gradient fused with the SwiGLU backward: dA = dy @ w[e]^T per group (as
+    grouped_mm), then dgu = swiglu_bwd(dA, gu) -- in the GEMM's epilogue on the GPU, so dA never reaches HBM (a
+    [rows, F] write and read saved per micro-batch and layer). gu [R, 2F] (gate | up); returns dgu [R, 2F]. Rows
+    outside every group are left unwritten, as swiglu_bwd leaves rows past nrows."""
+    if use_native(dy) and os.environ.get("DLGM_MOE_FUSED_SWIGLU", "1") != "0":
+        G = w.shape[0]
+        N = w.shape[1] if transpose_w else w.shape[2]
+        R, K = dy.shape
+        out = torch.empty_like(gu)
+        b = w.transpose(1, 2) if transpose_w else w
+        hip_ops().gemm_mfma(out, dy, b, False, offsets, GROUP_M, R, N, K, G, w.stride(0), None, gu)
+        return out
+    from .activation import swiglu_bwd
+    return swiglu_bwd(grouped_mm(dy, w, offsets, transpose_w), gu)
 
 
 def grouped_wgrad(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, offsets: torch.Tensor,

@@ -86,6 +86,37 @@ def test_grouped_rows_forward_uneven_and_empty_groups():
 
 
 @pytest.mark.parametrize("transpose_w", [True, False])
+def test_grouped_dx_fused_swiglu_bwd_matches_unfused(transpose_w, monkeypatch):
+    """The down projection's input gradient with the SwiGLU backward in the epilogue is bit-exact with the unfused
+    pair (grouped_mm -> swiglu_bwd kernel): same bf16 rounding of dA, same fp32 math; uneven, empty, single-row and
+    partial-tile groups. Also within bf16 tolerance of the fp32 PyTorch reference."""
+    g = torch.Generator(device=dev).manual_seed(11)
+    sizes = [300, 0, 1, 513, 256, 77]
+    R, K, F, G = sum(sizes), 512, 768, len(sizes)
+    offs = torch.tensor([0] + list(torch.tensor(sizes).cumsum(0)), dtype=torch.int32, device=dev)
+    dy = torch.randn(R, K, device=dev, generator=g).to(torch.bfloat16)
+    w = (torch.randn(G, F, K, device=dev, generator=g) if transpose_w else
+         torch.randn(G, K, F, device=dev, generator=g)).to(torch.bfloat16) * 0.1
+    gu = torch.randn(R, 2 * F, device=dev, generator=g).to(torch.bfloat16)
+    monkeypatch.setenv("DLGM_MOE_FUSED_SWIGLU", "1")
+    got = gm.grouped_dx_swiglu(dy, w, offs, gu, transpose_w=transpose_w)
+    monkeypatch.setenv("DLGM_MOE_FUSED_SWIGLU", "0")
+    ref = gm.grouped_dx_swiglu(dy, w, offs, gu, transpose_w=transpose_w)
+    assert got.shape == gu.shape and got.dtype == torch.bfloat16
+    assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
+    lo = 0
+    for e, n in enumerate(sizes):
+        if n:
+            we = w[e].float().t() if transpose_w else w[e].float()
+            d = dy[lo:lo + n].float() @ we
+            gg, uu = gu[lo:lo + n, :F].float(), gu[lo:lo + n, F:].float()
+            s = torch.sigmoid(gg)
+            want = torch.cat([d * uu * (s + gg * s * (1 - s)), d * gg * s], dim=1)
+            assert _rel(got[lo:lo + n], want) < 2e-2, e
+        lo += n
+
+
+@pytest.mark.parametrize("transpose_w", [True, False])
 def test_grouped_rows_narrow_long_k_split_k(transpose_w):
     """Narrow output (<= 16 column tiles) with a long K: the grouped-M launch splits K in two (fp32 partials + a
     reduce kernel), uneven / empty / single-row groups; also the balanced XCD remap over the real tiles."""
