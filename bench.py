@@ -116,7 +116,9 @@ def main() -> int:
     ap.add_argument("--mesh-sweep", default="auto", choices=["auto", "on", "off"],
                     help="after the result line, in a child process per rank: check the mesh and RCCL against each "
                          "other and one process ([mesh-check] on stderr), then on the GPU measure the device-driven "
-                         "xGMI mesh collectives (auto: when WORLD_SIZE > 1)")
+                         "xGMI mesh collectives (auto: when WORLD_SIZE > 1 on the CPU; on GPUs only at WORLD_SIZE >= 8, the "
+                         "full node -- the driver's last scaling run -- so the untried peer-mapped transport cannot "
+                         "disturb the smaller runs before it)")
     ap.add_argument("--xgmi-mesh", default="off", choices=["on", "off"],
                     help="run the ZeRO collectives over the device-driven xGMI mesh instead of RCCL rings")
     ap.add_argument("--defer-expert-wgrad", default="auto", choices=["auto", "on", "off"],
@@ -291,7 +293,8 @@ def main() -> int:
         dog.cancel()
         if out is not None:
             out["extra"]["comm_busbw"] = rows
-    mesh_sweep = args.mesh_sweep == "on" or (args.mesh_sweep == "auto" and env.world > 1)
+    mesh_sweep = args.mesh_sweep == "on" or (args.mesh_sweep == "auto" and env.world > 1 and
+                                              (env.device.type != "cuda" or env.world >= 8))
     port = None
     if mesh_sweep and env.world > 1:  # agree on the child job's rendezvous port while the group still exists
         pt = torch.tensor([_free_port() if env.rank == 0 else 0], dtype=torch.int64, device=env.device)
