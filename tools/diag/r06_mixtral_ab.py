@@ -15,6 +15,10 @@ if v == "nowt":
         cfg.expert_weight_cache = False
         orig(self, model_cfg, cfg, *a, **k)
     Z.ZeroEngine.__init__ = init
+elif v == "tcmain":  # the per-step W^T rebuild on the compute stream instead of the "tcache" side stream
+    from distributed_llm_training_gpu_manager_amd.utils import streams as S
+    _side = S.side_stream
+    S.side_stream = lambda device, name: None if name == "tcache" else _side(device, name)
 import bench  # noqa: E402
 
 sys.argv = ["bench.py", "--model", "mixtral-8x7b", "--n-layers", "2", "--seq", "4096", "--ga", "4", "--steps", "15",
