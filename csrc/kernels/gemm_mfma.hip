@@ -30,6 +30,7 @@
 // Work order: blocks are remapped so consecutive tiles (sharing an A row panel) land on one XCD.
 #include <torch/all.h>
 #include <c10/hip/HIPStream.h>
+#include <cstdlib>
 #include "dlgm_common.h"
 
 using namespace dlgm;
@@ -73,7 +74,54 @@ struct GemmArgs {
   // row stride ldc) and store dgate at column c and dup at column glu_f + c of C ([rows, 2 glu_f])
   const bf16* glu;
   int glu_f;
+  // grouped-M tail split (narrow launches, bf16 out): per XCD, the whole rounds of tiles run unsplit and a last
+  // round at most half full runs with every tile's K range in two halves (twice the blocks, each half as long);
+  // those blocks store fp32 partials at tpart [2][M][N] that tail_reduce_kernel sums into C. xcu = CUs per XCD
+  // (one block per CU: the kernel's LDS and registers admit one)
+  int tsplit, xcu;
+  float* tpart;
 };
+
+// Per-XCD plan of the tail split: the XCD runs tiles [x q, x q + qx); the first `full` of them unsplit; if
+// `split`, the remaining `tail` tiles as two K halves each.
+struct TailPlan {
+  int qx, full, tail;
+  bool split;
+};
+
+__device__ __forceinline__ TailPlan tail_plan(int real, int q, int x, int xcu) {
+  TailPlan t;
+  t.qx = max(0, min(q, real - x * q));
+  const int whole = t.qx / xcu * xcu;
+  t.tail = t.qx - whole;
+  t.split = t.tail > 0 && 2 * t.tail <= xcu;
+  t.full = t.split ? whole : t.qx;
+  return t;
+}
+
+// grouped-M: the tiles of a group are its row tiles x all column tiles, group after group, row tiles fastest
+// (see the kernel). Tile j -> group, column tile, first row and row end; false past the last group's tiles.
+__device__ __forceinline__ bool group_tile(const GemmArgs& p, int j, int& grp, int& tn, int& m_lo, int& m_hi) {
+  for (int e = 0; e < p.G; ++e) {
+    const int lo = p.offsets[e], hi = p.offsets[e + 1];
+    const int te = (hi - lo + BM - 1) / BM;
+    if (j < te * p.tiles_n) {
+      grp = e;
+      tn = j / te;
+      m_lo = lo + (j - tn * te) * BM;
+      m_hi = hi;
+      return true;
+    }
+    j -= te * p.tiles_n;
+  }
+  return false;
+}
+
+__device__ __forceinline__ int grouped_real_tiles(const GemmArgs& p) {
+  int real = 0;
+  for (int e = 0; e < p.G; ++e) real += (p.offsets[e + 1] - p.offsets[e] + BM - 1) / BM;
+  return real * p.tiles_n;
+}
 
 
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
@@ -255,17 +303,28 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
   // grouped-M grids are sized for the worst case and their tail is spare blocks: the XCD-contiguous remap over the
   // whole grid hands every spare id to the last XCD(s) and leaves them idle (the real tiles are the low ids)
   int id;
+  int thalf = -1;  // tail split: the K half (0 / 1) of a split tail tile this block computes; -1 = the whole tile
   if constexpr (MODE == kGroupM) {
     if (p.chunk) {
       // balanced XCD-contiguous order over the REAL tiles (counted from the device offsets): XCD x runs ids
       // [x*q, (x+1)*q) first and its spare blocks last, so every XCD gets 1/8 of the work and each keeps the
       // contiguous, L2-sharing run of an expert's tiles
-      int real = 0;
-      for (int e = 0; e < p.G; ++e) real += (p.offsets[e + 1] - p.offsets[e] + BM - 1) / BM;
-      real *= p.tiles_n * p.splitk;
+      const int real = grouped_real_tiles(p) * p.splitk;
       const int q = (real + 7) / 8, x = blockIdx.x & 7, k = blockIdx.x >> 3;
-      id = x * q + k;
-      if (k >= q || id >= real) return;  // spare block (grid sized for the worst case)
+      if (p.tsplit) {  // the XCD's whole rounds unsplit, then its short last round as K halves (two blocks a tile)
+        const TailPlan tp = tail_plan(real, q, x, p.xcu);
+        if (k < tp.full) {
+          id = x * q + k;
+        } else if (tp.split && k - tp.full < 2 * tp.tail) {
+          id = x * q + tp.full + ((k - tp.full) >> 1);
+          thalf = (k - tp.full) & 1;
+        } else {
+          return;  // spare block
+        }
+      } else {
+        id = x * q + k;
+        if (k >= q || id >= real) return;  // spare block (grid sized for the worst case)
+      }
     } else {
       id = xcd_remap(blockIdx.x, gridDim.x);
     }
@@ -314,20 +373,13 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
       k_hi = min(p.K, k_lo + ks);
       split_off = (int64_t)part * p.c_sstride;
     }
-    grp = -1;
-    for (int e = 0; e < p.G; ++e) {
-      const int lo = p.offsets[e], hi = p.offsets[e + 1];
-      const int te = (hi - lo + BM - 1) / BM;
-      if (j < te * p.tiles_n) {
-        grp = e;
-        tn = j / te;
-        m_lo = lo + (j - tn * te) * BM;  // this block's first row (absolute)
-        m_hi = hi;
-        break;
-      }
-      j -= te * p.tiles_n;
+    if (thalf >= 0) {
+      const int ks = ((p.K + 1) / 2 + BK - 1) / BK * BK;
+      k_lo = thalf * ks;
+      k_hi = min(p.K, k_lo + ks);
     }
-    if (grp < 0) return;  // spare block: the grid is sized for the worst case
+    // expert by expert, row tiles fastest (group_tile); m_lo = this block's first row (absolute)
+    if (!group_tile(p, j, grp, tn, m_lo, m_hi)) return;  // spare block: the grid is sized for the worst case
   } else {  // grouped-K (one segment, or kGroupKSeg: the group's rows of every segment)
     const int per = p.tiles_m * p.tiles_n;
     grp = id / per;
@@ -561,6 +613,20 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
     }
   };
   constexpr bool KSTATS = (MODE == kGroupK || MODE == kGroupKSeg) && EPI != kStoreBf16;
+  if constexpr (MODE == kGroupM && EPI == kStoreBf16) {
+    if (thalf >= 0) {  // a split tail tile: this K half's fp32 partial, summed into C by tail_reduce_kernel
+      float* T = p.tpart + (int64_t)thalf * p.M * p.N;
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) {
+        const int mrow = wr * 128 + 16 * mi + i;
+        if (mrow >= rows_valid) continue;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          *reinterpret_cast<f32x4*>(T + (int64_t)(m0 + mrow) * p.N + n0 + wc * 64 + 16 * ni + 4 * g) = acc[mi][ni];
+      }
+      return;
+    }
+  }
   if constexpr (EPI == kStoreBf16) {
     // bf16 tile through LDS: the accumulators' native layout gives 8-byte stores of 16 rows x 32 B each; staged as
     // a row-major [256][512 B] image (16-B chunk c of row r at c ^ (r & 31): conflict-free 8-byte writes and
@@ -678,6 +744,31 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 }
 
 
+// C rows / columns of the split tail tiles = tpart[0] + tpart[1] -> bf16. One block per possible split tile
+// (8 XCDs x xcu / 2), which recomputes the kernel's plan from the device offsets; idle when its slot is unused.
+__global__ __launch_bounds__(256) void tail_reduce_kernel(GemmArgs p) {
+  const int half = max(1, p.xcu / 2);
+  const int x = blockIdx.x / half, s = blockIdx.x - x * half;
+  const int real = grouped_real_tiles(p);
+  const int q = (real + 7) / 8;
+  const TailPlan tp = tail_plan(real, q, x, p.xcu);
+  if (!tp.split || s >= tp.tail) return;
+  int grp, tn, m_lo, m_hi;
+  if (!group_tile(p, x * q + tp.full + s, grp, tn, m_lo, m_hi)) return;
+  const int rows = min(BM, m_hi - m_lo);
+  const int64_t slice = (int64_t)p.M * p.N;
+  const int c = (threadIdx.x & 31) * 8;
+  bf16* C = reinterpret_cast<bf16*>(p.c);
+  for (int r = threadIdx.x >> 5; r < rows; r += 8) {
+    const int64_t o = (int64_t)(m_lo + r) * p.N + tn * BN + c;
+    const f32x4 a0 = *reinterpret_cast<const f32x4*>(p.tpart + o) + *reinterpret_cast<const f32x4*>(p.tpart + slice + o);
+    const f32x4 a1 =
+        *reinterpret_cast<const f32x4*>(p.tpart + o + 4) + *reinterpret_cast<const f32x4*>(p.tpart + slice + o + 4);
+    const f32x8 v = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    store8f(C + (int64_t)(m_lo + r) * p.ldc + tn * BN + c, v);
+  }
+}
+
 template <int MODE, bool AK, bool BKM>
 void launch_epi(int epi, dim3 grid, hipStream_t st, const GemmArgs& a) {
   if (epi == kStoreBf16)
@@ -763,7 +854,26 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
   at::Tensor out_final = out;
   // (round 4: splitting K >= 8192 in two and K >= 24576 in three measured 3-7 % slower on the Mixtral shapes than
   // this rule: the fp32 partial traffic outweighs the fuller last round; profiles/gemm_splitk_policy_ab_r04.jsonl)
-  if (mode == kGroupM && !out32 && !fused_glu && out.is_contiguous() && ldc == N && p.tiles_n <= 16 && K >= 16384) {
+  // round 6: the tail split instead -- each XCD runs its whole rounds of tiles unsplit and only a last round at most
+  // half full as K halves (fp32 partials for those tiles alone); DLGM_GEMM_TSPLIT=0 restores the rule above
+  static const bool tsplit_on = [] {
+    const char* e = std::getenv("DLGM_GEMM_TSPLIT");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  at::Tensor tpart;
+  if (mode == kGroupM && !out32 && !fused_glu && p.tiles_n <= 16 && K >= 4096 && tsplit_on) {
+    static int cu_count[64] = {};  // per device, queried once
+    int dev = 0;
+    DLGM_CHECK_HIP(hipGetDevice(&dev));
+    int& cus = cu_count[dev & 63];
+    if (cus == 0) DLGM_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    p.tsplit = 1;
+    p.xcu = std::max(2, cus / 8);
+    tpart = at::empty({2, M, N}, out.options().dtype(at::kFloat));
+    p.tpart = tpart.data_ptr<float>();
+  }
+  if (mode == kGroupM && !out32 && !fused_glu && !p.tsplit && out.is_contiguous() && ldc == N && p.tiles_n <= 16 &&
+      K >= 16384) {
     p.splitk = 2;
     part = at::empty({p.splitk, M, N}, out.options().dtype(at::kFloat));
     p.c = part.data_ptr();
@@ -781,6 +891,7 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
     p.offsets = offsets->data_ptr<int>();
     if (mode == kGroupM) {
       nblk = ((M + BM - 1) / BM + G) * p.tiles_n * p.splitk;  // M = total rows: worst-case tiles over all groups
+      if (p.tsplit) nblk += 8 * (p.xcu / 2);  // an XCD's split tail takes up to xcu / 2 more blocks
       nblk = (nblk + 7) / 8 * 8;  // whole rounds of the 8 XCDs (the balanced remap's block -> XCD mapping)
     } else {
       nblk = G * (int64_t)p.tiles_m * p.tiles_n;
@@ -818,6 +929,10 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
     launch_epi<kGroupK, false, false>(epi, grid, st, p);
   }
   DLGM_CHECK_HIP(hipGetLastError());
+  if (p.tsplit) {
+    tail_reduce_kernel<<<8 * (p.xcu / 2), 256, 0, st>>>(p);
+    DLGM_CHECK_HIP(hipGetLastError());
+  }
   if (p.splitk > 1) {
     TORCH_CHECK(out_final.is_contiguous() && out_final.size(-1) == N && (N % 8) == 0, "gemm_mfma: split-K out layout");
     const int64_t n = M * N;

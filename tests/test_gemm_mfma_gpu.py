@@ -136,6 +136,30 @@ def test_grouped_rows_narrow_long_k_split_k(transpose_w):
         lo += n
 
 
+@pytest.mark.parametrize("sizes", [
+    [1500, 0, 1, 2100, 700, 1800, 1200, 891],      # 36 row tiles x 16 = 576: 72 per XCD -> 2 rounds + a split tail of 8
+    [2560, 2561, 0, 2048, 1280, 1287, 768, 100],   # 44 row tiles: 88 per XCD -> a tail of 24 (> half a round), unsplit
+])
+@pytest.mark.parametrize("transpose_w", [True, False])
+def test_grouped_rows_narrow_tail_split(sizes, transpose_w):
+    """Narrow grouped-M launch at the Mixtral down-projection shape (N = 4096, K = 4096): each XCD's whole rounds of
+    tiles store bf16 directly, a last round at most half full runs as K halves whose fp32 partials the tail reduce
+    sums (the tiles on both sides of that split, partial row tiles and an empty group included)."""
+    g = torch.Generator(device=dev).manual_seed(13)
+    R, K, N, G = sum(sizes), 4096, 4096, len(sizes)
+    offs = torch.tensor([0] + list(torch.tensor(sizes).cumsum(0)), dtype=torch.int32, device=dev)
+    x = torch.randn(R, K, device=dev, generator=g).to(torch.bfloat16)
+    w = (torch.randn(G, N, K, device=dev, generator=g) if transpose_w else
+         torch.randn(G, K, N, device=dev, generator=g)).to(torch.bfloat16)
+    out = gm.grouped_mm(x, w, offs, transpose_w=transpose_w)
+    lo = 0
+    for e, n in enumerate(sizes):
+        if n:
+            we = w[e].float().t() if transpose_w else w[e].float()
+            assert _rel(out[lo:lo + n], x[lo:lo + n].float() @ we) < 1e-2, e
+        lo += n
+
+
 def test_grouped_weight_gradient_uneven_and_empty_groups():
     g = torch.Generator(device=dev).manual_seed(3)
     sizes = [130, 0, 700, 1]
