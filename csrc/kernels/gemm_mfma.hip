@@ -74,10 +74,10 @@ struct GemmArgs {
   // row stride ldc) and store dgate at column c and dup at column glu_f + c of C ([rows, 2 glu_f])
   const bf16* glu;
   int glu_f;
-  // grouped-M tail split (narrow launches, bf16 out): per XCD, the whole rounds of tiles run unsplit and a last
-  // round at most half full runs with every tile's K range in two halves (twice the blocks, each half as long);
-  // those blocks store fp32 partials at tpart [2][M][N] that tail_reduce_kernel sums into C. xcu = CUs per XCD
-  // (one block per CU: the kernel's LDS and registers admit one)
+  // grouped-M tail split (bf16 out): per XCD, the whole rounds of tiles run unsplit and a last round at most half
+  // full runs with every tile's K range in two halves (twice the blocks, each half as long); those blocks store
+  // fp32 partials at tpart [8 * xcu / 2 slots][2 halves][BM][BN] (slot = XCD x its tail tile) that
+  // tail_reduce_kernel sums into C. xcu = CUs per XCD (one block per CU: the kernel's LDS and registers admit one)
   int tsplit, xcu;
   float* tpart;
 };
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
   // grouped-M grids are sized for the worst case and their tail is spare blocks: the XCD-contiguous remap over the
   // whole grid hands every spare id to the last XCD(s) and leaves them idle (the real tiles are the low ids)
   int id;
-  int thalf = -1;  // tail split: the K half (0 / 1) of a split tail tile this block computes; -1 = the whole tile
+  int thalf = -1;  // tail split: 2 * slot + K half of the split tail tile this block computes; -1 = the whole tile
   if constexpr (MODE == kGroupM) {
     if (p.chunk) {
       // balanced XCD-contiguous order over the REAL tiles (counted from the device offsets): XCD x runs ids
@@ -317,7 +317,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
           id = x * q + k;
         } else if (tp.split && k - tp.full < 2 * tp.tail) {
           id = x * q + tp.full + ((k - tp.full) >> 1);
-          thalf = (k - tp.full) & 1;
+          thalf = (x * (p.xcu / 2) + ((k - tp.full) >> 1)) * 2 + ((k - tp.full) & 1);  // partial slice index
         } else {
           return;  // spare block
         }
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
     }
     if (thalf >= 0) {
       const int ks = ((p.K + 1) / 2 + BK - 1) / BK * BK;
-      k_lo = thalf * ks;
+      k_lo = (thalf & 1) * ks;
       k_hi = min(p.K, k_lo + ks);
     }
     // expert by expert, row tiles fastest (group_tile); m_lo = this block's first row (absolute)
@@ -615,14 +615,14 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
   constexpr bool KSTATS = (MODE == kGroupK || MODE == kGroupKSeg) && EPI != kStoreBf16;
   if constexpr (MODE == kGroupM && EPI == kStoreBf16) {
     if (thalf >= 0) {  // a split tail tile: this K half's fp32 partial, summed into C by tail_reduce_kernel
-      float* T = p.tpart + (int64_t)thalf * p.M * p.N;
+      float* T = p.tpart + (int64_t)thalf * BM * BN;
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi) {
         const int mrow = wr * 128 + 16 * mi + i;
         if (mrow >= rows_valid) continue;
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni)
-          *reinterpret_cast<f32x4*>(T + (int64_t)(m0 + mrow) * p.N + n0 + wc * 64 + 16 * ni + 4 * g) = acc[mi][ni];
+          *reinterpret_cast<f32x4*>(T + mrow * BN + wc * 64 + 16 * ni + 4 * g) = acc[mi][ni];
       }
       return;
     }
@@ -756,14 +756,13 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(GemmArgs p) {
   int grp, tn, m_lo, m_hi;
   if (!group_tile(p, x * q + tp.full + s, grp, tn, m_lo, m_hi)) return;
   const int rows = min(BM, m_hi - m_lo);
-  const int64_t slice = (int64_t)p.M * p.N;
+  const float* T = p.tpart + (int64_t)blockIdx.x * 2 * BM * BN;  // slot x * half + s: [2 halves][BM][BN]
   const int c = (threadIdx.x & 31) * 8;
   bf16* C = reinterpret_cast<bf16*>(p.c);
   for (int r = threadIdx.x >> 5; r < rows; r += 8) {
-    const int64_t o = (int64_t)(m_lo + r) * p.N + tn * BN + c;
-    const f32x4 a0 = *reinterpret_cast<const f32x4*>(p.tpart + o) + *reinterpret_cast<const f32x4*>(p.tpart + slice + o);
-    const f32x4 a1 =
-        *reinterpret_cast<const f32x4*>(p.tpart + o + 4) + *reinterpret_cast<const f32x4*>(p.tpart + slice + o + 4);
+    const int o = r * BN + c;
+    const f32x4 a0 = *reinterpret_cast<const f32x4*>(T + o) + *reinterpret_cast<const f32x4*>(T + BM * BN + o);
+    const f32x4 a1 = *reinterpret_cast<const f32x4*>(T + o + 4) + *reinterpret_cast<const f32x4*>(T + BM * BN + o + 4);
     const f32x8 v = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
     store8f(C + (int64_t)(m_lo + r) * p.ldc + tn * BN + c, v);
   }
@@ -854,14 +853,17 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
   at::Tensor out_final = out;
   // (round 4: splitting K >= 8192 in two and K >= 24576 in three measured 3-7 % slower on the Mixtral shapes than
   // this rule: the fp32 partial traffic outweighs the fuller last round; profiles/gemm_splitk_policy_ab_r04.jsonl)
-  // round 6: the tail split instead -- each XCD runs its whole rounds of tiles unsplit and only a last round at most
-  // half full as K halves (fp32 partials for those tiles alone); DLGM_GEMM_TSPLIT=0 restores the rule above
-  static const bool tsplit_on = [] {
+  // round 6, every grouped-M bf16 launch with K >= 4096: the tail split instead -- each XCD runs its whole rounds of
+  // tiles unsplit and only a last round at most half full as K halves (fp32 partials for those tiles alone, summed
+  // by tail_reduce_kernel): +1.7 % on the Mixtral step for the narrow launches alone
+  // (profiles/gemm_tail_split_ab_r06.json). DLGM_GEMM_TSPLIT=0 restores the rule below
+  static const int tsplit_mode = [] {  // 0 off, 1 every width, 2 narrow launches (<= 16 column tiles) only
     const char* e = std::getenv("DLGM_GEMM_TSPLIT");
-    return !(e != nullptr && e[0] == '0');
+    return e == nullptr ? 1 : std::atoi(e);
   }();
   at::Tensor tpart;
-  if (mode == kGroupM && !out32 && !fused_glu && p.tiles_n <= 16 && K >= 4096 && tsplit_on) {
+  if (mode == kGroupM && !out32 && !fused_glu && K >= 4096 && tsplit_mode != 0 &&
+      (tsplit_mode == 1 || p.tiles_n <= 16)) {
     static int cu_count[64] = {};  // per device, queried once
     int dev = 0;
     DLGM_CHECK_HIP(hipGetDevice(&dev));
@@ -869,7 +871,7 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
     if (cus == 0) DLGM_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     p.tsplit = 1;
     p.xcu = std::max(2, cus / 8);
-    tpart = at::empty({2, M, N}, out.options().dtype(at::kFloat));
+    tpart = at::empty({8 * (p.xcu / 2), 2, BM, BN}, out.options().dtype(at::kFloat));
     p.tpart = tpart.data_ptr<float>();
   }
   if (mode == kGroupM && !out32 && !fused_glu && !p.tsplit && out.is_contiguous() && ldc == N && p.tiles_n <= 16 &&
