@@ -15,6 +15,13 @@ if v == "nowt":
         cfg.expert_weight_cache = False
         orig(self, model_cfg, cfg, *a, **k)
     Z.ZeroEngine.__init__ = init
+elif v == "nohead":  # (round-6 experiment, since removed) the LM head's dW per micro-batch, not once per step
+    orig = Z.ZeroEngine.__init__
+
+    def init(self, model_cfg, cfg, *a, **k):
+        cfg.defer_head_wgrad = False
+        orig(self, model_cfg, cfg, *a, **k)
+    Z.ZeroEngine.__init__ = init
 elif v == "tcmain":  # the per-step W^T rebuild on the compute stream instead of the "tcache" side stream
     from distributed_llm_training_gpu_manager_amd.utils import streams as S
     _side = S.side_stream
