@@ -74,28 +74,42 @@ struct GemmArgs {
   // row stride ldc) and store dgate at column c and dup at column glu_f + c of C ([rows, 2 glu_f])
   const bf16* glu;
   int glu_f;
-  // grouped-M tail split (bf16 out): per XCD, the whole rounds of tiles run unsplit and a last round at most half
-  // full runs with every tile's K range in two halves (twice the blocks, each half as long); those blocks store
-  // fp32 partials at tpart [8 * xcu / 2 slots][2 halves][BM][BN] (slot = XCD x its tail tile) that
-  // tail_reduce_kernel sums into C. xcu = CUs per XCD (one block per CU: the kernel's LDS and registers admit one)
-  int tsplit, xcu;
+  // grouped-M tail split (bf16 out): per XCD, the whole rounds of tiles run unsplit and the short last round's
+  // tiles run with their K range in s parts (s = 2..4 blocks a tile, chosen to fill the CUs best); those blocks
+  // store fp32 partials at tpart [8 XCDs][kMaxSplit * xcu slices][BM][BN] that tail_reduce_kernel sums into C.
+  // xcu = CUs per XCD (one block per CU: the kernel's LDS and registers admit one)
+  int tsplit, xcu, tmax;  // tmax: most K parts per tail tile (2..kMaxSplit)
   float* tpart;
 };
 
-// Per-XCD plan of the tail split: the XCD runs tiles [x q, x q + qx); the first `full` of them unsplit; if
-// `split`, the remaining `tail` tiles as two K halves each.
+constexpr int kMaxSplit = 4;
+
+// Per-XCD plan of the tail split: the XCD runs tiles [x q, x q + qx); the first `full` of them unsplit, then (s > 1)
+// the remaining `tail` tiles as s K parts each. s minimises the last round's length ceil(tail s / xcu) / s tile
+// times (ties: the fewer parts), e.g. with 32 CUs: tail 8 -> 4 parts (1/4), 10 -> 3, 16 -> 2, 20 -> 3 (2/3),
+// 24 -> 4 (3/4), 25.. -> none.
 struct TailPlan {
-  int qx, full, tail;
-  bool split;
+  int qx, full, tail, s;
 };
 
-__device__ __forceinline__ TailPlan tail_plan(int real, int q, int x, int xcu) {
+__device__ __forceinline__ TailPlan tail_plan(int real, int q, int x, int xcu, int tmax) {
   TailPlan t;
   t.qx = max(0, min(q, real - x * q));
   const int whole = t.qx / xcu * xcu;
   t.tail = t.qx - whole;
-  t.split = t.tail > 0 && 2 * t.tail <= xcu;
-  t.full = t.split ? whole : t.qx;
+  t.s = 1;
+  if (t.tail > 0) {
+    int best_num = 1, best_den = 1;  // last-round length as a fraction of a tile time: rounds / s
+    for (int s = 2; s <= tmax; ++s) {
+      const int rounds = (t.tail * s + xcu - 1) / xcu;
+      if (rounds * best_den < best_num * s) {
+        best_num = rounds;
+        best_den = s;
+        t.s = s;
+      }
+    }
+  }
+  t.full = t.s > 1 ? whole : t.qx;
   return t;
 }
 
@@ -303,7 +317,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
   // grouped-M grids are sized for the worst case and their tail is spare blocks: the XCD-contiguous remap over the
   // whole grid hands every spare id to the last XCD(s) and leaves them idle (the real tiles are the low ids)
   int id;
-  int thalf = -1;  // tail split: 2 * slot + K half of the split tail tile this block computes; -1 = the whole tile
+  int tslice = -1, tpi = 0, tparts = 1;  // tail split: partial slice, K part and parts of this block's tile
   if constexpr (MODE == kGroupM) {
     if (p.chunk) {
       // balanced XCD-contiguous order over the REAL tiles (counted from the device offsets): XCD x runs ids
@@ -311,13 +325,16 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
       // contiguous, L2-sharing run of an expert's tiles
       const int real = grouped_real_tiles(p) * p.splitk;
       const int q = (real + 7) / 8, x = blockIdx.x & 7, k = blockIdx.x >> 3;
-      if (p.tsplit) {  // the XCD's whole rounds unsplit, then its short last round as K halves (two blocks a tile)
-        const TailPlan tp = tail_plan(real, q, x, p.xcu);
+      if (p.tsplit) {  // the XCD's whole rounds unsplit, then its short last round as K parts (s blocks a tile)
+        const TailPlan tp = tail_plan(real, q, x, p.xcu, p.tmax);
         if (k < tp.full) {
           id = x * q + k;
-        } else if (tp.split && k - tp.full < 2 * tp.tail) {
-          id = x * q + tp.full + ((k - tp.full) >> 1);
-          thalf = (x * (p.xcu / 2) + ((k - tp.full) >> 1)) * 2 + ((k - tp.full) & 1);  // partial slice index
+        } else if (tp.s > 1 && k - tp.full < tp.s * tp.tail) {
+          const int kk = k - tp.full;
+          id = x * q + tp.full + kk / tp.s;
+          tslice = x * kMaxSplit * p.xcu + kk;  // = the tile's first slice + its part
+          tpi = kk % tp.s;
+          tparts = tp.s;
         } else {
           return;  // spare block
         }
@@ -373,9 +390,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
       k_hi = min(p.K, k_lo + ks);
       split_off = (int64_t)part * p.c_sstride;
     }
-    if (thalf >= 0) {
-      const int ks = ((p.K + 1) / 2 + BK - 1) / BK * BK;
-      k_lo = (thalf & 1) * ks;
+    if (tslice >= 0) {
+      const int ks = ((p.K + tparts - 1) / tparts + BK - 1) / BK * BK;
+      k_lo = min(p.K, tpi * ks);
       k_hi = min(p.K, k_lo + ks);
     }
     // expert by expert, row tiles fastest (group_tile); m_lo = this block's first row (absolute)
@@ -614,8 +631,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_mfma_kernel(GemmArgs p) {
   };
   constexpr bool KSTATS = (MODE == kGroupK || MODE == kGroupKSeg) && EPI != kStoreBf16;
   if constexpr (MODE == kGroupM && EPI == kStoreBf16) {
-    if (thalf >= 0) {  // a split tail tile: this K half's fp32 partial, summed into C by tail_reduce_kernel
-      float* T = p.tpart + (int64_t)thalf * BM * BN;
+    if (tslice >= 0) {  // a split tail tile: this K part's fp32 partial, summed into C by tail_reduce_kernel
+      float* T = p.tpart + (int64_t)tslice * BM * BN;
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi) {
         const int mrow = wr * 128 + 16 * mi + i;
@@ -744,25 +761,27 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 }
 
 
-// C rows / columns of the split tail tiles = tpart[0] + tpart[1] -> bf16. One block per possible split tile
-// (8 XCDs x xcu / 2), which recomputes the kernel's plan from the device offsets; idle when its slot is unused.
+// C rows / columns of the split tail tiles = the sum of their s partial slices -> bf16. One block per possible split
+// tile (8 XCDs x xcu), which recomputes the kernel's plan from the device offsets; idle when its slot is unused.
 __global__ __launch_bounds__(256) void tail_reduce_kernel(GemmArgs p) {
-  const int half = max(1, p.xcu / 2);
-  const int x = blockIdx.x / half, s = blockIdx.x - x * half;
+  const int x = blockIdx.x / p.xcu, s = blockIdx.x - x * p.xcu;
   const int real = grouped_real_tiles(p);
   const int q = (real + 7) / 8;
-  const TailPlan tp = tail_plan(real, q, x, p.xcu);
-  if (!tp.split || s >= tp.tail) return;
+  const TailPlan tp = tail_plan(real, q, x, p.xcu, p.tmax);
+  if (tp.s < 2 || s >= tp.tail) return;
   int grp, tn, m_lo, m_hi;
   if (!group_tile(p, x * q + tp.full + s, grp, tn, m_lo, m_hi)) return;
   const int rows = min(BM, m_hi - m_lo);
-  const float* T = p.tpart + (int64_t)blockIdx.x * 2 * BM * BN;  // slot x * half + s: [2 halves][BM][BN]
+  const float* T = p.tpart + ((int64_t)x * kMaxSplit * p.xcu + (int64_t)s * tp.s) * BM * BN;  // the tile's slices
   const int c = (threadIdx.x & 31) * 8;
   bf16* C = reinterpret_cast<bf16*>(p.c);
   for (int r = threadIdx.x >> 5; r < rows; r += 8) {
     const int o = r * BN + c;
-    const f32x4 a0 = *reinterpret_cast<const f32x4*>(T + o) + *reinterpret_cast<const f32x4*>(T + BM * BN + o);
-    const f32x4 a1 = *reinterpret_cast<const f32x4*>(T + o + 4) + *reinterpret_cast<const f32x4*>(T + BM * BN + o + 4);
+    f32x4 a0 = *reinterpret_cast<const f32x4*>(T + o), a1 = *reinterpret_cast<const f32x4*>(T + o + 4);
+    for (int pt = 1; pt < tp.s; ++pt) {  // fixed order: deterministic
+      a0 += *reinterpret_cast<const f32x4*>(T + (int64_t)pt * BM * BN + o);
+      a1 += *reinterpret_cast<const f32x4*>(T + (int64_t)pt * BM * BN + o + 4);
+    }
     const f32x8 v = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
     store8f(C + (int64_t)(m_lo + r) * p.ldc + tn * BN + c, v);
   }
@@ -854,8 +873,8 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
   // (round 4: splitting K >= 8192 in two and K >= 24576 in three measured 3-7 % slower on the Mixtral shapes than
   // this rule: the fp32 partial traffic outweighs the fuller last round; profiles/gemm_splitk_policy_ab_r04.jsonl)
   // round 6, every grouped-M bf16 launch with K >= 4096: the tail split instead -- each XCD runs its whole rounds of
-  // tiles unsplit and only a last round at most half full as K halves (fp32 partials for those tiles alone, summed
-  // by tail_reduce_kernel): +1.7 % on the Mixtral step for the narrow launches alone
+  // tiles unsplit and only its short last round's tiles as K parts (fp32 partials for those tiles alone, summed
+  // by tail_reduce_kernel): +1.7 % on the Mixtral step with halves for the narrow launches alone
   // (profiles/gemm_tail_split_ab_r06.json). DLGM_GEMM_TSPLIT=0 restores the rule below
   static const int tsplit_mode = [] {  // 0 off, 1 every width, 2 narrow launches (<= 16 column tiles) only
     const char* e = std::getenv("DLGM_GEMM_TSPLIT");
@@ -869,9 +888,14 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
     DLGM_CHECK_HIP(hipGetDevice(&dev));
     int& cus = cu_count[dev & 63];
     if (cus == 0) DLGM_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    static const int tmax = [] {  // DLGM_GEMM_TSPLIT_PARTS: most K parts per tail tile (default and cap 4)
+      const char* e = std::getenv("DLGM_GEMM_TSPLIT_PARTS");
+      return std::min(kMaxSplit, std::max(2, e == nullptr ? kMaxSplit : std::atoi(e)));
+    }();
     p.tsplit = 1;
+    p.tmax = tmax;
     p.xcu = std::max(2, cus / 8);
-    tpart = at::empty({8 * (p.xcu / 2), 2, BM, BN}, out.options().dtype(at::kFloat));
+    tpart = at::empty({8 * kMaxSplit * p.xcu, BM, BN}, out.options().dtype(at::kFloat));
     p.tpart = tpart.data_ptr<float>();
   }
   if (mode == kGroupM && !out32 && !fused_glu && !p.tsplit && out.is_contiguous() && ldc == N && p.tiles_n <= 16 &&
@@ -893,7 +917,7 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
     p.offsets = offsets->data_ptr<int>();
     if (mode == kGroupM) {
       nblk = ((M + BM - 1) / BM + G) * p.tiles_n * p.splitk;  // M = total rows: worst-case tiles over all groups
-      if (p.tsplit) nblk += 8 * (p.xcu / 2);  // an XCD's split tail takes up to xcu / 2 more blocks
+      if (p.tsplit) nblk += 8 * (kMaxSplit - 1) * p.xcu;  // an XCD's split tail: up to (s - 1) tail more blocks
       nblk = (nblk + 7) / 8 * 8;  // whole rounds of the 8 XCDs (the balanced remap's block -> XCD mapping)
     } else {
       nblk = G * (int64_t)p.tiles_m * p.tiles_n;
@@ -932,7 +956,7 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
   }
   DLGM_CHECK_HIP(hipGetLastError());
   if (p.tsplit) {
-    tail_reduce_kernel<<<8 * (p.xcu / 2), 256, 0, st>>>(p);
+    tail_reduce_kernel<<<8 * p.xcu, 256, 0, st>>>(p);
     DLGM_CHECK_HIP(hipGetLastError());
   }
   if (p.splitk > 1) {

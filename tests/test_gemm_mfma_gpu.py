@@ -119,7 +119,7 @@ def test_grouped_dx_fused_swiglu_bwd_matches_unfused(transpose_w, monkeypatch):
 @pytest.mark.parametrize("transpose_w", [True, False])
 def test_grouped_rows_narrow_long_k_split_k(transpose_w):
     """Narrow output (<= 16 column tiles) with a long K: 32 tiles, i.e. a single short round on every XCD, so the
-    tail split runs every tile as two K halves (fp32 partials + the tail reduce); uneven / empty / single-row
+    tail split runs every tile as four K parts (fp32 partials + the tail reduce); uneven / empty / single-row
     groups; also the balanced XCD remap over the real tiles."""
     g = torch.Generator(device=dev).manual_seed(7)
     sizes = [700, 0, 1, 513, 1300, 77, 256, 33]
@@ -138,14 +138,15 @@ def test_grouped_rows_narrow_long_k_split_k(transpose_w):
 
 
 @pytest.mark.parametrize("sizes,N", [
-    ([1500, 0, 1, 2100, 700, 1800, 1200, 891], 4096),     # 36 row tiles x 16 = 576: 72 per XCD -> 2 rounds + 8 split
-    ([2560, 2561, 0, 2048, 1280, 1287, 768, 100], 4096),  # 44 row tiles: 88 per XCD -> a tail of 24, unsplit
-    ([1500, 0, 1, 2100, 700, 1800, 1200, 891], 6144),     # 36 x 24 = 864: 108 per XCD -> 3 rounds + 12 split
+    ([1500, 0, 1, 2100, 700, 1800, 1200, 891], 4096),     # 36 row tiles x 16 = 576: 72 per XCD -> 2 rounds + 8 in 4 parts
+    ([2560, 2561, 0, 2048, 1280, 1287, 768, 100], 4096),  # 44 row tiles: 88 per XCD -> a tail of 24 in 4 parts
+    ([2560, 2561, 0, 2048, 1280, 1287, 768, 356], 4096),  # 45 row tiles: 90 per XCD -> a tail of 26, unsplit
+    ([1500, 0, 1, 2100, 700, 1800, 1200, 891], 6144),     # 36 x 24 = 864: 108 per XCD -> 3 rounds + 12 in halves
 ])
 @pytest.mark.parametrize("transpose_w", [True, False])
 def test_grouped_rows_tail_split(sizes, N, transpose_w):
     """Grouped-M launches at the Mixtral down-projection shape (N = 4096, K = 4096) and a wider one: each XCD's whole
-    rounds of tiles store bf16 directly, a last round at most half full runs as K halves whose fp32 partials the
+    rounds of tiles store bf16 directly, its short last round runs as 2-4 K parts per tile whose fp32 partials the
     tail reduce sums (the tiles on both sides of that split, partial row tiles and an empty group included)."""
     g = torch.Generator(device=dev).manual_seed(13)
     R, K, G = sum(sizes), 4096, len(sizes)
