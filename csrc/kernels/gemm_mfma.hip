@@ -881,6 +881,8 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
     return e == nullptr ? 1 : std::atoi(e);
   }();
   at::Tensor tpart;
+  // (not on the fused SwiGLU-backward launch: with the SwiGLU backward in tail_reduce_kernel that launch measured
+  // 1.3 % slower on the Mixtral step, profiles/gemm_tail_split_ab_r06.json glu_tail_split)
   if (mode == kGroupM && !out32 && !fused_glu && K >= 4096 && tsplit_mode != 0 &&
       (tsplit_mode == 1 || p.tiles_n <= 16)) {
     static int cu_count[64] = {};  // per device, queried once
