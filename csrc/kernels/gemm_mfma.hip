@@ -79,6 +79,7 @@ struct GemmArgs {
   // store fp32 partials at tpart [8 XCDs][kMaxSplit * xcu slices][BM][BN] that tail_reduce_kernel sums into C.
   // xcu = CUs per XCD (one block per CU: the kernel's LDS and registers admit one)
   int tsplit, xcu, tmax;  // tmax: most K parts per tail tile (2..kMaxSplit)
+  int tbands;             // tail_reduce_kernel blocks per tile (row bands of BM / tbands rows)
   float* tpart;
 };
 
@@ -761,10 +762,11 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 }
 
 
-// C rows / columns of the split tail tiles = the sum of their s partial slices -> bf16. One block per possible split
-// tile (8 XCDs x xcu), which recomputes the kernel's plan from the device offsets; idle when its slot is unused.
+// C rows / columns of the split tail tiles = the sum of their s partial slices -> bf16. tbands blocks (row bands) per
+// possible split tile (8 XCDs x xcu), each recomputing the kernel's plan from the device offsets; idle when unused.
 __global__ __launch_bounds__(256) void tail_reduce_kernel(GemmArgs p) {
-  const int x = blockIdx.x / p.xcu, s = blockIdx.x - x * p.xcu;
+  const int band = blockIdx.x % p.tbands, slot = blockIdx.x / p.tbands;  // a row band of one tile
+  const int x = slot / p.xcu, s = slot - x * p.xcu;
   const int real = grouped_real_tiles(p);
   const int q = (real + 7) / 8;
   const TailPlan tp = tail_plan(real, q, x, p.xcu, p.tmax);
@@ -775,7 +777,8 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(GemmArgs p) {
   const float* T = p.tpart + ((int64_t)x * kMaxSplit * p.xcu + (int64_t)s * tp.s) * BM * BN;  // the tile's slices
   const int c = (threadIdx.x & 31) * 8;
   bf16* C = reinterpret_cast<bf16*>(p.c);
-  for (int r = threadIdx.x >> 5; r < rows; r += 8) {
+  const int rb = BM / p.tbands, r_end = min(rows, (band + 1) * rb);
+  for (int r = band * rb + (threadIdx.x >> 5); r < r_end; r += 8) {
     const int o = r * BN + c;
     f32x4 a0 = *reinterpret_cast<const f32x4*>(T + o), a1 = *reinterpret_cast<const f32x4*>(T + o + 4);
     for (int pt = 1; pt < tp.s; ++pt) {  // fixed order: deterministic
@@ -894,8 +897,14 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
       const char* e = std::getenv("DLGM_GEMM_TSPLIT_PARTS");
       return std::min(kMaxSplit, std::max(2, e == nullptr ? kMaxSplit : std::atoi(e)));
     }();
+    static const int tbands = [] {  // DLGM_GEMM_TRED_BANDS: reduce blocks per tile (1..32, a divisor of 256)
+      const char* e = std::getenv("DLGM_GEMM_TRED_BANDS");
+      const int v = e == nullptr ? 8 : std::atoi(e);
+      return (v >= 1 && v <= 32 && 256 % v == 0) ? v : 8;
+    }();
     p.tsplit = 1;
     p.tmax = tmax;
+    p.tbands = tbands;
     p.xcu = std::max(2, cus / 8);
     tpart = at::empty({8 * kMaxSplit * p.xcu, BM, BN}, out.options().dtype(at::kFloat));
     p.tpart = tpart.data_ptr<float>();
@@ -958,7 +967,7 @@ void dlgm_gemm_mfma(at::Tensor out, const at::Tensor& a, const at::Tensor& b, bo
   }
   DLGM_CHECK_HIP(hipGetLastError());
   if (p.tsplit) {
-    tail_reduce_kernel<<<8 * p.xcu, 256, 0, st>>>(p);
+    tail_reduce_kernel<<<8 * p.xcu * p.tbands, 256, 0, st>>>(p);
     DLGM_CHECK_HIP(hipGetLastError());
   }
   if (p.splitk > 1) {
