@@ -30,4 +30,6 @@ import bench  # noqa: E402
 
 sys.argv = ["bench.py", "--model", "mixtral-8x7b", "--n-layers", "2", "--seq", "4096", "--ga", "4", "--steps", "15",
             "--warmup", "3", "--no-telemetry"]
+if v == "ovl":  # per-group AdamW on the optimizer stream beside the next step's forward
+    sys.argv += ["--optimizer-overlap", "on"]
 sys.exit(bench.main())
