@@ -27,7 +27,9 @@
 // The XOR swizzles are applied to the DMA's per-lane SOURCE address (the DMA writes lane-linearly)
 // and to the reads. The MFMA computes D^T = B^T A^T so each lane ends up holding 4 consecutive
 // columns of one row of C: the epilogue moves 16-byte float4 (fp32) / 8-byte bf16x4 vectors.
-// Work order: blocks are remapped so consecutive tiles (sharing an A row panel) land on one XCD.
+// Work order: blocks are remapped so consecutive tiles (sharing an A row panel) land on one XCD. Grouped-M launches
+// with K >= 4096 run each XCD's whole rounds of tiles as usual and its short last round as 2-4 K parts per tile
+// (fp32 partials + tail_reduce_kernel), so the last round is not left mostly idle (tail_plan).
 #include <torch/all.h>
 #include <c10/hip/HIPStream.h>
 #include <cstdlib>
