@@ -164,6 +164,20 @@ def test_grouped_rows_tail_split(sizes, N, transpose_w):
         lo += n
 
 
+def test_grouped_rows_tail_split_is_deterministic():
+    """The tail split's partials are summed in a fixed order: two launches over the same operands and routing are
+    bit-identical (the engine's bit-identity checks rely on it)."""
+    g = torch.Generator(device=dev).manual_seed(21)
+    sizes = [1500, 0, 1, 2100, 700, 1800, 1200, 891]  # a tail of 8 tiles per XCD in 4 K parts
+    R, K, N, G = sum(sizes), 4096, 4096, len(sizes)
+    offs = torch.tensor([0] + list(torch.tensor(sizes).cumsum(0)), dtype=torch.int32, device=dev)
+    x = torch.randn(R, K, device=dev, generator=g).to(torch.bfloat16)
+    w = torch.randn(G, N, K, device=dev, generator=g).to(torch.bfloat16)
+    a = gm.grouped_mm(x, w, offs)
+    b = gm.grouped_mm(x, w, offs)
+    assert torch.equal(a.view(torch.int16), b.view(torch.int16))
+
+
 def test_grouped_weight_gradient_uneven_and_empty_groups():
     g = torch.Generator(device=dev).manual_seed(3)
     sizes = [130, 0, 700, 1]
